@@ -1,0 +1,343 @@
+// `stripe` - native command-line driver.
+//
+// The reference has no CLI: argc/argv only reach MPI_Init; input path, output
+// path, filter chain and parameters are hard-coded (kernel.cu:96,104,110,195,236;
+// kern.cpp:17,33,92) and it is launched by an external `mpiexec -n N`.  Here one
+// process drives N ranks (one host thread per rank, one GPU per rank over RCCL,
+// or N logical ranks on fewer GPUs / on the CPU), all parameters are flags:
+//
+//   stripe run   --input in.ppm --output out.ppm --chain gray:ref,contrast:3.5,emboss3
+//                [--preset ref-gpu|ref-cpu] [--ranks N] [--backend rccl|local|host]
+//                [--devices 0,1,..] [--border reflect101|replicate|constant|skip]
+//                [--no-halo] [--expand-gray] [--legacy-partition] [--iterations K]
+//                [--no-fuse] [--no-overlap] [--verbose]
+//   stripe bench --synthetic 16384x16384x3 --seed 1 --chain gaussian5 --ranks 1,2,4,8
+//                --iters 20 --warmup 5 --scope resident,dist [--backend rccl|local]
+//                [--json out.json]
+//   stripe cmp   a.ppm b.ppm [--tol 0]
+//   stripe gen   --synthetic WxHxC --seed S --output x.ppm
+//   stripe info  [--chain ...] [--channels C]
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <map>
+#include <mutex>
+#include <thread>
+
+#include "stripe/engine.h"
+
+using namespace stripe;
+
+namespace {
+
+struct Args {
+  std::string cmd;
+  std::map<std::string, std::string> kv;
+  std::vector<std::string> pos;
+  bool has(const std::string& k) const { return kv.count(k) > 0; }
+  std::string get(const std::string& k, const std::string& d = "") const {
+    auto it = kv.find(k);
+    return it == kv.end() ? d : it->second;
+  }
+  int geti(const std::string& k, int d) const { return has(k) ? std::stoi(get(k)) : d; }
+};
+
+const std::vector<std::string> kFlags = {"no-halo", "expand-gray", "legacy-partition", "no-fuse",
+                                         "no-overlap", "verbose", "help"};
+
+Args parse_args(int argc, char** argv) {
+  Args a;
+  if (argc < 2) return a;
+  a.cmd = argv[1];
+  for (int i = 2; i < argc; ++i) {
+    std::string s = argv[i];
+    if (s.rfind("--", 0) == 0) {
+      std::string k = s.substr(2);
+      auto eq = k.find('=');
+      if (eq != std::string::npos) {
+        a.kv[k.substr(0, eq)] = k.substr(eq + 1);
+      } else if (std::find(kFlags.begin(), kFlags.end(), k) != kFlags.end()) {
+        a.kv[k] = "1";
+      } else {
+        STRIPE_CHECK(i + 1 < argc, "flag --" << k << " needs a value");
+        a.kv[k] = argv[++i];
+      }
+    } else {
+      a.pos.push_back(s);
+    }
+  }
+  return a;
+}
+
+std::vector<int> parse_int_list(const std::string& s) {
+  std::vector<int> v;
+  std::string cur;
+  for (char c : s + ",") {
+    if (c == ',') {
+      if (!cur.empty()) v.push_back(std::stoi(cur));
+      cur.clear();
+    } else {
+      cur.push_back(c);
+    }
+  }
+  return v;
+}
+
+void parse_shape(const std::string& s, int* W, int* H, int* C) {
+  *C = 3;
+  int n = std::sscanf(s.c_str(), "%dx%dx%d", W, H, C);
+  STRIPE_CHECK(n >= 2, "shape must be WxH or WxHxC, got '" << s << "'");
+}
+
+int device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+EngineConfig config_from(const Args& a, int W, int H, int C) {
+  EngineConfig cfg;
+  cfg.W = W;
+  cfg.H = H;
+  cfg.C = C;
+  cfg.chain = a.get("chain", "gaussian5");
+  const std::string preset = a.get("preset");
+  if (preset == "ref-gpu") {
+    // kernel.cu: gray(ref) -> contrast 3.5 -> emboss3, stripes independent, legacy
+    // split, 3-channel output (GRAY2BGR, kernel.cu:210)
+    cfg.chain = "gray:ref,contrast:3.5,emboss3@skip,expand";
+    cfg.halo = false;
+    cfg.legacy_partition = true;
+  } else if (preset == "ref-cpu") {
+    cfg.chain = "gray:bt601,contrast:3:cv,emboss3,expand";  // kern.cpp
+    cfg.halo = false;
+    cfg.legacy_partition = true;
+  } else if (!preset.empty()) {
+    fail("unknown preset '" + preset + "' (ref-gpu|ref-cpu)");
+  }
+  if (a.has("border")) cfg.border = parse_border(a.get("border"));
+  if (a.has("no-halo")) cfg.halo = false;
+  if (a.has("legacy-partition")) cfg.legacy_partition = true;
+  if (a.has("no-fuse")) cfg.fuse = false;
+  if (a.has("no-overlap")) cfg.overlap = false;
+  if (a.has("expand-gray") && cfg.chain.find("expand") == std::string::npos) cfg.chain += ",expand";
+  cfg.band = a.geti("band", 0);
+  const std::string be = a.get("backend", device_count() > 0 ? "local" : "host");
+  cfg.backend = be == "host" ? BackendKind::Host : BackendKind::Device;
+  return cfg;
+}
+
+// Communicators + devices for N ranks of the chosen backend.
+struct Group {
+  std::vector<std::unique_ptr<Comm>> owned;
+  std::vector<Comm*> comms;
+  std::vector<int> devices;
+};
+
+Group make_group(const std::string& backend, int N, const std::vector<int>& devlist) {
+  Group g;
+  const int ndev = device_count();
+  std::vector<int> devs = devlist;
+  if (devs.empty())
+    for (int r = 0; r < N; ++r) devs.push_back(ndev > 0 ? r % ndev : 0);
+  STRIPE_CHECK((int)devs.size() >= N, "need " << N << " devices, got " << devs.size());
+  devs.resize(N);
+  if (backend == "rccl") {
+    STRIPE_CHECK(ndev >= N, "rccl backend needs one GPU per rank (" << N << " ranks, " << ndev << " GPUs)");
+    g.owned = make_rccl_comms_all(devs);
+  } else {
+    auto hub = make_local_hub(N, backend != "host");
+    for (int r = 0; r < N; ++r) g.owned.push_back(make_local_comm(hub, r));
+  }
+  for (auto& c : g.owned) g.comms.push_back(c.get());
+  if (backend != "host") g.devices = devs;
+  return g;
+}
+
+int cmd_run(const Args& a) {
+  STRIPE_CHECK(a.has("input") && a.has("output"), "run needs --input and --output");
+  Image img = read_pnm(a.get("input"));
+  EngineConfig cfg = config_from(a, img.W, img.H, img.C);
+  const int N = a.geti("ranks", 1);
+  const std::string backend = a.get("backend", cfg.backend == BackendKind::Host ? "host" : "local");
+  const int iters = a.geti("iterations", 1);
+  if (a.has("verbose")) {
+    std::cerr << compile_chain(parse_chain(cfg.chain), cfg.C, cfg.border, cfg.fuse).describe();
+    std::cerr << plan_rows(cfg.H, N, 1, cfg.legacy_partition).describe() << "\n";
+  }
+  Group g = make_group(backend, N, parse_int_list(a.get("devices")));
+  PhaseTimes t;
+  const auto t0 = std::chrono::steady_clock::now();
+  Image out = run_group(cfg, g.comms, g.devices, img, iters, &t);
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  write_pnm(a.get("output"), out);
+  std::printf("{\"cmd\":\"run\",\"W\":%d,\"H\":%d,\"C\":%d,\"ranks\":%d,\"backend\":\"%s\",\"chain\":\"%s\","
+              "\"wall_ms\":%.3f,\"kernel_ms\":%.4f}\n",
+              img.W, img.H, img.C, N, backend.c_str(), cfg.chain.c_str(), ms, t.run);
+  return 0;
+}
+
+int cmd_cmp(const Args& a) {
+  STRIPE_CHECK(a.pos.size() == 2, "cmp needs two files");
+  Image x = read_pnm(a.pos[0]), y = read_pnm(a.pos[1]);
+  CmpResult r = compare_images(x, y);
+  const int tol = a.geti("tol", 0);
+  if (!r.same_shape) {
+    std::printf("{\"same_shape\":false}\n");
+    return 2;
+  }
+  std::printf("{\"same_shape\":true,\"max_abs\":%d,\"n_diff\":%lld,\"psnr\":%.3f}\n", r.max_abs, (long long)r.n_diff,
+              r.psnr);
+  return r.max_abs <= tol ? 0 : 1;
+}
+
+int cmd_gen(const Args& a) {
+  int W, H, C;
+  parse_shape(a.get("synthetic", "512x512x3"), &W, &H, &C);
+  Image img = synth_image((uint64_t)std::stoull(a.get("seed", "1")), W, H, C);
+  STRIPE_CHECK(a.has("output"), "gen needs --output");
+  write_pnm(a.get("output"), img);
+  return 0;
+}
+
+int cmd_info(const Args& a) {
+  const int n = device_count();
+  std::printf("devices: %d\n", n);
+  for (int d = 0; d < n; ++d) {
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, d) == hipSuccess)
+      std::printf("  [%d] %s %s CUs=%d HBM=%.1f GB\n", d, p.name, p.gcnArchName, p.multiProcessorCount,
+                  p.totalGlobalMem / 1e9);
+  }
+  std::printf("rccl: %s\n", n > 0 ? rccl_version().c_str() : "n/a");
+  if (a.has("chain"))
+    std::printf("%s", compile_chain(parse_chain(a.get("chain")), a.geti("channels", 3),
+                                    parse_border(a.get("border", "reflect101")), !a.has("no-fuse"))
+                          .describe()
+                          .c_str());
+  return 0;
+}
+
+// ---- bench ----
+struct BenchResult {
+  double ms_per_iter = 0;
+};
+
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int cmd_bench(const Args& a) {
+  int W, H, C;
+  parse_shape(a.get("synthetic", "16384x16384x3"), &W, &H, &C);
+  EngineConfig cfg = config_from(a, W, H, C);
+  const uint64_t seed = std::stoull(a.get("seed", "1"));
+  const int iters = a.geti("iters", 20), warmup = a.geti("warmup", 5);
+  const std::vector<int> ranks = parse_int_list(a.get("ranks", "1"));
+  const std::string backend = a.get("backend", cfg.backend == BackendKind::Host ? "host" : "local");
+  std::string scopes = a.get("scope", "resident");
+  std::vector<std::string> results;
+  Image full;  // only for dist scope
+  if (scopes.find("dist") != std::string::npos) full = synth_image(seed, W, H, C);
+  for (int N : ranks) {
+    Group g = make_group(backend, N, parse_int_list(a.get("devices")));
+    for (const std::string scope : {"resident", "dist"}) {
+      if (scopes.find(scope) == std::string::npos) continue;
+      std::vector<double> per_rank(N, 0);
+      std::mutex mu;
+      std::exception_ptr err;
+      auto body = [&](int r) {
+        try {
+          EngineConfig c = cfg;
+          c.root_buffers = scope == "dist";
+          if (!g.devices.empty()) c.device = g.devices[r];
+          Engine e(c, g.comms[r]);
+          if (scope == "dist") {
+            if (r == 0) e.load_root(full.data.data(), false);
+          } else {
+            e.load_synthetic(seed);
+          }
+          e.synchronize();
+          auto step = [&]() {
+            if (scope == "dist") {
+              e.scatter();
+              e.run(1);
+              e.gather();
+            } else {
+              e.run(1);
+            }
+          };
+          for (int i = 0; i < warmup; ++i) step();
+          e.synchronize();
+          g.comms[r]->barrier();
+          const double t0 = now_ms();
+          for (int i = 0; i < iters; ++i) step();
+          e.synchronize();
+          g.comms[r]->barrier();
+          const double t1 = now_ms();
+          std::lock_guard<std::mutex> lk(mu);
+          per_rank[r] = (t1 - t0) / iters;
+        } catch (...) {
+          std::lock_guard<std::mutex> lk(mu);
+          if (!err) err = std::current_exception();
+          g.comms[r]->abort("bench rank failed");
+        }
+      };
+      std::vector<std::thread> th;
+      for (int r = 0; r < N; ++r) th.emplace_back(body, r);
+      for (auto& t : th) t.join();
+      if (err) std::rethrow_exception(err);
+      double ms = 0;
+      for (double v : per_rank) ms = std::max(ms, v);
+      const double mpx = (double)W * H / (ms * 1e-3) / 1e6;
+      char buf[512];
+      std::snprintf(buf, sizeof buf,
+                    "{\"metric\":\"Mpixels/s\",\"scope\":\"%s\",\"value\":%.1f,\"ms_per_iter\":%.4f,\"n_ranks\":%d,"
+                    "\"backend\":\"%s\",\"chain\":\"%s\",\"W\":%d,\"H\":%d,\"C\":%d,\"iters\":%d,\"warmup\":%d}",
+                    scope.c_str(), mpx, ms, N, backend.c_str(), cfg.chain.c_str(), W, H, C, iters, warmup);
+      std::printf("%s\n", buf);
+      std::fflush(stdout);
+      results.push_back(buf);
+    }
+  }
+  if (a.has("json")) {
+    std::ofstream f(a.get("json"));
+    for (auto& r : results) f << r << "\n";
+  }
+  return 0;
+}
+
+void usage() {
+  std::fprintf(stderr,
+               "usage: stripe <run|bench|cmp|gen|info> [options]\n"
+               "  run   --input in.ppm --output out.ppm [--chain C | --preset ref-gpu|ref-cpu] [--ranks N]\n"
+               "        [--backend rccl|local|host] [--devices 0,1,..] [--border MODE] [--no-halo]\n"
+               "        [--expand-gray] [--legacy-partition] [--iterations K] [--no-fuse] [--no-overlap]\n"
+               "  bench --synthetic WxHxC [--seed S] [--chain C] [--ranks 1,2,4,8] [--iters N] [--warmup N]\n"
+               "        [--scope resident,dist] [--backend rccl|local|host] [--json out.json]\n"
+               "  cmp   a.ppm b.ppm [--tol T]\n"
+               "  gen   --synthetic WxHxC [--seed S] --output out.ppm\n"
+               "  info  [--chain C] [--channels C]\n");
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  Args a = parse_args(argc, argv);
+  try {
+    if (a.cmd == "run") return cmd_run(a);
+    if (a.cmd == "bench") return cmd_bench(a);
+    if (a.cmd == "cmp") return cmd_cmp(a);
+    if (a.cmd == "gen") return cmd_gen(a);
+    if (a.cmd == "info") return cmd_info(a);
+    usage();
+    return a.cmd.empty() || a.cmd == "help" || a.cmd == "--help" ? 0 : 2;
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "stripe: error: %s\n", e.what());
+    return 1;
+  }
+}

@@ -1,0 +1,231 @@
+// Chain compiler: parse -> fuse pointwise runs -> passes with halo/margin contracts.
+#include "stripe/chain.h"
+
+#include <algorithm>
+#include <sstream>
+
+namespace stripe {
+
+uint8_t PointwiseProgram::apply_channel_lut(uint8_t v) const {
+  if (has_pre) v = pre[v];
+  if (has_post) v = post[v];
+  return v;
+}
+
+GrayParams gray_params(GrayMode m) {
+  GrayParams gp;
+  if (m == GrayMode::Ref) {
+    gp.mode = 1;
+    const double w[3] = {0.3, 0.59, 0.11};  // R, G, B (kernel.cu:40-42)
+    for (int c = 0; c < 3; ++c) {
+      bool ok = find_trunc_magic(w[c], &gp.mult[c], &gp.shift[c]);
+      STRIPE_CHECK(ok, "no exact integer form for trunc(x*" << w[c] << ")");
+    }
+  } else {
+    gp.mode = 0;
+    gp.mult[0] = 4899;
+    gp.mult[1] = 9617;
+    gp.mult[2] = 1868;
+    gp.shift[0] = gp.shift[1] = gp.shift[2] = 14;
+  }
+  return gp;
+}
+
+namespace {
+
+std::array<uint8_t, 256> identity_lut() {
+  std::array<uint8_t, 256> l{};
+  for (int i = 0; i < 256; ++i) l[i] = (uint8_t)i;
+  return l;
+}
+
+// Fold a per-channel LUT op into `prog` at its current position.
+void fold_lut(PointwiseProgram& prog, const Op& op) {
+  if (!prog.gray) {
+    if (!prog.has_pre) {
+      prog.pre = identity_lut();
+      prog.has_pre = true;
+    }
+    for (auto& v : prog.pre) v = apply_pointwise_u8(op, v);
+  } else {
+    if (!prog.has_post) {
+      prog.post = identity_lut();
+      prog.has_post = true;
+    }
+    for (auto& v : prog.post) v = apply_pointwise_u8(op, v);
+  }
+}
+
+// Without a gray stage pre and post are one per-channel LUT: keep it in `post`.
+void normalize(PointwiseProgram& prog) {
+  if (!prog.gray && prog.has_pre) {
+    std::array<uint8_t, 256> l{};
+    for (int i = 0; i < 256; ++i) l[i] = prog.has_post ? prog.post[prog.pre[i]] : prog.pre[i];
+    prog.post = l;
+    prog.has_post = true;
+    prog.has_pre = false;
+  }
+  auto is_id = [](const std::array<uint8_t, 256>& l) {
+    for (int i = 0; i < 256; ++i)
+      if (l[i] != i) return false;
+    return true;
+  };
+  if (prog.has_post && is_id(prog.post)) prog.has_post = false;
+  if (prog.has_pre && is_id(prog.pre)) prog.has_pre = false;
+}
+
+std::string prog_desc(const PointwiseProgram& p) {
+  std::string s;
+  if (p.has_pre) s += "lut,";
+  if (p.gray) s += p.gmode == GrayMode::Ref ? "gray:ref," : "gray:bt601,";
+  if (p.has_post) s += "lut,";
+  if (p.expand) s += "expand,";
+  if (!s.empty()) s.pop_back();
+  return s;
+}
+
+}  // namespace
+
+std::string Plan::describe() const {
+  std::ostringstream os;
+  os << "chain '" << spec << "': " << cin << "ch -> " << cout << "ch, " << passes.size()
+     << " pass(es), max radius " << max_radius << "\n";
+  for (size_t i = 0; i < passes.size(); ++i) os << "  pass " << i << ": " << passes[i].desc << "\n";
+  return os.str();
+}
+
+Plan compile_chain(const std::vector<Op>& ops, int cin, Border default_border, bool fuse) {
+  STRIPE_CHECK(cin == 1 || cin == 3, "input must have 1 or 3 channels, got " << cin);
+  Plan plan;
+  plan.spec = chain_to_string(ops);
+  plan.cin = cin;
+  int c = cin;
+  PointwiseProgram pending;
+  int pending_cin = c;
+
+  auto flush_pointwise = [&]() {
+    normalize(pending);
+    if (!pending.identity()) {
+      Pass p;
+      p.kind = PassKind::Pointwise;
+      p.cin = pending_cin;
+      p.cout = pending.channels_out(pending_cin);
+      p.cmid = p.cout;
+      p.pro = pending;
+      p.desc = "pointwise[" + prog_desc(pending) + "] " + std::to_string(p.cin) + "->" +
+               std::to_string(p.cout) + "ch";
+      plan.passes.push_back(p);
+    }
+    pending = PointwiseProgram{};
+    pending_cin = c;
+  };
+
+  for (const Op& op : ops) {
+    if (op.pointwise()) {
+      switch (op.kind) {
+        case OpKind::Gray:
+          if (c == 1) break;  // gray of gray is the identity
+          if (pending.expand || (!fuse && !pending.identity())) flush_pointwise();
+          pending.gray = true;
+          pending.gmode = op.gray;
+          c = 1;
+          break;
+        case OpKind::Expand:
+          STRIPE_CHECK(c == 1, "expand needs a 1-channel image (after gray)");
+          if (!fuse && !pending.identity()) flush_pointwise();
+          pending.expand = true;
+          c = 3;
+          break;
+        default:
+          // a LUT after expand equals the same LUT before it (channels are copies)
+          if (!fuse && !pending.identity()) flush_pointwise();
+          fold_lut(pending, op);
+          break;
+      }
+      continue;
+    }
+    // stencil / conv
+    Pass p;
+    p.border = op.has_border ? op.border : default_border;
+    normalize(pending);
+    const bool conv = op.kind == OpKind::Conv;
+    if (conv || !fuse || !pending.prologue_ok()) flush_pointwise();
+    if (conv) {
+      STRIPE_CHECK(p.border != Border::Skip, "skip border is only defined for integer stencils");
+      p.kind = PassKind::Conv;
+      p.K = op.K;
+      p.R = op.K / 2;
+      p.conv_w = op.weights;
+      p.cin = p.cmid = p.cout = c;
+      p.desc = "conv" + std::to_string(op.K) + "x" + std::to_string(op.K) + "(mfma) " +
+               std::to_string(c) + "ch border=" + border_name(p.border);
+    } else {
+      const StencilInfo& si = stencil_info(op.sid);
+      p.kind = si.separable ? PassKind::Separable : PassKind::Direct;
+      p.sid = op.sid;
+      p.K = si.K;
+      p.R = si.K / 2;
+      p.cin = pending_cin;
+      p.pro = pending;
+      p.cmid = p.cout = c;
+      std::string pro = prog_desc(pending);
+      p.desc = std::string(si.separable ? "separable " : "direct ") + si.name +
+               (pro.empty() ? "" : " prologue[" + pro + "]") + " " + std::to_string(p.cin) +
+               "->" + std::to_string(p.cout) + "ch border=" + border_name(p.border);
+    }
+    plan.passes.push_back(p);
+    pending = PointwiseProgram{};
+    pending_cin = c;
+  }
+  // trailing pointwise ops: epilogue of the last stencil if LUT-only, else own pass
+  normalize(pending);
+  if (!pending.identity()) {
+    if (fuse && !plan.passes.empty() && pending.lut_only() &&
+        (plan.passes.back().kind == PassKind::Separable || plan.passes.back().kind == PassKind::Direct) &&
+        !plan.passes.back().has_epi) {
+      Pass& last = plan.passes.back();
+      last.has_epi = true;
+      last.epi = pending.post;
+      last.desc += " epilogue[lut]";
+      pending = PointwiseProgram{};
+    } else {
+      flush_pointwise();
+    }
+  }
+  if (plan.passes.empty()) {  // identity chain: keep one copy pass so outputs are fresh
+    Pass p;
+    p.kind = PassKind::Pointwise;
+    p.cin = p.cout = p.cmid = c;
+    p.desc = "pointwise[copy]";
+    plan.passes.push_back(p);
+  }
+  plan.cout = c;
+
+  // halo/margin contracts: each pass's output margins serve the next stencil consumer
+  int next_r = 0;
+  Border next_b = Border::Reflect101;
+  for (int i = (int)plan.passes.size() - 1; i >= 0; --i) {
+    Pass& p = plan.passes[i];
+    p.out_margin_px = next_r;
+    p.out_margin_border = next_b;
+    if (p.kind != PassKind::Pointwise) {
+      next_r = p.R;
+      next_b = p.border == Border::Skip ? Border::Reflect101 : p.border;
+    }
+  }
+  plan.in_margin_px = next_r;
+  plan.in_margin_border = next_b;
+  plan.max_radius = 0;
+  plan.max_channels = cin;
+  for (const Pass& p : plan.passes) {
+    plan.max_radius = std::max(plan.max_radius, p.R);
+    plan.max_channels = std::max(plan.max_channels, std::max(p.cin, p.cout));
+  }
+  // a pointwise pass cannot move a margin across a channel change: 3->1 keeps
+  // margins valid (per pixel), and every C stores >= kMaxRadius... check it.
+  for (const Pass& p : plan.passes)
+    STRIPE_CHECK(p.out_margin_px <= margin_pixels(p.cout), "margin contract too wide");
+  return plan;
+}
+
+}  // namespace stripe

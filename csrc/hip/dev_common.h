@@ -1,0 +1,159 @@
+// Device helpers shared by the stripe kernels (gfx950, wave64).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "stripe/common.h"
+
+namespace stripe {
+namespace dev {
+
+constexpr int kNT = 256;  // threads per workgroup (4 waves)
+
+// Kernel argument block (by value, scalar registers).
+struct KArgs {
+  const uint8_t* in;
+  uint8_t* out;
+  const uint8_t* luts;      // [pre | post | epi] 256 B each
+  const uint8_t* zero_row;  // origin of a zero row (Constant y-border)
+  int64_t in_pitch, out_pitch;
+  int W;          // pixels
+  int E;          // output row bytes (W * cmid for stencils, W * cout for pointwise)
+  int rows;       // local rows
+  int row0, Hg;   // border geometry
+  int border;     // Border enum
+  int ry0, ry1, ry2, ry3;  // output row ranges [ry0,ry1) U [ry2,ry3)
+  int band;       // rows per workgroup
+  int nb0;        // workgroups (in y) covering range 0
+  int out_px;     // x-margin pixels to maintain on the output
+  int out_border; // border mode encoded in those margins
+  int has_pre, has_post, has_epi;
+  int gmode;      // 0 bt601, 1 ref
+  uint32_t gmul[3];
+  int gshift[3];
+  int cin;        // pointwise: input channels
+};
+
+__device__ __forceinline__ int border_index_dev(int i, int n, int b) {
+  if (i >= 0 && i < n) return i;
+  if (b == (int)Border::Constant) return -1;
+  if (b == (int)Border::Replicate) return i < 0 ? 0 : n - 1;
+  if (n == 1) return 0;
+  const int period = 2 * (n - 1);
+  int j = i % period;
+  if (j < 0) j += period;
+  return j < n ? j : period - j;
+}
+
+// Input row pointer for local row y with the global-edge border applied (scalar).
+__device__ __forceinline__ const uint8_t* in_row(const KArgs& a, int y) {
+  int g = a.row0 + y;
+  if (g < 0 || g >= a.Hg) {
+    const int m = border_index_dev(g, a.Hg, a.border);
+    if (m < 0) return a.zero_row;
+    g = m;
+  }
+  return a.in + (int64_t)(g - a.row0) * a.in_pitch;
+}
+
+// Row range of workgroup row `by`.
+__device__ __forceinline__ void band_range(const KArgs& a, int by, int& ys, int& ye) {
+  if (by < a.nb0) {
+    ys = a.ry0 + by * a.band;
+    ye = min(ys + a.band, a.ry1);
+  } else {
+    ys = a.ry2 + (by - a.nb0) * a.band;
+    ye = min(ys + a.band, a.ry3);
+  }
+}
+
+__device__ __forceinline__ uint32_t byte_of(const uint32_t (&d)[4], int j) {
+  return (d[j >> 2] >> ((j & 3) * 8)) & 0xFFu;
+}
+
+// Dynamic byte select without scratch (cndmask chain).
+__device__ __forceinline__ uint32_t byte_dyn(const uint32_t (&d)[4], int j) {
+  const uint32_t w = j < 4 ? d[0] : (j < 8 ? d[1] : (j < 12 ? d[2] : d[3]));
+  return (w >> ((j & 3) * 8)) & 0xFFu;
+}
+
+__device__ __forceinline__ uint32_t pack4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  return a | (b << 8) | (c << 16) | (d << 24);
+}
+
+// Gray of one pixel (semantic R, G, B).
+__device__ __forceinline__ uint32_t gray_dev(const KArgs& a, uint32_t r, uint32_t g, uint32_t b) {
+  if (a.gmode == 1)
+    return ((r * a.gmul[0]) >> a.gshift[0]) + ((g * a.gmul[1]) >> a.gshift[1]) +
+           ((b * a.gmul[2]) >> a.gshift[2]);
+  return (r * 4899u + g * 9617u + b * 1868u + 8192u) >> 14;
+}
+
+// 16 RGB pixels (48 bytes) -> 16 gray bytes (4 dwords).
+__device__ __forceinline__ void gray16(const KArgs& a, const uint32_t (&rgb)[12], uint32_t (&o)[4]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int p = q * 4 + e;
+      const int b0 = 3 * p;
+      const uint32_t r = (rgb[b0 >> 2] >> ((b0 & 3) * 8)) & 0xFF;
+      const uint32_t g = (rgb[(b0 + 1) >> 2] >> (((b0 + 1) & 3) * 8)) & 0xFF;
+      const uint32_t bl = (rgb[(b0 + 2) >> 2] >> (((b0 + 2) & 3) * 8)) & 0xFF;
+      v[e] = gray_dev(a, r, g, bl);
+    }
+    o[q] = pack4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+__device__ __forceinline__ void lut16(const uint8_t* lut, uint32_t (&o)[4]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t w = o[q];
+    o[q] = pack4(lut[w & 0xFF], lut[(w >> 8) & 0xFF], lut[(w >> 16) & 0xFF], lut[w >> 24]);
+  }
+}
+
+// Store 16 output bytes at row + cb; only bytes < E (straddling chunk is split).
+__device__ __forceinline__ void store_chunk(uint8_t* row, int cb, int E, const uint32_t (&o)[4]) {
+  if (cb + 16 <= E) {
+    *reinterpret_cast<uint4*>(row + cb) = make_uint4(o[0], o[1], o[2], o[3]);
+  } else {
+    for (int j = 0; j < E - cb; ++j) row[cb + j] = (uint8_t)byte_dyn(o, j);
+  }
+}
+
+// Maintain the x-margins of an output row: margin pixel m (m < 0 or m >= W) takes
+// the value of pixel border_index(m).  Each lane writes the margin bytes whose
+// source lies in its own 16-byte chunk [cb, cb+16).  Only edge lanes do work.
+template <int C>
+__device__ __forceinline__ void write_margins(uint8_t* row, int cb, const KArgs& a, const uint32_t (&o)[4]) {
+  const int px = a.out_px;
+  if (px == 0) return;
+  const int E = a.W * C;
+  const int reach = (px + 1) * C + 16;
+  if (cb >= reach && cb + 16 <= E - reach) return;  // interior lane
+  for (int k = 1; k <= px; ++k) {
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+      const int m = side == 0 ? -k : a.W - 1 + k;
+      const int s = border_index_dev(m, a.W, a.out_border);
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const int dst = m * C + c;
+        if (s < 0) {
+          if (cb == 0) row[dst] = 0;  // constant border: one lane writes the zeros
+          continue;
+        }
+        const int sb = s * C + c - cb;
+        if (sb >= 0 && sb < 16 && cb + sb < E) row[dst] = (uint8_t)byte_dyn(o, sb);
+      }
+    }
+  }
+}
+
+}  // namespace dev
+}  // namespace stripe

@@ -1,0 +1,67 @@
+// Communication layer: point-to-point groups + barrier, behind one narrow interface.
+//
+// Reference call sites: MPI_Init/Comm_rank/Comm_size, 2x Barrier,
+// Bcast of 4 ints, Scatter, Gather, Finalize on MPI_COMM_WORLD over host memory
+// (kernel.cu:104-137,223-225,250).  Here every data movement is expressed as a
+// group of sends/receives so the same partition/halo logic runs on:
+//   rccl  - RCCL (ncclSend/ncclRecv in ncclGroupStart/End) device-to-device over
+//           xGMI, one rank per GPU (multi-process or one thread per GPU);
+//   local - N ranks inside one process (threads), device copies on the ranks'
+//           streams (lets N logical ranks share the single GPU of a test box;
+//           RCCL rejects duplicate devices in one communicator);
+//   host  - N ranks inside one process, host memcpy (CPU-only runs/tests);
+//   py    - callbacks into Python (torch.distributed gloo) for multi-process CPU tests.
+// Error handling (Q9): any failure aborts the whole group instead of hanging it.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <array>
+#include <functional>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "stripe/common.h"
+
+namespace stripe {
+
+class Comm {
+ public:
+  virtual ~Comm() = default;
+  virtual int rank() const = 0;
+  virtual int size() const = 0;
+  virtual const char* backend() const = 0;
+  virtual bool device_buffers() const = 0;  // send/recv pointers are device memory
+  virtual void group_start() = 0;
+  virtual void send(const void* buf, size_t bytes, int peer, hipStream_t s) = 0;
+  virtual void recv(void* buf, size_t bytes, int peer, hipStream_t s) = 0;
+  virtual void group_end() = 0;
+  virtual void barrier() = 0;  // host-blocking, all ranks
+  virtual void abort(const std::string& why) = 0;
+};
+
+// ---- RCCL ----
+using UniqueId = std::array<char, 128>;
+UniqueId rccl_unique_id();
+std::unique_ptr<Comm> make_rccl_comm(const UniqueId& id, int rank, int world, int device);
+// One process driving `devices.size()` GPUs (caller runs one thread per rank).
+std::vector<std::unique_ptr<Comm>> make_rccl_comms_all(const std::vector<int>& devices);
+std::string rccl_version();
+
+// ---- in-process groups ----
+class LocalHub;
+std::shared_ptr<LocalHub> make_local_hub(int world, bool device, double timeout_s = 300.0);
+std::unique_ptr<Comm> make_local_comm(const std::shared_ptr<LocalHub>& hub, int rank);
+
+// ---- Python / external callbacks (host buffers) ----
+struct CallbackOps {
+  std::function<void()> group_start;
+  std::function<void(const void*, size_t, int)> send;
+  std::function<void(void*, size_t, int)> recv;
+  std::function<void()> group_end;
+  std::function<void()> barrier;
+};
+std::unique_ptr<Comm> make_callback_comm(int rank, int world, CallbackOps ops);
+
+}  // namespace stripe

@@ -1,0 +1,153 @@
+// Per-rank stripe engine: owns the rank's padded stripe buffers, streams and
+// compiled pass constants, and executes the chain with halo exchange.
+//
+// Reference equivalent: the body of main() between MPI_Scatter and MPI_Gather
+// (kernel.cu:139-225): cudaSetDevice(0) on every rank (Q8), cudaMalloc with
+// leaked host buffers (Q11), synchronous pageable memcpys, three default-stream
+// launches, cudaDeviceSynchronize.  Here: rank r -> device r, RAII buffers,
+// a compute stream plus a comm stream, halo rows exchanged while the interior
+// rows are computed, then the boundary rows.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "stripe/chain.h"
+#include "stripe/comm.h"
+#include "stripe/golden.h"
+#include "stripe/image.h"
+#include "stripe/kernels.h"
+#include "stripe/partition.h"
+
+namespace stripe {
+
+enum class BackendKind : int { Device = 0, Host = 1 };
+
+struct EngineConfig {
+  int W = 0, H = 0, C = 3;      // full input image
+  std::string chain = "gaussian5";
+  Border border = Border::Reflect101;  // default border of stencils without "@mode"
+  bool halo = true;             // false: every stripe filtered as its own image (legacy, Q6)
+  bool legacy_partition = false;  // rows/size per rank, remainder dropped (Q7)
+  bool overlap = true;          // interior/boundary split, halo exchange on a side stream
+  bool fuse = true;             // fuse pointwise runs into stencil prologue/epilogue
+  int device = -1;              // HIP device for this rank (-1: keep current)
+  BackendKind backend = BackendKind::Device;
+  int band = 0;                 // stencil rows per workgroup (0 = auto)
+  bool root_buffers = false;    // rank 0 allocates full-frame in/out buffers (scatter/gather)
+};
+
+// Device or host allocation freed on destruction.
+class Buffer {
+ public:
+  Buffer() = default;
+  Buffer(size_t bytes, bool device);
+  ~Buffer();
+  Buffer(const Buffer&) = delete;
+  Buffer& operator=(const Buffer&) = delete;
+  Buffer(Buffer&& o) noexcept { *this = std::move(o); }
+  Buffer& operator=(Buffer&& o) noexcept;
+  uint8_t* data() const { return p_; }
+  size_t bytes() const { return n_; }
+
+ private:
+  uint8_t* p_ = nullptr;
+  size_t n_ = 0;
+  bool dev_ = false;
+};
+
+struct PhaseTimes {  // milliseconds of the last call of each phase (device events)
+  double run = 0, scatter = 0, gather = 0, load = 0, store = 0;
+};
+
+class Engine {
+ public:
+  Engine(const EngineConfig& cfg, Comm* comm);
+  ~Engine();
+  Engine(const Engine&) = delete;
+  Engine& operator=(const Engine&) = delete;
+
+  const EngineConfig& config() const { return cfg_; }
+  const Plan& plan() const { return plan_; }
+  const Partition& partition() const { return part_; }
+  const Stripe& stripe() const { return part_.of(rank_); }
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+  bool device() const { return cfg_.backend == BackendKind::Device; }
+  int out_channels() const { return plan_.cout; }
+  hipStream_t stream() const { return s_compute_; }
+  // Run everything on an externally owned stream (e.g. torch's current stream).
+  void use_external_stream(hipStream_t s);
+
+  // ---- input ----
+  void load_synthetic(uint64_t seed);                     // own stripe, generated in place
+  void load_packed(const void* src, bool src_device);     // own stripe, packed rows
+  void load_root(const void* full, bool src_device);      // rank 0: full frame into root buffer
+  void load_root_synthetic(uint64_t seed);                // rank 0: synthetic full frame on device
+  void scatter();                                         // root buffer -> every rank's stripe
+
+  // ---- compute ----
+  void run(int iterations = 1);
+
+  // ---- output ----
+  void store_packed(void* dst, bool dst_device);          // own output stripe, packed
+  void gather();                                          // every stripe -> root output buffer
+  void store_root(void* full, bool dst_device);           // rank 0: root output buffer, packed
+
+  void synchronize();
+  const PhaseTimes& times() const { return times_; }
+  // device pointer + pitch of the current input/output stripe origins (for tests)
+  const uint8_t* input_origin() const;
+  const uint8_t* output_origin() const;
+  int64_t pitch(int C) const { return padded_pitch(cfg_.W, C); }
+
+ private:
+  struct PassRt {
+    PassConsts pc;
+    Buffer luts;
+  };
+  uint8_t* origin(const Buffer& b, int C) const;
+  uint8_t* root_origin(const Buffer& b, int C) const;
+  void exchange_halo(uint8_t* org, int C, int R, hipStream_t s);
+  void run_pass(const Pass& p, const uint8_t* in, uint8_t* out);
+  void copy2d(void* dst, int64_t dpitch, const void* src, int64_t spitch, int64_t width, int64_t rows,
+              hipStream_t s, int kind);
+  void fill_margins(uint8_t* org, int C, int y0, int y1, int px, Border b, hipStream_t s);
+  void record(hipEvent_t e, hipStream_t s);
+  float elapsed(hipEvent_t a, hipEvent_t b);
+  RowGeom geom() const;
+
+  EngineConfig cfg_;
+  Comm* comm_ = nullptr;
+  int rank_ = 0, world_ = 1;
+  Plan plan_;
+  Partition part_;
+  int halo_ = 0;            // halo rows allocated above/below the stripe
+  int rows_alloc_ = 0;
+  Buffer buf_[2];
+  int cur_ = 0;             // which buffer holds the current input
+  int cur_c_ = 3;           // channels of the current input
+  Buffer zero_;             // one all-zero padded row (Constant y-border)
+  Buffer root_in_, root_out_;
+  std::vector<PassRt> prt_;
+  hipStream_t s_compute_ = nullptr, s_comm_ = nullptr;
+  bool own_streams_ = false;
+  hipEvent_t ev_[8] = {};
+  PhaseTimes times_;
+  int out_buf_ = -1;        // buffer holding the last run's output
+  int out_c_ = 0;
+};
+
+// Convenience driver: run the whole distributed pipeline on `world` in-process
+// ranks (local device backend or host backend), root -> scatter -> run -> gather.
+Image run_local_group(const EngineConfig& cfg, int world, const Image& input, int iterations,
+                      PhaseTimes* times = nullptr);
+// Same driver over caller-provided communicators (one host thread per rank);
+// devices[r] is rank r's HIP device (empty: keep cfg.device).
+Image run_group(const EngineConfig& cfg, const std::vector<Comm*>& comms, const std::vector<int>& devices,
+                const Image& input, int iterations, PhaseTimes* times = nullptr);
+
+}  // namespace stripe

@@ -1,0 +1,75 @@
+// Host image container, PPM/PGM I/O and the seeded synthetic generator.
+//
+// Reference I/O is OpenCV: imread of a hard-coded JPEG path (kernel.cu:110),
+// lossy imwrite("imageFinalEmboss2.jpg") (kernel.cu:236), blocking imshow/waitKey
+// windows (kernel.cu:120-122,233-235).  The rebuild is headless and lossless:
+// binary PPM (P6, 3 channels RGB) / PGM (P5, gray), maxval 255; ASCII P2/P3 are
+// accepted on input.  Writes go to a temp file then rename() so a crash never
+// leaves a half-written output.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#endif
+
+#include "stripe/common.h"
+
+namespace stripe {
+
+struct Image {
+  int W = 0, H = 0, C = 0;      // C in {1, 3}; pixels interleaved R,G,B
+  std::vector<uint8_t> data;    // packed, H * W * C bytes
+
+  Image() = default;
+  Image(int w, int h, int c) : W(w), H(h), C(c), data((size_t)w * h * c, 0) {}
+  size_t bytes() const { return data.size(); }
+  int64_t row_bytes() const { return (int64_t)W * C; }
+  uint8_t* row(int y) { return data.data() + (size_t)y * W * C; }
+  const uint8_t* row(int y) const { return data.data() + (size_t)y * W * C; }
+};
+
+Image read_pnm(const std::string& path);
+void write_pnm(const std::string& path, const Image& img);
+// In-memory variants (used by tests and the bindings).
+Image decode_pnm(const std::string& bytes);
+std::string encode_pnm(const Image& img);
+
+// ---- synthetic random-pixel frames ----
+// Counter-based: byte (y, b) of a W*C row is a pure function of (seed, y, b), so
+// every rank generates its own stripe with no root copy and no host round trip.
+#if defined(__HIPCC__)
+#define STRIPE_SYNTH_HD __host__ __device__ __forceinline__
+#else
+#define STRIPE_SYNTH_HD inline
+#endif
+
+STRIPE_SYNTH_HD uint32_t synth_byte(uint64_t seed, int64_t y, int64_t b) {
+  // splitmix64 finaliser over a unique 64-bit counter
+  uint64_t z = seed * 0x9E3779B97F4A7C15ull + (uint64_t)y * 0xD1B54A32D192ED03ull +
+               (uint64_t)b * 0xABC98388FB8FAC03ull;
+  z ^= z >> 30;
+  z *= 0xBF58476D1CE4E5B9ull;
+  z ^= z >> 27;
+  z *= 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)(z >> 24) & 0xFFu;
+}
+
+// rows [row0, row0 + rows) of a W x H x C synthetic frame, packed
+void synth_rows(uint64_t seed, int W, int C, int row0, int rows, uint8_t* dst);
+Image synth_image(uint64_t seed, int W, int H, int C);
+
+// Compare two images; returns max |a-b| and counts differing bytes.
+struct CmpResult {
+  bool same_shape = false;
+  int max_abs = 0;
+  int64_t n_diff = 0;
+  double psnr = 0.0;
+};
+CmpResult compare_images(const Image& a, const Image& b);
+
+}  // namespace stripe

@@ -1,0 +1,63 @@
+// Host-side launch API of the HIP kernels (csrc/hip/*.hip).
+//
+// All launches are asynchronous on the given stream and error-checked
+// (hipGetLastError after every launch; the reference never checks its three
+// launches, kernel.cu:192-195, Q10).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "stripe/chain.h"
+
+namespace stripe {
+
+#define HIP_CHECK(expr)                                                              \
+  do {                                                                               \
+    hipError_t _e = (expr);                                                          \
+    if (_e != hipSuccess) {                                                          \
+      std::ostringstream _os;                                                        \
+      _os << __FILE__ << ":" << __LINE__ << ": " #expr " failed: " << hipGetErrorString(_e); \
+      ::stripe::fail(_os.str());                                                     \
+    }                                                                                \
+  } while (0)
+
+// Device-resident per-pass constants, built once by the engine.
+struct PassConsts {
+  uint8_t* luts = nullptr;   // [pre 256 | post 256 | epi 256]
+  void* conv = nullptr;      // conv pass: packed MFMA operand tables
+  size_t conv_bytes = 0;
+};
+
+struct PassLaunch {
+  const uint8_t* in = nullptr;   // origin (local row 0, byte 0) of the input stripe
+  int64_t in_pitch = 0;
+  uint8_t* out = nullptr;        // origin of the output stripe
+  int64_t out_pitch = 0;
+  int W = 0;                     // pixels per row
+  int rows = 0;                  // local rows owned
+  int row0 = 0, Hg = 0;          // border geometry (global row of local 0, global H)
+  int nrange = 1;                // 1 or 2 output row ranges
+  int ry[4] = {0, 0, 0, 0};      // [ry0, ry1) and [ry2, ry3)
+  const uint8_t* zero_row = nullptr;  // origin of an all-zero row (Constant y-border)
+  int band = 0;                  // rows per workgroup (0 = auto)
+};
+
+void launch_pass(const Pass& p, const PassConsts& pc, const PassLaunch& L, hipStream_t s);
+void launch_pointwise(const Pass& p, const PassConsts& pc, const PassLaunch& L, hipStream_t s);
+void launch_stencil(const Pass& p, const PassConsts& pc, const PassLaunch& L, hipStream_t s);
+void launch_conv(const Pass& p, const PassConsts& pc, const PassLaunch& L, hipStream_t s);
+
+// Write the x-margins of rows [y0, y1) of a stripe from its own pixels.
+void launch_fill_margins(uint8_t* origin, int64_t pitch, int W, int C, int y0, int y1, int px,
+                         Border b, hipStream_t s);
+
+// Synthetic pixels for local rows [0, rows) (global row0..), margins included.
+void launch_synth(uint8_t* origin, int64_t pitch, int W, int C, int row0, int rows, uint64_t seed,
+                  int margin_px, Border b, hipStream_t s);
+
+// Build the device constant block of a conv pass (MFMA operand tables).
+void prepare_conv_consts(const Pass& p, PassConsts* pc, hipStream_t s);
+
+}  // namespace stripe

@@ -1,0 +1,342 @@
+// Python bindings (pybind11): the native core exposed to the Python package.
+//
+// Device buffers cross the boundary as integer pointers (torch tensor
+// data_ptr()) plus a stream handle (torch.cuda.current_stream().cuda_stream),
+// so the Python side never copies pixel data; host images cross as numpy arrays.
+#include <pybind11/functional.h>
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <memory>
+
+#include "stripe/chain.h"
+#include "stripe/comm.h"
+#include "stripe/engine.h"
+#include "stripe/golden.h"
+#include "stripe/image.h"
+#include "stripe/partition.h"
+
+namespace py = pybind11;
+using namespace stripe;
+
+namespace {
+
+using U8Array = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>;
+
+Image image_from_numpy(const U8Array& a) {
+  Image img;
+  if (a.ndim() == 2) {
+    img = Image((int)a.shape(1), (int)a.shape(0), 1);
+  } else if (a.ndim() == 3) {
+    img = Image((int)a.shape(1), (int)a.shape(0), (int)a.shape(2));
+  } else {
+    fail("image array must be HxW or HxWxC");
+  }
+  STRIPE_CHECK(img.C == 1 || img.C == 3, "image must have 1 or 3 channels");
+  std::memcpy(img.data.data(), a.data(), img.bytes());
+  return img;
+}
+
+U8Array image_to_numpy(const Image& img) {
+  std::vector<py::ssize_t> shape = {img.H, img.W};
+  if (img.C != 1) shape.push_back(img.C);
+  U8Array a(shape);
+  std::memcpy(a.mutable_data(), img.data.data(), img.bytes());
+  return a;
+}
+
+hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Comm wrapper owning its hub reference (Python-visible handle).
+struct PyComm {
+  std::unique_ptr<Comm> comm;
+};
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "stripe: MI355X-native distributed image filtering core (HIP/RCCL)";
+
+  py::register_exception<Error>(m, "StripeError", PyExc_RuntimeError);
+
+  py::enum_<Border>(m, "Border")
+      .value("reflect101", Border::Reflect101)
+      .value("replicate", Border::Replicate)
+      .value("constant", Border::Constant)
+      .value("skip", Border::Skip);
+  m.def("parse_border", &parse_border);
+  m.def("border_index", &border_index);
+
+  py::enum_<BackendKind>(m, "Backend").value("device", BackendKind::Device).value("host", BackendKind::Host);
+
+  // ---- image I/O ----
+  m.def("read_pnm", [](const std::string& p) { return image_to_numpy(read_pnm(p)); });
+  m.def("write_pnm", [](const std::string& p, const U8Array& a) { write_pnm(p, image_from_numpy(a)); });
+  m.def("decode_pnm", [](py::bytes b) { return image_to_numpy(decode_pnm(std::string(b))); });
+  m.def("encode_pnm", [](const U8Array& a) { return py::bytes(encode_pnm(image_from_numpy(a))); });
+  m.def("synth_image", [](uint64_t seed, int W, int H, int C) { return image_to_numpy(synth_image(seed, W, H, C)); });
+  m.def("synth_rows", [](uint64_t seed, int W, int C, int row0, int rows) {
+    Image img(W, rows, C);
+    synth_rows(seed, W, C, row0, rows, img.data.data());
+    return image_to_numpy(img);
+  });
+  m.def("synth_byte", [](uint64_t seed, int64_t y, int64_t b) { return synth_byte(seed, y, b); });
+
+  // ---- filter spec ----
+  m.def("parse_chain", [](const std::string& s) { return chain_to_string(parse_chain(s)); },
+        "canonical spelling of a chain");
+  m.def("gray_pixel", [](const std::string& mode, int r, int g, int b) {
+    return (int)gray_pixel(mode == "ref" ? GrayMode::Ref : GrayMode::BT601, (uint8_t)r, (uint8_t)g, (uint8_t)b);
+  });
+  m.def("pointwise_lut", [](const std::string& op) {
+    auto ops = parse_chain(op);
+    STRIPE_CHECK(ops.size() == 1 && ops[0].pointwise() && ops[0].kind != OpKind::Gray &&
+                     ops[0].kind != OpKind::Expand,
+                 "pointwise_lut needs one per-channel op");
+    std::vector<int> lut(256);
+    for (int v = 0; v < 256; ++v) lut[v] = apply_pointwise_u8(ops[0], (uint8_t)v);
+    return lut;
+  });
+  m.def("stencil_weights", [](const std::string& name) {
+    StencilId sid;
+    STRIPE_CHECK(stencil_from_name(name, &sid), "unknown stencil " << name);
+    const StencilInfo& s = stencil_info(sid);
+    py::dict d;
+    d["K"] = s.K;
+    d["w"] = s.w;
+    d["div"] = s.div;
+    d["separable"] = s.separable;
+    d["sobel"] = s.sobel;
+    return d;
+  });
+  m.def("gaussian_1d", &gaussian_1d, py::arg("K"), py::arg("sigma") = 0.0);
+  m.def("describe_chain", [](const std::string& chain, int cin, const std::string& border, bool fuse) {
+    return compile_chain(parse_chain(chain), cin, parse_border(border), fuse).describe();
+  }, py::arg("chain"), py::arg("cin") = 3, py::arg("border") = "reflect101", py::arg("fuse") = true);
+  m.def("plan_info", [](const std::string& chain, int cin, const std::string& border, bool fuse) {
+    Plan p = compile_chain(parse_chain(chain), cin, parse_border(border), fuse);
+    py::dict d;
+    d["cin"] = p.cin;
+    d["cout"] = p.cout;
+    d["max_radius"] = p.max_radius;
+    d["in_margin_px"] = p.in_margin_px;
+    py::list passes;
+    for (const auto& ps : p.passes) {
+      py::dict q;
+      q["kind"] = (int)ps.kind;
+      q["desc"] = ps.desc;
+      q["R"] = ps.R;
+      q["cin"] = ps.cin;
+      q["cout"] = ps.cout;
+      q["out_margin_px"] = ps.out_margin_px;
+      passes.append(q);
+    }
+    d["passes"] = passes;
+    return d;
+  }, py::arg("chain"), py::arg("cin") = 3, py::arg("border") = "reflect101", py::arg("fuse") = true);
+
+  // ---- golden ----
+  m.def("golden_apply", [](const U8Array& a, const std::string& chain, const std::string& border, bool fuse) {
+    Image img = image_from_numpy(a);
+    Image out;
+    {
+      py::gil_scoped_release nogil;
+      Plan p = compile_chain(parse_chain(chain), img.C, parse_border(border), fuse);
+      out = golden_apply_plan(img, p);
+    }
+    return image_to_numpy(out);
+  }, py::arg("image"), py::arg("chain"), py::arg("border") = "reflect101", py::arg("fuse") = true);
+  m.def("golden_apply_unfused", [](const U8Array& a, const std::string& chain, const std::string& border) {
+    Image img = image_from_numpy(a);
+    Image out;
+    {
+      py::gil_scoped_release nogil;
+      out = golden_apply_ops(img, parse_chain(chain), parse_border(border));
+    }
+    return image_to_numpy(out);
+  }, py::arg("image"), py::arg("chain"), py::arg("border") = "reflect101");
+
+  // ---- partition ----
+  m.def("plan_rows", [](int H, int world, int min_rows, bool legacy) {
+    Partition p = plan_rows(H, world, min_rows, legacy);
+    std::vector<std::pair<int, int>> v;
+    for (const auto& s : p.stripes) v.emplace_back(s.row0, s.rows);
+    return py::make_tuple(v, p.active);
+  }, py::arg("H"), py::arg("world"), py::arg("min_rows") = 1, py::arg("legacy") = false);
+
+  // ---- comm ----
+  py::class_<PyComm>(m, "Comm")
+      .def_property_readonly("rank", [](const PyComm& c) { return c.comm->rank(); })
+      .def_property_readonly("size", [](const PyComm& c) { return c.comm->size(); })
+      .def_property_readonly("backend", [](const PyComm& c) { return std::string(c.comm->backend()); })
+      .def("barrier", [](PyComm& c) {
+        py::gil_scoped_release nogil;
+        c.comm->barrier();
+      });
+  m.def("rccl_unique_id", []() {
+    UniqueId id = rccl_unique_id();
+    return py::bytes(id.data(), id.size());
+  });
+  m.def("rccl_version", &rccl_version);
+  m.def("make_rccl_comm", [](py::bytes uid, int rank, int world, int device) {
+    std::string s(uid);
+    STRIPE_CHECK(s.size() == 128, "unique id must be 128 bytes");
+    UniqueId id;
+    std::memcpy(id.data(), s.data(), 128);
+    auto c = std::make_unique<PyComm>();
+    {
+      py::gil_scoped_release nogil;
+      c->comm = make_rccl_comm(id, rank, world, device);
+    }
+    return c;
+  });
+  m.def("make_callback_comm", [](int rank, int world, py::function group_start, py::function send,
+                                 py::function recv, py::function group_end, py::function barrier) {
+    CallbackOps ops;
+    ops.group_start = [group_start]() {
+      py::gil_scoped_acquire g;
+      group_start();
+    };
+    ops.send = [send](const void* p, size_t n, int peer) {
+      py::gil_scoped_acquire g;
+      send((uintptr_t)p, n, peer);
+    };
+    ops.recv = [recv](void* p, size_t n, int peer) {
+      py::gil_scoped_acquire g;
+      recv((uintptr_t)p, n, peer);
+    };
+    ops.group_end = [group_end]() {
+      py::gil_scoped_acquire g;
+      group_end();
+    };
+    ops.barrier = [barrier]() {
+      py::gil_scoped_acquire g;
+      barrier();
+    };
+    auto c = std::make_unique<PyComm>();
+    c->comm = make_callback_comm(rank, world, std::move(ops));
+    return c;
+  });
+
+  // ---- engine ----
+  py::class_<EngineConfig>(m, "EngineConfig")
+      .def(py::init<>())
+      .def_readwrite("W", &EngineConfig::W)
+      .def_readwrite("H", &EngineConfig::H)
+      .def_readwrite("C", &EngineConfig::C)
+      .def_readwrite("chain", &EngineConfig::chain)
+      .def_readwrite("border", &EngineConfig::border)
+      .def_readwrite("halo", &EngineConfig::halo)
+      .def_readwrite("legacy_partition", &EngineConfig::legacy_partition)
+      .def_readwrite("overlap", &EngineConfig::overlap)
+      .def_readwrite("fuse", &EngineConfig::fuse)
+      .def_readwrite("device", &EngineConfig::device)
+      .def_readwrite("backend", &EngineConfig::backend)
+      .def_readwrite("band", &EngineConfig::band)
+      .def_readwrite("root_buffers", &EngineConfig::root_buffers);
+
+  py::class_<PhaseTimes>(m, "PhaseTimes")
+      .def_readonly("run", &PhaseTimes::run)
+      .def_readonly("scatter", &PhaseTimes::scatter)
+      .def_readonly("gather", &PhaseTimes::gather);
+
+  py::class_<Engine>(m, "Engine")
+      .def(py::init([](const EngineConfig& cfg, PyComm* comm) {
+             py::gil_scoped_release nogil;
+             return std::make_unique<Engine>(cfg, comm ? comm->comm.get() : nullptr);
+           }),
+           py::arg("config"), py::arg("comm") = nullptr, py::keep_alive<1, 3>())
+      .def_property_readonly("rank", &Engine::rank)
+      .def_property_readonly("world", &Engine::world)
+      .def_property_readonly("out_channels", &Engine::out_channels)
+      .def_property_readonly("plan", [](const Engine& e) { return e.plan().describe(); })
+      .def_property_readonly("partition", [](const Engine& e) { return e.partition().describe(); })
+      .def_property_readonly("stripe", [](const Engine& e) {
+        return py::make_tuple(e.stripe().row0, e.stripe().rows);
+      })
+      .def("use_external_stream", [](Engine& e, uintptr_t s) { e.use_external_stream(as_stream(s)); })
+      .def("load_synthetic", [](Engine& e, uint64_t seed) {
+        py::gil_scoped_release nogil;
+        e.load_synthetic(seed);
+      })
+      .def("load_packed_ptr", [](Engine& e, uintptr_t p, bool dev) {
+        py::gil_scoped_release nogil;
+        e.load_packed(reinterpret_cast<const void*>(p), dev);
+      })
+      .def("load_packed", [](Engine& e, const U8Array& a) {
+        STRIPE_CHECK((size_t)a.size() == (size_t)e.stripe().rows * e.config().W * e.config().C,
+                     "stripe array has the wrong size");
+        e.load_packed(a.data(), false);
+        e.synchronize();
+      })
+      .def("load_root", [](Engine& e, const U8Array& a) {
+        e.load_root(a.data(), false);
+        e.synchronize();
+      })
+      .def("load_root_synthetic", [](Engine& e, uint64_t seed) {
+        py::gil_scoped_release nogil;
+        e.load_root_synthetic(seed);
+      })
+      .def("load_root_ptr", [](Engine& e, uintptr_t p, bool dev) { e.load_root(reinterpret_cast<const void*>(p), dev); })
+      .def("scatter", [](Engine& e) {
+        py::gil_scoped_release nogil;
+        e.scatter();
+      })
+      .def("run", [](Engine& e, int it) {
+        py::gil_scoped_release nogil;
+        e.run(it);
+      }, py::arg("iterations") = 1)
+      .def("gather", [](Engine& e) {
+        py::gil_scoped_release nogil;
+        e.gather();
+      })
+      .def("store_packed_ptr", [](Engine& e, uintptr_t p, bool dev) {
+        py::gil_scoped_release nogil;
+        e.store_packed(reinterpret_cast<void*>(p), dev);
+      })
+      .def("store_packed", [](Engine& e) {
+        const auto& c = e.config();
+        std::vector<py::ssize_t> shape = {e.stripe().rows, c.W};
+        if (e.out_channels() != 1) shape.push_back(e.out_channels());
+        U8Array a(shape);
+        {
+          py::gil_scoped_release nogil;
+          e.store_packed(a.mutable_data(), false);
+          e.synchronize();
+        }
+        return a;
+      })
+      .def("store_root", [](Engine& e) {
+        const auto& c = e.config();
+        std::vector<py::ssize_t> shape = {c.H, c.W};
+        if (e.out_channels() != 1) shape.push_back(e.out_channels());
+        U8Array a(shape);
+        {
+          py::gil_scoped_release nogil;
+          e.store_root(a.mutable_data(), false);
+          e.synchronize();
+        }
+        return a;
+      })
+      .def("store_root_ptr", [](Engine& e, uintptr_t p, bool dev) { e.store_root(reinterpret_cast<void*>(p), dev); })
+      .def("synchronize", [](Engine& e) {
+        py::gil_scoped_release nogil;
+        e.synchronize();
+      })
+      .def_property_readonly("times", [](const Engine& e) { return e.times(); });
+
+  m.def("run_local_group", [](const EngineConfig& cfg, int world, const U8Array& a, int iterations) {
+    Image img = image_from_numpy(a);
+    Image out;
+    {
+      py::gil_scoped_release nogil;
+      out = run_local_group(cfg, world, img, iterations);
+    }
+    return image_to_numpy(out);
+  }, py::arg("config"), py::arg("world"), py::arg("image"), py::arg("iterations") = 1);
+
+  m.attr("kMarginBytes") = kMarginBytes;
+  m.attr("kMaxRadius") = kMaxRadius;
+  m.def("padded_pitch", &padded_pitch);
+}

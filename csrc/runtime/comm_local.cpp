@@ -1,0 +1,234 @@
+// In-process communication groups (local = device copies, host = memcpy) and the
+// callback backend.  Semantics match a grouped ncclSend/ncclRecv: sends are
+// posted immediately, group_end() completes this rank's receives, then waits for
+// its sends to be consumed (so the sender may reuse its buffer afterwards).
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <mutex>
+
+#include "stripe/comm.h"
+#include "stripe/kernels.h"
+
+namespace stripe {
+
+struct Msg {
+  const void* ptr = nullptr;
+  size_t bytes = 0;
+  int src_dev = -1;
+  hipEvent_t ready = nullptr;  // recorded on the sender's stream (device mode)
+  hipEvent_t done = nullptr;   // recorded on the receiver's stream after the copy
+  bool consumed = false;
+};
+
+class LocalHub {
+ public:
+  LocalHub(int world, bool device, double timeout_s) : world_(world), device_(device), timeout_s_(timeout_s) {}
+  int world() const { return world_; }
+  bool device() const { return device_; }
+
+  void post(int src, int dst, const std::shared_ptr<Msg>& m) {
+    std::lock_guard<std::mutex> lk(mu_);
+    box_[{src, dst}].push_back(m);
+    cv_.notify_all();
+  }
+  std::shared_ptr<Msg> take(int src, int dst) {
+    std::unique_lock<std::mutex> lk(mu_);
+    auto& q = box_[{src, dst}];
+    wait(lk, [&] { return !q.empty(); }, "receive from rank " + std::to_string(src));
+    auto m = q.front();
+    q.pop_front();
+    return m;
+  }
+  void mark_consumed(const std::shared_ptr<Msg>& m) {
+    std::lock_guard<std::mutex> lk(mu_);
+    m->consumed = true;
+    cv_.notify_all();
+  }
+  void wait_consumed(const std::shared_ptr<Msg>& m, int dst) {
+    std::unique_lock<std::mutex> lk(mu_);
+    wait(lk, [&] { return m->consumed; }, "send to rank " + std::to_string(dst) + " to be received");
+  }
+  void barrier() {
+    std::unique_lock<std::mutex> lk(mu_);
+    const long gen = bar_gen_;
+    if (++bar_count_ == world_) {
+      bar_count_ = 0;
+      ++bar_gen_;
+      cv_.notify_all();
+      return;
+    }
+    wait(lk, [&] { return bar_gen_ != gen; }, "barrier");
+  }
+  void abort(const std::string& why) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!aborted_) abort_msg_ = why;
+    aborted_ = true;
+    cv_.notify_all();
+  }
+
+ private:
+  template <class Pred>
+  void wait(std::unique_lock<std::mutex>& lk, Pred pred, const std::string& what) {
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s_);
+    while (!pred()) {
+      if (aborted_) fail("communicator aborted (" + abort_msg_ + ") while waiting for " + what);
+      if (cv_.wait_until(lk, deadline) == std::cv_status::timeout && !pred()) {
+        aborted_ = true;
+        abort_msg_ = "timeout waiting for " + what;
+        cv_.notify_all();
+        fail("local comm: " + abort_msg_);
+      }
+    }
+  }
+
+  const int world_;
+  const bool device_;
+  const double timeout_s_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::map<std::pair<int, int>, std::deque<std::shared_ptr<Msg>>> box_;
+  int bar_count_ = 0;
+  long bar_gen_ = 0;
+  bool aborted_ = false;
+  std::string abort_msg_;
+};
+
+namespace {
+
+class LocalComm final : public Comm {
+ public:
+  LocalComm(std::shared_ptr<LocalHub> hub, int rank) : hub_(std::move(hub)), rank_(rank) {}
+  int rank() const override { return rank_; }
+  int size() const override { return hub_->world(); }
+  const char* backend() const override { return hub_->device() ? "local" : "host"; }
+  bool device_buffers() const override { return hub_->device(); }
+  void group_start() override {
+    STRIPE_CHECK(!in_group_, "nested group_start");
+    in_group_ = true;
+  }
+  void send(const void* buf, size_t bytes, int peer, hipStream_t s) override {
+    check_peer(peer);
+    auto m = std::make_shared<Msg>();
+    m->ptr = buf;
+    m->bytes = bytes;
+    if (hub_->device()) {
+      HIP_CHECK(hipGetDevice(&m->src_dev));
+      HIP_CHECK(hipEventCreateWithFlags(&m->ready, hipEventDisableTiming));
+      HIP_CHECK(hipEventRecord(m->ready, s));
+    }
+    hub_->post(rank_, peer, m);
+    sends_.push_back({m, peer, s});
+    if (!in_group_) group_end_impl();
+  }
+  void recv(void* buf, size_t bytes, int peer, hipStream_t s) override {
+    check_peer(peer);
+    recvs_.push_back({buf, bytes, peer, s});
+    if (!in_group_) group_end_impl();
+  }
+  void group_end() override {
+    STRIPE_CHECK(in_group_, "group_end without group_start");
+    in_group_ = false;
+    group_end_impl();
+  }
+  void barrier() override { hub_->barrier(); }
+  void abort(const std::string& why) override { hub_->abort(why); }
+
+ private:
+  struct PendingSend {
+    std::shared_ptr<Msg> m;
+    int peer;
+    hipStream_t s;
+  };
+  struct PendingRecv {
+    void* buf;
+    size_t bytes;
+    int peer;
+    hipStream_t s;
+  };
+  void check_peer(int peer) const {
+    STRIPE_CHECK(peer >= 0 && peer < hub_->world() && peer != rank_, "bad peer " << peer);
+  }
+  void group_end_impl() {
+    try {
+      for (auto& r : recvs_) {
+        auto m = hub_->take(r.peer, rank_);
+        STRIPE_CHECK(m->bytes == r.bytes, "size mismatch: rank " << r.peer << " sent " << m->bytes
+                                                                 << " B, rank " << rank_ << " expects " << r.bytes);
+        if (hub_->device()) {
+          int dev = 0;
+          HIP_CHECK(hipGetDevice(&dev));
+          HIP_CHECK(hipStreamWaitEvent(r.s, m->ready, 0));
+          if (m->src_dev == dev)
+            HIP_CHECK(hipMemcpyAsync(r.buf, m->ptr, r.bytes, hipMemcpyDeviceToDevice, r.s));
+          else
+            HIP_CHECK(hipMemcpyPeerAsync(r.buf, dev, m->ptr, m->src_dev, r.bytes, r.s));
+          HIP_CHECK(hipEventCreateWithFlags(&m->done, hipEventDisableTiming));
+          HIP_CHECK(hipEventRecord(m->done, r.s));
+        } else {
+          std::memcpy(r.buf, m->ptr, r.bytes);
+        }
+        hub_->mark_consumed(m);
+      }
+      recvs_.clear();
+      for (auto& sd : sends_) {
+        hub_->wait_consumed(sd.m, sd.peer);
+        if (hub_->device()) {
+          HIP_CHECK(hipStreamWaitEvent(sd.s, sd.m->done, 0));
+          // the events may be destroyed once enqueued waits reference them
+          HIP_CHECK(hipEventDestroy(sd.m->ready));
+          HIP_CHECK(hipEventDestroy(sd.m->done));
+        }
+      }
+      sends_.clear();
+    } catch (const std::exception& e) {
+      hub_->abort(std::string("rank ") + std::to_string(rank_) + ": " + e.what());
+      throw;
+    }
+  }
+
+  std::shared_ptr<LocalHub> hub_;
+  int rank_;
+  bool in_group_ = false;
+  std::vector<PendingSend> sends_;
+  std::vector<PendingRecv> recvs_;
+};
+
+class CallbackComm final : public Comm {
+ public:
+  CallbackComm(int rank, int world, CallbackOps ops) : rank_(rank), world_(world), ops_(std::move(ops)) {}
+  int rank() const override { return rank_; }
+  int size() const override { return world_; }
+  const char* backend() const override { return "callback"; }
+  bool device_buffers() const override { return false; }
+  void group_start() override { ops_.group_start(); }
+  void send(const void* buf, size_t bytes, int peer, hipStream_t) override { ops_.send(buf, bytes, peer); }
+  void recv(void* buf, size_t bytes, int peer, hipStream_t) override { ops_.recv(buf, bytes, peer); }
+  void group_end() override { ops_.group_end(); }
+  void barrier() override { ops_.barrier(); }
+  void abort(const std::string& why) override { fail("callback comm aborted: " + why); }
+
+ private:
+  int rank_, world_;
+  CallbackOps ops_;
+};
+
+}  // namespace
+
+std::shared_ptr<LocalHub> make_local_hub(int world, bool device, double timeout_s) {
+  STRIPE_CHECK(world >= 1, "world must be >= 1");
+  return std::make_shared<LocalHub>(world, device, timeout_s);
+}
+
+std::unique_ptr<Comm> make_local_comm(const std::shared_ptr<LocalHub>& hub, int rank) {
+  STRIPE_CHECK(rank >= 0 && rank < hub->world(), "bad rank");
+  return std::make_unique<LocalComm>(hub, rank);
+}
+
+std::unique_ptr<Comm> make_callback_comm(int rank, int world, CallbackOps ops) {
+  return std::make_unique<CallbackComm>(rank, world, std::move(ops));
+}
+
+}  // namespace stripe

@@ -1,0 +1,100 @@
+// RCCL backend: grouped ncclSend/ncclRecv over xGMI (replaces MPI_Scatter/Gather,
+// kernel.cu:137,223 and provides the halo exchange the reference lacks, Q6).
+#include <rccl/rccl.h>
+
+#include <cstring>
+
+#include "stripe/comm.h"
+#include "stripe/kernels.h"
+
+namespace stripe {
+
+#define NCCL_CHECK(expr)                                                               \
+  do {                                                                                 \
+    ncclResult_t _r = (expr);                                                          \
+    if (_r != ncclSuccess) {                                                           \
+      std::ostringstream _os;                                                          \
+      _os << __FILE__ << ":" << __LINE__ << ": " #expr " failed: " << ncclGetErrorString(_r); \
+      ::stripe::fail(_os.str());                                                       \
+    }                                                                                  \
+  } while (0)
+
+namespace {
+
+class RcclComm final : public Comm {
+ public:
+  RcclComm(ncclComm_t c, int rank, int world, int device) : comm_(c), rank_(rank), world_(world), dev_(device) {
+    HIP_CHECK(hipSetDevice(dev_));
+    HIP_CHECK(hipStreamCreateWithFlags(&bar_stream_, hipStreamNonBlocking));
+    HIP_CHECK(hipMalloc(&bar_buf_, sizeof(int)));
+  }
+  ~RcclComm() override {
+    if (comm_) {
+      if (aborted_) ncclCommAbort(comm_);
+      else ncclCommDestroy(comm_);
+    }
+    if (bar_buf_) (void)hipFree(bar_buf_);
+    if (bar_stream_) (void)hipStreamDestroy(bar_stream_);
+  }
+  int rank() const override { return rank_; }
+  int size() const override { return world_; }
+  const char* backend() const override { return "rccl"; }
+  bool device_buffers() const override { return true; }
+  void group_start() override { NCCL_CHECK(ncclGroupStart()); }
+  void send(const void* buf, size_t bytes, int peer, hipStream_t s) override {
+    NCCL_CHECK(ncclSend(buf, bytes, ncclUint8, peer, comm_, s));
+  }
+  void recv(void* buf, size_t bytes, int peer, hipStream_t s) override {
+    NCCL_CHECK(ncclRecv(buf, bytes, ncclUint8, peer, comm_, s));
+  }
+  void group_end() override { NCCL_CHECK(ncclGroupEnd()); }
+  void barrier() override {
+    NCCL_CHECK(ncclAllReduce(bar_buf_, bar_buf_, 1, ncclInt32, ncclSum, comm_, bar_stream_));
+    HIP_CHECK(hipStreamSynchronize(bar_stream_));
+  }
+  void abort(const std::string&) override { aborted_ = true; }
+
+ private:
+  ncclComm_t comm_ = nullptr;
+  int rank_, world_, dev_;
+  bool aborted_ = false;
+  hipStream_t bar_stream_ = nullptr;
+  int* bar_buf_ = nullptr;
+};
+
+}  // namespace
+
+UniqueId rccl_unique_id() {
+  ncclUniqueId id;
+  NCCL_CHECK(ncclGetUniqueId(&id));
+  static_assert(sizeof(ncclUniqueId) == 128, "unexpected ncclUniqueId size");
+  UniqueId out;
+  std::memcpy(out.data(), &id, 128);
+  return out;
+}
+
+std::unique_ptr<Comm> make_rccl_comm(const UniqueId& uid, int rank, int world, int device) {
+  HIP_CHECK(hipSetDevice(device));
+  ncclUniqueId id;
+  std::memcpy(&id, uid.data(), 128);
+  ncclComm_t c;
+  NCCL_CHECK(ncclCommInitRank(&c, world, id, rank));
+  return std::make_unique<RcclComm>(c, rank, world, device);
+}
+
+std::vector<std::unique_ptr<Comm>> make_rccl_comms_all(const std::vector<int>& devices) {
+  const int n = (int)devices.size();
+  std::vector<ncclComm_t> comms(n);
+  NCCL_CHECK(ncclCommInitAll(comms.data(), n, devices.data()));
+  std::vector<std::unique_ptr<Comm>> out;
+  for (int r = 0; r < n; ++r) out.push_back(std::make_unique<RcclComm>(comms[r], r, n, devices[r]));
+  return out;
+}
+
+std::string rccl_version() {
+  int v = 0;
+  ncclGetVersion(&v);
+  return std::to_string(v);
+}
+
+}  // namespace stripe

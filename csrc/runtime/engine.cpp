@@ -1,0 +1,462 @@
+// Per-rank stripe engine (see engine.h).
+#include "stripe/engine.h"
+
+#include <cstring>
+#include <exception>
+#include <mutex>
+#include <thread>
+
+namespace stripe {
+
+// ---------------------------------------------------------------------------
+// Buffer
+// ---------------------------------------------------------------------------
+Buffer::Buffer(size_t bytes, bool device) : n_(bytes), dev_(device) {
+  if (bytes == 0) return;
+  if (device) {
+    HIP_CHECK(hipMalloc(&p_, bytes));
+    HIP_CHECK(hipMemset(p_, 0, bytes));
+  } else {
+    p_ = static_cast<uint8_t*>(std::calloc(bytes, 1));
+    STRIPE_CHECK(p_ != nullptr, "host allocation of " << bytes << " bytes failed");
+  }
+}
+
+Buffer::~Buffer() {
+  if (!p_) return;
+  if (dev_) (void)hipFree(p_);
+  else std::free(p_);
+}
+
+Buffer& Buffer::operator=(Buffer&& o) noexcept {
+  if (this != &o) {
+    if (p_) {
+      if (dev_) (void)hipFree(p_);
+      else std::free(p_);
+    }
+    p_ = o.p_;
+    n_ = o.n_;
+    dev_ = o.dev_;
+    o.p_ = nullptr;
+    o.n_ = 0;
+  }
+  return *this;
+}
+
+// ---------------------------------------------------------------------------
+// Engine
+// ---------------------------------------------------------------------------
+Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
+  STRIPE_CHECK(cfg_.W >= 1 && cfg_.H >= 1, "bad image size " << cfg_.W << "x" << cfg_.H);
+  STRIPE_CHECK(cfg_.C == 1 || cfg_.C == 3, "image must have 1 or 3 channels");
+  if (comm_) {
+    rank_ = comm_->rank();
+    world_ = comm_->size();
+    STRIPE_CHECK(comm_->device_buffers() == device(),
+                 "comm backend '" << comm_->backend() << "' does not match the engine backend");
+  }
+  plan_ = compile_chain(parse_chain(cfg_.chain), cfg_.C, cfg_.border, cfg_.fuse);
+  part_ = plan_rows(cfg_.H, world_, std::max(1, plan_.max_radius), cfg_.legacy_partition);
+  halo_ = plan_.max_radius;
+  const Stripe& st = stripe();
+  rows_alloc_ = st.rows + 2 * halo_;
+  const int64_t pmax = padded_pitch(cfg_.W, plan_.max_channels);
+  if (device()) {
+    if (cfg_.device >= 0) HIP_CHECK(hipSetDevice(cfg_.device));
+    HIP_CHECK(hipStreamCreateWithFlags(&s_compute_, hipStreamNonBlocking));
+    HIP_CHECK(hipStreamCreateWithFlags(&s_comm_, hipStreamNonBlocking));
+    own_streams_ = true;
+    for (auto& e : ev_) HIP_CHECK(hipEventCreate(&e));
+  }
+  for (auto& b : buf_) b = Buffer((size_t)std::max(1, rows_alloc_) * pmax, device());
+  zero_ = Buffer((size_t)pmax, device());
+  if (cfg_.root_buffers && rank_ == 0) {
+    root_in_ = Buffer((size_t)cfg_.H * padded_pitch(cfg_.W, plan_.cin), device());
+    root_out_ = Buffer((size_t)cfg_.H * padded_pitch(cfg_.W, plan_.cout), device());
+  }
+  // per-pass constants
+  prt_.resize(plan_.passes.size());
+  for (size_t i = 0; i < plan_.passes.size(); ++i) {
+    const Pass& p = plan_.passes[i];
+    std::vector<uint8_t> l(768);
+    for (int v = 0; v < 256; ++v) {
+      l[v] = p.pro.has_pre ? p.pro.pre[v] : (uint8_t)v;
+      l[256 + v] = p.pro.has_post ? p.pro.post[v] : (uint8_t)v;
+      l[512 + v] = p.has_epi ? p.epi[v] : (uint8_t)v;
+    }
+    prt_[i].luts = Buffer(768, device());
+    if (device()) {
+      HIP_CHECK(hipMemcpy(prt_[i].luts.data(), l.data(), 768, hipMemcpyHostToDevice));
+      if (p.kind == PassKind::Conv) prepare_conv_consts(p, &prt_[i].pc, s_compute_);
+    } else {
+      std::memcpy(prt_[i].luts.data(), l.data(), 768);
+    }
+    prt_[i].pc.luts = prt_[i].luts.data();
+  }
+  cur_c_ = cfg_.C;
+  if (device()) HIP_CHECK(hipDeviceSynchronize());
+}
+
+Engine::~Engine() {
+  if (device()) {
+    (void)hipDeviceSynchronize();
+    for (auto& p : prt_)
+      if (p.pc.conv) (void)hipFree(p.pc.conv);
+    for (auto& e : ev_)
+      if (e) (void)hipEventDestroy(e);
+    if (own_streams_) {
+      (void)hipStreamDestroy(s_comm_);
+      if (s_compute_) (void)hipStreamDestroy(s_compute_);
+    }
+  }
+}
+
+void Engine::use_external_stream(hipStream_t s) {
+  STRIPE_CHECK(device(), "external streams need the device backend");
+  if (own_streams_ && s_compute_) {
+    HIP_CHECK(hipStreamSynchronize(s_compute_));
+    HIP_CHECK(hipStreamDestroy(s_compute_));
+  }
+  s_compute_ = s;
+}
+
+uint8_t* Engine::origin(const Buffer& b, int C) const {
+  return b.data() + (int64_t)halo_ * pitch(C) + kMarginBytes;
+}
+
+uint8_t* Engine::root_origin(const Buffer& b, int C) const {
+  (void)C;
+  return b.data() + kMarginBytes;
+}
+
+const uint8_t* Engine::input_origin() const { return origin(buf_[cur_], cur_c_); }
+const uint8_t* Engine::output_origin() const {
+  STRIPE_CHECK(out_buf_ >= 0, "no output yet");
+  return origin(buf_[out_buf_], out_c_);
+}
+
+RowGeom Engine::geom() const {
+  const Stripe& st = stripe();
+  if (cfg_.halo) return RowGeom{st.row0, cfg_.H};
+  return RowGeom{0, st.rows};  // legacy: each stripe is an image of its own
+}
+
+void Engine::record(hipEvent_t e, hipStream_t s) {
+  if (device()) HIP_CHECK(hipEventRecord(e, s));
+}
+
+float Engine::elapsed(hipEvent_t a, hipEvent_t b) {
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0;
+  return ms;
+}
+
+void Engine::copy2d(void* dst, int64_t dpitch, const void* src, int64_t spitch, int64_t width, int64_t rows,
+                    hipStream_t s, int kind) {
+  (void)kind;
+  if (rows <= 0 || width <= 0) return;
+  if (device()) {
+    HIP_CHECK(hipMemcpy2DAsync(dst, (size_t)dpitch, src, (size_t)spitch, (size_t)width, (size_t)rows,
+                               hipMemcpyDefault, s));
+  } else {
+    for (int64_t r = 0; r < rows; ++r)
+      std::memcpy((uint8_t*)dst + r * dpitch, (const uint8_t*)src + r * spitch, (size_t)width);
+  }
+}
+
+void Engine::fill_margins(uint8_t* org, int C, int y0, int y1, int px, Border b, hipStream_t s) {
+  if (!device()) return;  // the golden path resolves borders by index
+  launch_fill_margins(org, pitch(C), cfg_.W, C, y0, y1, px, b, s);
+}
+
+void Engine::load_synthetic(uint64_t seed) {
+  const Stripe& st = stripe();
+  const int C = plan_.cin;
+  uint8_t* org = origin(buf_[0], C);
+  if (device()) {
+    launch_synth(org, pitch(C), cfg_.W, C, st.row0, st.rows, seed, plan_.in_margin_px, plan_.in_margin_border,
+                 s_compute_);
+  } else {
+    std::vector<uint8_t> tmp((size_t)st.rows * cfg_.W * C);
+    synth_rows(seed, cfg_.W, C, st.row0, st.rows, tmp.data());
+    copy2d(org, pitch(C), tmp.data(), (int64_t)cfg_.W * C, (int64_t)cfg_.W * C, st.rows, nullptr, 0);
+  }
+  cur_ = 0;
+  cur_c_ = C;
+}
+
+void Engine::load_packed(const void* src, bool src_device) {
+  (void)src_device;
+  const Stripe& st = stripe();
+  const int C = plan_.cin;
+  const int64_t E = (int64_t)cfg_.W * C;
+  uint8_t* org = origin(buf_[0], C);
+  record(ev_[6], s_compute_);
+  copy2d(org, pitch(C), src, E, E, st.rows, s_compute_, 0);
+  fill_margins(org, C, 0, st.rows, plan_.in_margin_px, plan_.in_margin_border, s_compute_);
+  record(ev_[7], s_compute_);
+  cur_ = 0;
+  cur_c_ = C;
+}
+
+void Engine::load_root(const void* full, bool src_device) {
+  (void)src_device;
+  if (rank_ != 0) return;
+  STRIPE_CHECK(root_in_.data() != nullptr, "root buffers not allocated (EngineConfig::root_buffers)");
+  const int C = plan_.cin;
+  const int64_t E = (int64_t)cfg_.W * C;
+  uint8_t* org = root_origin(root_in_, C);
+  copy2d(org, pitch(C), full, E, E, cfg_.H, s_compute_, 0);
+  fill_margins(org, C, 0, cfg_.H, plan_.in_margin_px, plan_.in_margin_border, s_compute_);
+}
+
+void Engine::load_root_synthetic(uint64_t seed) {
+  if (rank_ != 0) return;
+  STRIPE_CHECK(root_in_.data() != nullptr, "root buffers not allocated (EngineConfig::root_buffers)");
+  const int C = plan_.cin;
+  uint8_t* org = root_origin(root_in_, C);
+  if (device()) {
+    launch_synth(org, pitch(C), cfg_.W, C, 0, cfg_.H, seed, plan_.in_margin_px, plan_.in_margin_border,
+                 s_compute_);
+  } else {
+    std::vector<uint8_t> tmp((size_t)cfg_.H * cfg_.W * C);
+    synth_rows(seed, cfg_.W, C, 0, cfg_.H, tmp.data());
+    copy2d(org, pitch(C), tmp.data(), (int64_t)cfg_.W * C, (int64_t)cfg_.W * C, cfg_.H, nullptr, 0);
+  }
+}
+
+void Engine::scatter() {
+  const int C = plan_.cin;
+  const int64_t P = pitch(C);
+  const Stripe& st = stripe();
+  record(ev_[2], s_compute_);
+  if (rank_ == 0) {
+    STRIPE_CHECK(root_in_.data() != nullptr, "root buffers not allocated (EngineConfig::root_buffers)");
+    const uint8_t* src = root_origin(root_in_, C) - kMarginBytes;
+    if (comm_ && part_.active > 1) {
+      comm_->group_start();
+      for (int r = 1; r < part_.active; ++r) {
+        const Stripe& sr = part_.of(r);
+        comm_->send(src + (int64_t)sr.row0 * P, (size_t)(sr.rows * P), r, s_compute_);
+      }
+      comm_->group_end();
+    }
+    uint8_t* dst = origin(buf_[0], C) - kMarginBytes;
+    if (device())
+      HIP_CHECK(hipMemcpyAsync(dst, src + (int64_t)st.row0 * P, (size_t)(st.rows * P), hipMemcpyDeviceToDevice,
+                               s_compute_));
+    else
+      std::memcpy(dst, src + (int64_t)st.row0 * P, (size_t)(st.rows * P));
+  } else if (st.rows > 0) {
+    comm_->group_start();
+    comm_->recv(origin(buf_[0], C) - kMarginBytes, (size_t)(st.rows * P), 0, s_compute_);
+    comm_->group_end();
+  }
+  record(ev_[3], s_compute_);
+  cur_ = 0;
+  cur_c_ = C;
+}
+
+void Engine::exchange_halo(uint8_t* org, int C, int R, hipStream_t s) {
+  const Stripe& st = stripe();
+  if (st.rows == 0 || part_.active <= 1) return;
+  const int64_t P = pitch(C);
+  const size_t bytes = (size_t)(R * P);
+  uint8_t* base = org - kMarginBytes;
+  const int up = rank_ > 0 ? rank_ - 1 : -1;
+  const int down = rank_ + 1 < part_.active ? rank_ + 1 : -1;
+  comm_->group_start();
+  if (up >= 0) {
+    comm_->send(base, bytes, up, s);
+    comm_->recv(base - (int64_t)R * P, bytes, up, s);
+  }
+  if (down >= 0) {
+    comm_->send(base + (int64_t)(st.rows - R) * P, bytes, down, s);
+    comm_->recv(base + (int64_t)st.rows * P, bytes, down, s);
+  }
+  comm_->group_end();
+}
+
+void Engine::run_pass(const Pass& p, const uint8_t* in, uint8_t* out) {
+  const Stripe& st = stripe();
+  const int rows = st.rows;
+  if (rows == 0) return;
+  const RowGeom g = geom();
+  const int R = p.R;
+  const bool xchg = cfg_.halo && R > 0 && part_.active > 1;
+  if (!device()) {
+    if (xchg) exchange_halo(const_cast<uint8_t*>(in), p.cin, R, nullptr);
+    golden_pass(p, ConstView{in, pitch(p.cin)}, MutView{out, pitch(p.cout)}, cfg_.W, g, 0, rows);
+    return;
+  }
+  const size_t pi = (size_t)(&p - plan_.passes.data());
+  const PassConsts& pc = prt_[pi].pc;
+  PassLaunch L;
+  L.in = in;
+  L.in_pitch = pitch(p.cin);
+  L.out = out;
+  L.out_pitch = pitch(p.cout);
+  L.W = cfg_.W;
+  L.rows = rows;
+  L.row0 = g.row0;
+  L.Hg = g.Hg;
+  L.zero_row = zero_.data() + kMarginBytes;
+  L.band = cfg_.band;
+  if (!xchg) {
+    L.nrange = 1;
+    L.ry[0] = 0;
+    L.ry[1] = rows;
+    launch_pass(p, pc, L, s_compute_);
+  } else if (cfg_.overlap && rows > 2 * R) {
+    // halo rows fly on the comm stream while the interior rows are computed
+    HIP_CHECK(hipEventRecord(ev_[4], s_compute_));
+    HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_[4], 0));
+    exchange_halo(const_cast<uint8_t*>(in), p.cin, R, s_comm_);
+    HIP_CHECK(hipEventRecord(ev_[5], s_comm_));
+    L.nrange = 1;
+    L.ry[0] = R;
+    L.ry[1] = rows - R;
+    launch_pass(p, pc, L, s_compute_);
+    HIP_CHECK(hipStreamWaitEvent(s_compute_, ev_[5], 0));
+    L.nrange = 2;
+    L.ry[0] = 0;
+    L.ry[1] = R;
+    L.ry[2] = rows - R;
+    L.ry[3] = rows;
+    launch_pass(p, pc, L, s_compute_);
+  } else {
+    exchange_halo(const_cast<uint8_t*>(in), p.cin, R, s_compute_);
+    L.nrange = 1;
+    L.ry[0] = 0;
+    L.ry[1] = rows;
+    launch_pass(p, pc, L, s_compute_);
+  }
+}
+
+void Engine::run(int iterations) {
+  STRIPE_CHECK(iterations >= 1, "iterations must be >= 1");
+  STRIPE_CHECK(iterations == 1 || plan_.cout == plan_.cin,
+               "iterating a chain needs equal input/output channels (" << plan_.cin << "->" << plan_.cout << ")");
+  record(ev_[0], s_compute_);
+  for (int it = 0; it < iterations; ++it) {
+    STRIPE_CHECK(cur_c_ == plan_.cin, "engine input has " << cur_c_ << " channels, chain expects " << plan_.cin);
+    for (const Pass& p : plan_.passes) {
+      run_pass(p, origin(buf_[cur_], p.cin), origin(buf_[cur_ ^ 1], p.cout));
+      cur_ ^= 1;
+    }
+    cur_c_ = plan_.cout;
+  }
+  record(ev_[1], s_compute_);
+  out_buf_ = cur_;
+  out_c_ = plan_.cout;
+}
+
+void Engine::store_packed(void* dst, bool dst_device) {
+  (void)dst_device;
+  STRIPE_CHECK(out_buf_ >= 0, "store_packed before run");
+  const int C = out_c_;
+  const int64_t E = (int64_t)cfg_.W * C;
+  copy2d(dst, E, origin(buf_[out_buf_], C), pitch(C), E, stripe().rows, s_compute_, 0);
+}
+
+void Engine::gather() {
+  STRIPE_CHECK(out_buf_ >= 0, "gather before run");
+  const int C = out_c_;
+  const int64_t P = pitch(C);
+  const Stripe& st = stripe();
+  record(ev_[2], s_compute_);
+  const uint8_t* src = origin(buf_[out_buf_], C) - kMarginBytes;
+  if (rank_ == 0) {
+    STRIPE_CHECK(root_out_.data() != nullptr, "root buffers not allocated (EngineConfig::root_buffers)");
+    uint8_t* dst = root_origin(root_out_, C) - kMarginBytes;
+    if (comm_ && part_.active > 1) {
+      comm_->group_start();
+      for (int r = 1; r < part_.active; ++r) {
+        const Stripe& sr = part_.of(r);
+        comm_->recv(dst + (int64_t)sr.row0 * P, (size_t)(sr.rows * P), r, s_compute_);
+      }
+      comm_->group_end();
+    }
+    if (device())
+      HIP_CHECK(hipMemcpyAsync(dst + (int64_t)st.row0 * P, src, (size_t)(st.rows * P), hipMemcpyDeviceToDevice,
+                               s_compute_));
+    else
+      std::memcpy(dst + (int64_t)st.row0 * P, src, (size_t)(st.rows * P));
+  } else if (st.rows > 0) {
+    comm_->group_start();
+    comm_->send(src, (size_t)(st.rows * P), 0, s_compute_);
+    comm_->group_end();
+  }
+  record(ev_[3], s_compute_);
+}
+
+void Engine::store_root(void* full, bool dst_device) {
+  (void)dst_device;
+  if (rank_ != 0) return;
+  const int C = out_c_ > 0 ? out_c_ : plan_.cout;
+  const int64_t E = (int64_t)cfg_.W * C;
+  copy2d(full, E, root_origin(root_out_, C), pitch(C), E, cfg_.H, s_compute_, 0);
+}
+
+void Engine::synchronize() {
+  if (!device()) return;
+  HIP_CHECK(hipStreamSynchronize(s_compute_));
+  HIP_CHECK(hipStreamSynchronize(s_comm_));
+  times_.run = elapsed(ev_[0], ev_[1]);
+}
+
+// ---------------------------------------------------------------------------
+// In-process group driver
+// ---------------------------------------------------------------------------
+Image run_group(const EngineConfig& cfg, const std::vector<Comm*>& comms, const std::vector<int>& devices,
+                const Image& input, int iterations, PhaseTimes* times) {
+  STRIPE_CHECK(input.W == cfg.W && input.H == cfg.H && input.C == cfg.C, "input does not match the config");
+  const int world = (int)comms.size();
+  Image out;
+  std::mutex mu;
+  std::exception_ptr err;
+  auto body = [&](int r) {
+    try {
+      EngineConfig c = cfg;
+      c.root_buffers = true;
+      if (!devices.empty()) c.device = devices[r];
+      Engine e(c, comms[r]);
+      if (r == 0) e.load_root(input.data.data(), false);
+      e.scatter();
+      e.run(iterations);
+      e.gather();
+      if (r == 0) {
+        Image o(cfg.W, cfg.H, e.out_channels());
+        e.store_root(o.data.data(), false);
+        e.synchronize();
+        std::lock_guard<std::mutex> lk(mu);
+        out = std::move(o);
+        if (times) *times = e.times();
+      }
+      e.synchronize();
+      comms[r]->barrier();
+    } catch (...) {
+      std::lock_guard<std::mutex> lk(mu);
+      if (!err) err = std::current_exception();
+      comms[r]->abort("rank " + std::to_string(r) + " failed");
+    }
+  };
+  std::vector<std::thread> th;
+  for (int r = 0; r < world; ++r) th.emplace_back(body, r);
+  for (auto& t : th) t.join();
+  if (err) std::rethrow_exception(err);
+  return out;
+}
+
+Image run_local_group(const EngineConfig& cfg, int world, const Image& input, int iterations, PhaseTimes* times) {
+  auto hub = make_local_hub(world, cfg.backend == BackendKind::Device);
+  std::vector<std::unique_ptr<Comm>> owned;
+  std::vector<Comm*> comms;
+  for (int r = 0; r < world; ++r) {
+    owned.push_back(make_local_comm(hub, r));
+    comms.push_back(owned.back().get());
+  }
+  return run_group(cfg, comms, {}, input, iterations, times);
+}
+
+}  // namespace stripe
