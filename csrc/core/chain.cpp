@@ -215,6 +215,12 @@ Plan compile_chain(const std::vector<Op>& ops, int cin, Border default_border, b
   }
   plan.in_margin_px = next_r;
   plan.in_margin_border = next_b;
+  // a chain that maps C -> C can be iterated (ping-pong): the last pass then
+  // feeds the first one, so it must maintain the first pass's input margins
+  if (plan.cout == plan.cin && plan.passes.back().out_margin_px < plan.in_margin_px) {
+    plan.passes.back().out_margin_px = plan.in_margin_px;
+    plan.passes.back().out_margin_border = plan.in_margin_border;
+  }
   plan.max_radius = 0;
   plan.max_channels = cin;
   for (const Pass& p : plan.passes) {

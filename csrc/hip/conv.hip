@@ -51,7 +51,9 @@ __global__ __launch_bounds__(256) void k_conv_mfma(ConvArgs ca) {
     __syncthreads();
     for (int i = tid; i < rows_in * kCTK; i += 256) {
       const int r = i / kCTK, px = i % kCTK;
-      const uint8_t* row = in_row(a, yb - R + r);
+      // rows past the range's last needed input row (ry1 - 1 + R) feed only
+      // outputs that are not stored; clamp so no read leaves the stripe + halo
+      const uint8_t* row = in_row(a, min(yb - R + r, a.ry1 - 1 + R));
       int x = x0 - R + px;
       // pixels beyond the right margin are never used by valid outputs; clamp reads
       if (x > a.W - 1 + R) x = a.W - 1 + R;

@@ -187,6 +187,7 @@ void launch_fill_margins(uint8_t* origin, int64_t pitch, int W, int C, int y0, i
                          hipStream_t s) {
   if (px <= 0 || y1 <= y0) return;
   STRIPE_CHECK(px <= margin_pixels(C), "margin of " << px << " px does not fit");
+  (void)hipGetLastError();
   dev::k_fill_margins<<<dim3(1, (unsigned)(y1 - y0)), dev::kNT, 0, s>>>(origin, pitch, W, C, y0, px, (int)b);
   HIP_CHECK(hipGetLastError());
 }
@@ -196,6 +197,7 @@ void launch_synth(uint8_t* origin, int64_t pitch, int W, int C, int row0, int ro
   if (rows <= 0) return;
   const int64_t E = (int64_t)W * C;
   const unsigned gx = (unsigned)std::min<int64_t>(div_up(E, 4 * dev::kNT), 64);
+  (void)hipGetLastError();
   dev::k_synth<<<dim3(gx, (unsigned)rows), dev::kNT, 0, s>>>(origin, pitch, E, row0, seed);
   HIP_CHECK(hipGetLastError());
   launch_fill_margins(origin, pitch, W, C, 0, rows, margin_px, b, s);

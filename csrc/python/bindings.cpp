@@ -241,7 +241,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readonly("scatter", &PhaseTimes::scatter)
       .def_readonly("gather", &PhaseTimes::gather);
 
-  py::class_<Engine>(m, "Engine")
+  py::class_<Engine>(m, "Engine", py::dynamic_attr())
       .def(py::init([](const EngineConfig& cfg, PyComm* comm) {
              py::gil_scoped_release nogil;
              return std::make_unique<Engine>(cfg, comm ? comm->comm.get() : nullptr);

@@ -45,7 +45,9 @@ def test_margin_contracts(C):
     r = [p["R"] for p in info["passes"]]
     m = [p["out_margin_px"] for p in info["passes"]]
     assert info["in_margin_px"] == r[0]
-    assert m[-1] == 0 and m[0] == r[1]
+    assert m[-1] == r[0] and m[0] == r[1]  # cyclic: iterating feeds pass 0 again
+    info = C.plan_info("gray,gaussian5", 3)
+    assert info["passes"][-1]["out_margin_px"] == 0  # 3 -> 1 channels cannot iterate
 
 
 def test_unfused_plan(C):
