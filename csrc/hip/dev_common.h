@@ -34,7 +34,21 @@ struct KArgs {
   uint32_t gmul[3];
   int gshift[3];
   int cin;        // pointwise: input channels
+  // buffer-descriptor view (stencil kernels): offsets of the origins in the
+  // allocations; every hot-loop load/store is a raw buffer op whose range check
+  // masks inactive lanes (no divergent branches around memory ops, so hipcc's
+  // vmcnt bookkeeping stays exact and prefetched rows stay in flight)
+  const uint8_t* in_base;
+  uint8_t* out_base;
+  uint32_t in_bytes, in_org, in_zero;
+  uint32_t out_bytes, out_org;
 };
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+constexpr uint32_t kOOB = 0x80000000u;  // lane offset bias that fails the range check
 
 __device__ __forceinline__ int border_index_dev(int i, int n, int b) {
   if (i >= 0 && i < n) return i;
@@ -58,6 +72,18 @@ __device__ __forceinline__ const uint8_t* in_row(const KArgs& a, int y) {
   return a.in + (int64_t)(g - a.row0) * a.in_pitch;
 }
 
+// Byte offset (in the input allocation) of local row y's origin, global-edge
+// border applied (scalar; no memory access).
+__device__ __forceinline__ uint32_t in_row_off(const KArgs& a, int y) {
+  int g = a.row0 + y;
+  if (g < 0 || g >= a.Hg) {
+    const int m = border_index_dev(g, a.Hg, a.border);
+    if (m < 0) return a.in_zero;
+    g = m;
+  }
+  return a.in_org + (uint32_t)((int64_t)(g - a.row0) * a.in_pitch);
+}
+
 // Row range of workgroup row `by`.
 __device__ __forceinline__ void band_range(const KArgs& a, int by, int& ys, int& ye) {
   if (by < a.nb0) {
@@ -71,12 +97,6 @@ __device__ __forceinline__ void band_range(const KArgs& a, int by, int& ys, int&
 
 __device__ __forceinline__ uint32_t byte_of(const uint32_t (&d)[4], int j) {
   return (d[j >> 2] >> ((j & 3) * 8)) & 0xFFu;
-}
-
-// Dynamic byte select without scratch (cndmask chain).
-__device__ __forceinline__ uint32_t byte_dyn(const uint32_t (&d)[4], int j) {
-  const uint32_t w = j < 4 ? d[0] : (j < 8 ? d[1] : (j < 12 ? d[2] : d[3]));
-  return (w >> ((j & 3) * 8)) & 0xFFu;
 }
 
 __device__ __forceinline__ uint32_t pack4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
@@ -118,41 +138,22 @@ __device__ __forceinline__ void lut16(const uint8_t* lut, uint32_t (&o)[4]) {
 }
 
 // Store 16 output bytes at row + cb; only bytes < E (straddling chunk is split).
+// Static byte indices only (a dynamic index would put `o` in scratch).
 __device__ __forceinline__ void store_chunk(uint8_t* row, int cb, int E, const uint32_t (&o)[4]) {
   if (cb + 16 <= E) {
     *reinterpret_cast<uint4*>(row + cb) = make_uint4(o[0], o[1], o[2], o[3]);
   } else {
-    for (int j = 0; j < E - cb; ++j) row[cb + j] = (uint8_t)byte_dyn(o, j);
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (cb + j < E) row[cb + j] = (uint8_t)byte_of(o, j);
   }
 }
 
-// Maintain the x-margins of an output row: margin pixel m (m < 0 or m >= W) takes
-// the value of pixel border_index(m).  Each lane writes the margin bytes whose
-// source lies in its own 16-byte chunk [cb, cb+16).  Only edge lanes do work.
+// True for lanes whose chunk needs the cold path (straddles E or feeds margins).
 template <int C>
-__device__ __forceinline__ void write_margins(uint8_t* row, int cb, const KArgs& a, const uint32_t (&o)[4]) {
-  const int px = a.out_px;
-  if (px == 0) return;
-  const int E = a.W * C;
-  const int reach = (px + 1) * C + 16;
-  if (cb >= reach && cb + 16 <= E - reach) return;  // interior lane
-  for (int k = 1; k <= px; ++k) {
-#pragma unroll
-    for (int side = 0; side < 2; ++side) {
-      const int m = side == 0 ? -k : a.W - 1 + k;
-      const int s = border_index_dev(m, a.W, a.out_border);
-#pragma unroll
-      for (int c = 0; c < C; ++c) {
-        const int dst = m * C + c;
-        if (s < 0) {
-          if (cb == 0) row[dst] = 0;  // constant border: one lane writes the zeros
-          continue;
-        }
-        const int sb = s * C + c - cb;
-        if (sb >= 0 && sb < 16 && cb + sb < E) row[dst] = (uint8_t)byte_dyn(o, sb);
-      }
-    }
-  }
+__device__ __forceinline__ bool edge_lane(int cb, int E, int px) {
+  const int reach = (px + 1) * C;
+  return cb + 16 > E || (px > 0 && (cb < reach || cb + 16 > E - reach));
 }
 
 }  // namespace dev

@@ -5,15 +5,20 @@
 // separate gray/contrast launches before it.  Here:
 //   * workgroup = 256 lanes x 16 output bytes = one 4 KiB row segment (254 output
 //     chunks + one halo chunk each side), marching down a band of rows;
-//   * each lane loads its 16-byte chunk of every input row once (dwordx4), applies
-//     the fused prologue (gray / LUT) in registers;
-//   * separable filters: the vertical taps run in registers (SWAR, two 16-bit
-//     sums per dword), one row of vertical sums goes through LDS (double-buffered,
-//     one barrier per row) for the horizontal taps;
+//   * each lane loads its 16-byte chunk of every input row once (buffer dwordx4,
+//     two rows in flight), applies the fused prologue (gray / LUT) in registers;
+//   * separable filters: vertical taps in registers as packed-u16 adds - the
+//     binomial Gaussians as a cascade of K-1 two-tap sums (no row ring) - one row
+//     of vertical sums through LDS (double-buffered, one barrier per row), the
+//     horizontal taps as packed-u16 multiply-adds on v_alignbyte-shifted pairs;
 //   * non-separable filters: a (K+1)-row LDS ring of prologue-applied rows; taps
 //     are compile-time literals (zero taps vanish);
-//   * out-of-place, deterministic; x-borders come from the buffer margins, the
-//     y-border from a scalar row remap; the epilogue maintains the output margins.
+//   * every hot-loop load/store is an unconditional raw buffer op; inactive lanes
+//     get an offset that fails the descriptor range check (no divergent branches
+//     around memory ops -> exact vmcnt, prefetches survive the barriers);
+//   * out-of-place and deterministic; the x-border comes from the buffer margins,
+//     the y-border from a scalar row remap; edge workgroups rewrite the output
+//     margins after their band (one vmcnt(0) + barrier per band).
 #include "dev_common.h"
 #include "stripe/kernels.h"
 #include "stripe/stencil_defs.h"
@@ -25,22 +30,27 @@ constexpr int kOutChunks = kNT - 2;  // output chunks per workgroup row segment
 
 enum { PRO_NONE = 0, PRO_LUT = 1, PRO_GRAY = 2 };
 
-// Load the lane's 16 output-channel bytes of input row `row` (after the prologue).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
+__device__ __forceinline__ uint32_t as_u32(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+
+// Load the lane's 16 output-channel bytes of the input row at `row_off`
+// (after the prologue).  `lane_off` carries kOOB for lanes that must not load.
 template <int PRO>
-__device__ __forceinline__ void load_chunk(const KArgs& a, const uint8_t* row, int cb, bool ld,
-                                           const uint8_t* lut_post, uint32_t (&o)[4]) {
-  if (!ld) {
-    o[0] = o[1] = o[2] = o[3] = 0;
-    return;
-  }
+__device__ __forceinline__ void load_chunk(const KArgs& a, __amdgpu_buffer_rsrc_t rin, uint32_t row_off,
+                                           uint32_t lane_off, const uint8_t* lut_post, uint32_t (&o)[4]) {
   if constexpr (PRO == PRO_GRAY) {
-    const uint4* p = reinterpret_cast<const uint4*>(row + 3 * cb);
-    const uint4 v0 = p[0], v1 = p[1], v2 = p[2];
+    const uint32_t off = row_off + lane_off;  // lane_off already scaled by 3
+    const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(rin, off, 0, 0);
+    const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(rin, off + 16, 0, 0);
+    const u32x4 v2 = __builtin_amdgcn_raw_buffer_load_b128(rin, off + 32, 0, 0);
     const uint32_t rgb[12] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, v2.z, v2.w};
     gray16(a, rgb, o);
     if (a.has_post) lut16(lut_post, o);
   } else {
-    const uint4 v = *reinterpret_cast<const uint4*>(row + cb);
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rin, row_off + lane_off, 0, 0);
     o[0] = v.x;
     o[1] = v.y;
     o[2] = v.z;
@@ -53,45 +63,144 @@ __device__ __forceinline__ void load_luts(const KArgs& a, uint8_t* lds) {
   for (int i = threadIdx.x; i < 768; i += kNT) lds[i] = a.luts[i];
 }
 
-// Final per-byte stage shared by both stencil forms.
+// Legacy skip border (kernel.cu:83 interior-only bounds): bytes of pixels in the
+// skip region keep the prologue value.
 template <int C>
-__device__ __forceinline__ void finish_row(const KArgs& a, uint8_t* orow, int cb, int gy, int R,
-                                           const uint8_t* lut_epi, const uint32_t (&center)[4],
+__device__ __forceinline__ void apply_skip(const KArgs& a, int cb, int gy, int R, const uint32_t (&center)[4],
                                            uint32_t (&o)[4]) {
-  if (a.border == (int)Border::Skip) {
-    const bool row_skip = gy <= R || gy >= a.Hg - R;
+  const bool row_skip = gy <= R || gy >= a.Hg - R;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      uint32_t w = o[q];
+  for (int q = 0; q < 4; ++q) {
+    uint32_t w = o[q];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int x = (cb + 4 * q + e) / C;
-        if (row_skip || x <= R || x >= a.W - R)
-          w = (w & ~(0xFFu << (8 * e))) | (center[q] & (0xFFu << (8 * e)));
-      }
-      o[q] = w;
+    for (int e = 0; e < 4; ++e) {
+      const int x = (cb + 4 * q + e) / C;
+      const uint32_t m = 0xFFu << (8 * e);
+      w = (row_skip || x <= R || x >= a.W - R) ? ((w & ~m) | (center[q] & m)) : w;
     }
+    o[q] = w;
   }
-  if (a.has_epi) lut16(lut_epi, o);
-  store_chunk(orow, cb, a.E, o);
-  write_margins<C>(orow, cb, a, o);
+}
+
+// After a band: edge workgroups rewrite the x-margins of their output rows
+// (margin pixel m <- pixel border_index(m) of the same row).  Reads use sc0 so
+// they see this CU's completed stores.
+template <int C>
+__device__ __forceinline__ void band_margins(const KArgs& a, int ys, int ye) {
+  const int px = a.out_px;
+  if (px == 0) return;
+  const int E = a.W * C;
+  const bool left = blockIdx.x == 0;
+  const bool right = (int)(blockIdx.x + 1) * kOutChunks * 16 >= E;
+  if (!left && !right) return;
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this band's stores are done
+  __syncthreads();
+  const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
+  const int nb = px * C;  // margin bytes per side
+  const int per_row = 2 * nb;
+  for (int i = threadIdx.x; i < (ye - ys) * per_row; i += kNT) {
+    const int y = ys + i / per_row;
+    const int t = i % per_row;
+    const int side = t >= nb;
+    const int k = (side ? t - nb : t) / C + 1;
+    const int c = (side ? t - nb : t) % C;
+    if ((side == 0 && !left) || (side == 1 && !right)) continue;
+    const int m = side ? a.W - 1 + k : -k;
+    const int src = border_index_dev(m, a.W, a.out_border);
+    const uint32_t row = a.out_org + (uint32_t)((int64_t)y * a.out_pitch);
+    uint8_t v = 0;
+    if (src >= 0) v = __builtin_amdgcn_raw_buffer_load_b8(rout, row + src * C + c, 0, 1);
+    __builtin_amdgcn_raw_buffer_store_b8(v, rout, row + m * C + c, 0, 0);
+  }
 }
 
 // ------------------------------------------------------------------------------
 // Separable filters (gaussian3/5/7, box3/5)
 // ------------------------------------------------------------------------------
-template <int C, class F, int PRO>
-__global__ __launch_bounds__(kNT) void k_sep(KArgs a) {
+__device__ __forceinline__ void unpack16(const uint32_t (&r)[4], uint32_t (&p)[8]) {
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    p[2 * d] = __builtin_amdgcn_perm(0u, r[d], 0x0c010c00u);      // (b0, b1)
+    p[2 * d + 1] = __builtin_amdgcn_perm(0u, r[d], 0x0c030c02u);  // (b2, b3)
+  }
+}
+
+template <class F>
+struct SepTraits {
+  static constexpr int gsum() {
+    int s = 0;
+    for (int i = 0; i < F::K; ++i) s += F::g(i);
+    return s;
+  }
+  static constexpr int log2div() {
+    int l = 0;
+    while ((1 << l) < F::DIV) ++l;
+    return (1 << l) == F::DIV ? l : -1;
+  }
+  // horizontal sums (+ rounding) fit 16 bits and the division is a shift
+  static constexpr bool H16 = log2div() >= 0 && gsum() * gsum() * 255 + F::DIV / 2 < 65536;
+};
+
+// u16 pair (v[k], v[k+1]) of the window (k: u16 index, compile-time after unroll)
+template <int WDW>
+__device__ __forceinline__ uint32_t pair_at(const uint32_t (&w)[WDW], int k) {
+  return (k & 1) ? __builtin_amdgcn_alignbyte(w[(k + 1) >> 1], w[(k - 1) >> 1], 2) : w[k >> 1];
+}
+
+// Vertical filter state.  Binomial filters: cascade of K-1 two-tap sums
+// s_k[y] = s_{k-1}[y] + s_{k-1}[y-1] (K-1 state rows); others: the last K rows.
+template <class F>
+struct VState {
+  static constexpr int NS = F::BINOM ? F::K - 1 : F::K;
+  uint32_t s[NS][8];
+};
+
+// Push one unpacked row; `v` receives the vertical sums of the row R above it.
+template <class F>
+__device__ __forceinline__ void vpush(const uint32_t (&row)[8], const VState<F>& prev, VState<F>& next,
+                                      uint32_t (&v)[8]) {
+  if constexpr (F::BINOM) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      uint32_t cur = row[k];
+#pragma unroll
+      for (int st = 0; st < F::K - 1; ++st) {
+        next.s[st][k] = cur;
+        cur = as_u32(as_u16x2(cur) + as_u16x2(prev.s[st][k]));
+      }
+      v[k] = cur;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+#pragma unroll
+      for (int i = 0; i < F::K - 1; ++i) next.s[i][k] = prev.s[i + 1][k];
+      next.s[F::K - 1][k] = row[k];
+      u16x2 acc = as_u16x2(next.s[0][k]) * (unsigned short)F::g(0);
+#pragma unroll
+      for (int i = 1; i < F::K; ++i) acc += as_u16x2(next.s[i][k]) * (unsigned short)F::g(i);
+      v[k] = as_u32(acc);
+    }
+  }
+}
+
+template <int C, class F, int PRO, bool SKIP>
+__global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : 4)) void k_sep(KArgs a) {
   constexpr int R = F::R, K = F::K;
   constexpr int WLO = (R * C <= 8) ? 8 : 16;  // u16 window start (relative to chunk)
   constexpr int WDW = (2 * WLO + 16) / 2;     // window dwords
+  constexpr int CIN = PRO == PRO_GRAY ? 3 : 1;  // input bytes per output byte
+  using T = SepTraits<F>;
   __shared__ __attribute__((aligned(16))) uint32_t vbuf[2][kNT * 8];
   __shared__ uint8_t luts[768];
 
   const int tid = threadIdx.x;
   const int cb = (int)blockIdx.x * (kOutChunks * 16) - 16 + tid * 16;
-  const bool ld = cb < a.E + 16;
   const bool st = tid >= 1 && tid <= kNT - 2 && cb < a.E;
+  const uint32_t lane_in = cb < a.E + 16 ? (uint32_t)(cb * CIN) : kOOB;
+  const uint32_t lane_out = st ? (uint32_t)cb : kOOB;
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);
+  const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
   int ys, ye;
   band_range(a, blockIdx.y, ys, ye);
   if (ys >= ye) return;
@@ -99,98 +208,124 @@ __global__ __launch_bounds__(kNT) void k_sep(KArgs a) {
     load_luts(a, luts);
     __syncthreads();
   }
+  const uint32_t last_row = in_row_off(a, ye - 1 + R);
 
-  // ring of K rows, SWAR split: lo holds bytes 0,2 / hi bytes 1,3 of each dword
-  uint32_t lo[K][4], hi[K][4];
-  auto put = [&](int slot, const uint32_t (&r)[4]) {
+  VState<F> sa, sb;
 #pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      lo[slot][d] = r[d] & 0x00FF00FFu;
-      hi[slot][d] = (r[d] >> 8) & 0x00FF00FFu;
-    }
-  };
+  for (int i = 0; i < VState<F>::NS; ++i)
 #pragma unroll
-  for (int i = 0; i < K - 1; ++i) {
-    uint32_t r[4];
-    load_chunk<PRO>(a, in_row(a, ys - R + i), cb, ld, luts + 256, r);
-    put(i + 1, r);
+    for (int k = 0; k < 8; ++k) sa.s[i][k] = 0;
+  uint32_t vdummy[8];
+#pragma unroll
+  for (int i = 0; i < K - 1; ++i) {  // prime with rows ys-R .. ys+R-1
+    uint32_t r[4], u[8];
+    load_chunk<PRO>(a, rin, in_row_off(a, ys - R + i), lane_in, luts + 256, r);
+    unpack16(r, u);
+    if (i & 1) vpush<F>(u, sb, sa, vdummy);
+    else vpush<F>(u, sa, sb, vdummy);
   }
-  uint32_t nxt[4];
-  load_chunk<PRO>(a, in_row(a, ys + R), cb, ld, luts + 256, nxt);
+  // two rows in flight per lane (one buffer per row parity); loads past the band
+  // re-read its last input row (unconditional: no branch around the load)
+  uint32_t nxa[4], nxb[4];
+  load_chunk<PRO>(a, rin, in_row_off(a, ys + R), lane_in, luts + 256, nxa);
+  load_chunk<PRO>(a, rin, ys + 1 < ye ? in_row_off(a, ys + 1 + R) : last_row, lane_in, luts + 256, nxb);
 
-  for (int y = ys; y < ye; ++y) {
-#pragma unroll
-    for (int i = 0; i < K - 1; ++i)
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        lo[i][d] = lo[i + 1][d];
-        hi[i][d] = hi[i + 1][d];
-      }
-    put(K - 1, nxt);
-    if (y + 1 < ye) load_chunk<PRO>(a, in_row(a, y + 1 + R), cb, ld, luts + 256, nxt);
-
-    // vertical taps in registers
-    uint32_t vv[8];
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      uint32_t sl = 0, sh = 0;
-#pragma unroll
-      for (int i = 0; i < K; ++i) {
-        sl += (uint32_t)F::g(i) * lo[i][d];
-        sh += (uint32_t)F::g(i) * hi[i][d];
-      }
-      vv[2 * d] = __builtin_amdgcn_perm(sh, sl, 0x05040100u);      // (v[4d],   v[4d+1])
-      vv[2 * d + 1] = __builtin_amdgcn_perm(sh, sl, 0x07060302u);  // (v[4d+2], v[4d+3])
-    }
+  auto row_step = [&](int y, const VState<F>& prev, VState<F>& next, uint32_t (&nb)[4], bool valid) {
+    uint32_t u[8], vv[8];
+    unpack16(nb, u);
+    load_chunk<PRO>(a, rin, y + 2 < ye ? in_row_off(a, y + 2 + R) : last_row, lane_in, luts + 256, nb);
+    vpush<F>(u, prev, next, vv);
     uint32_t* vb = vbuf[y & 1];
     reinterpret_cast<uint4*>(vb + tid * 8)[0] = make_uint4(vv[0], vv[1], vv[2], vv[3]);
     reinterpret_cast<uint4*>(vb + tid * 8)[1] = make_uint4(vv[4], vv[5], vv[6], vv[7]);
     __syncthreads();
-    if (!st) continue;
-
+    // lanes 0 and 255 (halo chunks) compute garbage and their store is masked
+    const int rl = tid == 0 ? 1 : (tid == kNT - 1 ? kNT - 2 : tid);  // keep LDS reads in bounds
     uint32_t w[WDW];
 #pragma unroll
     for (int q = 0; q < WDW / 4; ++q) {
-      const uint4 t = reinterpret_cast<const uint4*>(vb + tid * 8 - WLO / 2)[q];
+      const uint4 t = reinterpret_cast<const uint4*>(vb + rl * 8 - WLO / 2)[q];
       w[4 * q] = t.x;
       w[4 * q + 1] = t.y;
       w[4 * q + 2] = t.z;
       w[4 * q + 3] = t.w;
     }
-    uint32_t ob[16];
+    uint32_t o[4];
+    if constexpr (T::H16) {
+      uint32_t h[8];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      uint32_t h = 0;
+      for (int pp = 0; pp < 8; ++pp) {
+        u16x2 sacc = (u16x2)(unsigned short)(F::DIV / 2);
 #pragma unroll
-      for (int i = 0; i < K; ++i) {
-        const int k = WLO + j + (i - R) * C;
-        h += (uint32_t)F::g(i) * ((w[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu);
+        for (int i = 0; i < K; ++i)
+          sacc += as_u16x2(pair_at(w, WLO + 2 * pp + (i - R) * C)) * (unsigned short)F::g(i);
+        if constexpr (T::log2div() != 8) sacc = sacc >> (unsigned short)T::log2div();
+        h[pp] = as_u32(sacc);
       }
-      ob[j] = (h + F::DIV / 2) / F::DIV;
-    }
-    uint32_t o[4], center[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      o[q] = pack4(ob[4 * q], ob[4 * q + 1], ob[4 * q + 2], ob[4 * q + 3]);
-      center[q] = lo[R][q] | (hi[R][q] << 8);
+      for (int q = 0; q < 4; ++q)
+        o[q] = T::log2div() == 8 ? __builtin_amdgcn_perm(h[2 * q + 1], h[2 * q], 0x07050301u)
+                                 : __builtin_amdgcn_perm(h[2 * q + 1], h[2 * q], 0x06040200u);
+    } else {
+      uint32_t ob[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        uint32_t hs = 0;
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+          const int k = WLO + j + (i - R) * C;
+          hs += (uint32_t)F::g(i) * ((w[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu);
+        }
+        ob[j] = (hs + F::DIV / 2) / F::DIV;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = pack4(ob[4 * q], ob[4 * q + 1], ob[4 * q + 2], ob[4 * q + 3]);
     }
-    finish_row<C>(a, a.out + (int64_t)y * a.out_pitch, cb, a.row0 + y, R, luts + 512, center, o);
+    if constexpr (SKIP) {
+      uint32_t center[4];
+      load_chunk<PRO>(a, rin, in_row_off(a, y), lane_in, luts + 256, center);
+      apply_skip<C>(a, cb, a.row0 + y, R, center, o);
+    }
+    if (a.has_epi) lut16(luts + 512, o);
+    const u32x4 ov = {o[0], o[1], o[2], o[3]};
+    // rows past the band (odd band tail) are computed but their store is masked
+    __builtin_amdgcn_raw_buffer_store_b128(
+        ov, rout, valid ? a.out_org + (uint32_t)((int64_t)y * a.out_pitch) + lane_out : kOOB, 0, 0);
+  };
+
+  // ping-pong the filter state so no register copies are needed
+  constexpr bool live_in_b = ((K - 1) & 1) != 0;
+  // rows go in pairs with no branch around either step (the second one's store
+  // is masked at an odd band end), so hipcc keeps both prefetched rows in flight
+  for (int y = ys; y < ye; y += 2) {
+    if (live_in_b) {
+      row_step(y, sb, sa, nxa, true);
+      row_step(y + 1, sa, sb, nxb, y + 1 < ye);
+    } else {
+      row_step(y, sa, sb, nxa, true);
+      row_step(y + 1, sb, sa, nxb, y + 1 < ye);
+    }
   }
+  band_margins<C>(a, ys, ye);
 }
 
 // ------------------------------------------------------------------------------
 // Direct (non-separable) filters: emboss3/5, sharpen, laplace, sobel
 // ------------------------------------------------------------------------------
-template <int C, class F, int PRO>
-__global__ __launch_bounds__(kNT) void k_direct(KArgs a) {
+template <int C, class F, int PRO, bool SKIP>
+__global__ __launch_bounds__(kNT, 4) void k_direct(KArgs a) {
   constexpr int R = F::R, K = F::K, S = K + 1;
+  constexpr int CIN = PRO == PRO_GRAY ? 3 : 1;
   __shared__ __attribute__((aligned(16))) uint4 ring[S][kNT];
   __shared__ uint8_t luts[768];
 
   const int tid = threadIdx.x;
   const int cb = (int)blockIdx.x * (kOutChunks * 16) - 16 + tid * 16;
-  const bool ld = cb < a.E + 16;
   const bool st = tid >= 1 && tid <= kNT - 2 && cb < a.E;
+  const uint32_t lane_in = cb < a.E + 16 ? (uint32_t)(cb * CIN) : kOOB;
+  const uint32_t lane_out = st ? (uint32_t)cb : kOOB;
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);
+  const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
   int ys, ye;
   band_range(a, blockIdx.y, ys, ye);
   if (ys >= ye) return;
@@ -198,97 +333,103 @@ __global__ __launch_bounds__(kNT) void k_direct(KArgs a) {
     load_luts(a, luts);
     __syncthreads();
   }
-  // slot of row r is (r - (ys - R)) mod S; track the slot of row y - R incrementally
+  const uint32_t last_row = in_row_off(a, ye - 1 + R);
+  // slot of row r is (r - (ys - R)) mod S; s0 tracks the slot of row y - R
 #pragma unroll
   for (int i = 0; i < K - 1; ++i) {
     uint32_t r[4];
-    load_chunk<PRO>(a, in_row(a, ys - R + i), cb, ld, luts + 256, r);
+    load_chunk<PRO>(a, rin, in_row_off(a, ys - R + i), lane_in, luts + 256, r);
     ring[i][tid] = make_uint4(r[0], r[1], r[2], r[3]);
   }
   uint32_t nxt[4];
-  load_chunk<PRO>(a, in_row(a, ys + R), cb, ld, luts + 256, nxt);
-  int s0 = 0;  // slot of row y - R
+  load_chunk<PRO>(a, rin, in_row_off(a, ys + R), lane_in, luts + 256, nxt);
+  const int rl = tid == 0 ? 1 : (tid == kNT - 1 ? kNT - 2 : tid);
+  int s0 = 0;
   for (int y = ys; y < ye; ++y) {
     int sw = s0 + K - 1;
     if (sw >= S) sw -= S;
     ring[sw][tid] = make_uint4(nxt[0], nxt[1], nxt[2], nxt[3]);
-    if (y + 1 < ye) load_chunk<PRO>(a, in_row(a, y + 1 + R), cb, ld, luts + 256, nxt);
+    load_chunk<PRO>(a, rin, y + 1 < ye ? in_row_off(a, y + 1 + R) : last_row, lane_in, luts + 256, nxt);
     __syncthreads();
-    if (st) {
-      int acc[16], acc2[16];
+    int acc[16], acc2[16];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) acc[j] = acc2[j] = 0;
-      uint32_t center[4];
+    for (int j = 0; j < 16; ++j) acc[j] = acc2[j] = 0;
+    uint32_t center[4];
 #pragma unroll
-      for (int dy = 0; dy < K; ++dy) {
-        int sl = s0 + dy;
-        if (sl >= S) sl -= S;
-        const uint4 l = ring[sl][tid - 1], m = ring[sl][tid], r = ring[sl][tid + 1];
-        const uint32_t win[12] = {l.x, l.y, l.z, l.w, m.x, m.y, m.z, m.w, r.x, r.y, r.z, r.w};
-        if (dy == R) {
-          center[0] = m.x;
-          center[1] = m.y;
-          center[2] = m.z;
-          center[3] = m.w;
-        }
+    for (int dy = 0; dy < K; ++dy) {
+      int sl = s0 + dy;
+      if (sl >= S) sl -= S;
+      const uint4 l = ring[sl][rl - 1], m = ring[sl][rl], r = ring[sl][rl + 1];
+      const uint32_t win[12] = {l.x, l.y, l.z, l.w, m.x, m.y, m.z, m.w, r.x, r.y, r.z, r.w};
+      if (dy == R) {
+        center[0] = m.x;
+        center[1] = m.y;
+        center[2] = m.z;
+        center[3] = m.w;
+      }
 #pragma unroll
-        for (int dx = 0; dx < K; ++dx) {
-          const int wx = F::w(dy, dx);
-          int wy = 0;
-          if constexpr (F::SOBEL) wy = F::wy(dy, dx);
-          if (wx == 0 && wy == 0) continue;
+      for (int dx = 0; dx < K; ++dx) {
+        const int wx = F::w(dy, dx);
+        int wy = 0;
+        if constexpr (F::SOBEL) wy = F::wy(dy, dx);
+        if (wx == 0 && wy == 0) continue;
 #pragma unroll
-          for (int j = 0; j < 16; ++j) {
-            const int k = 16 + j + (dx - R) * C;
-            const int v = (int)((win[k >> 2] >> ((k & 3) * 8)) & 0xFFu);
-            if (wx != 0) acc[j] += wx * v;
-            if constexpr (F::SOBEL)
-              if (wy != 0) acc2[j] += wy * v;
-          }
+        for (int j = 0; j < 16; ++j) {
+          const int k = 16 + j + (dx - R) * C;
+          const int v = (int)((win[k >> 2] >> ((k & 3) * 8)) & 0xFFu);
+          if (wx != 0) acc[j] += wx * v;
+          if constexpr (F::SOBEL)
+            if (wy != 0) acc2[j] += wy * v;
         }
       }
-      uint32_t ob[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        int v = acc[j];
-        if constexpr (F::SOBEL) v = abs(acc[j]) + abs(acc2[j]);
-        ob[j] = (uint32_t)min(max(v, 0), 255);
-      }
-      uint32_t o[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) o[q] = pack4(ob[4 * q], ob[4 * q + 1], ob[4 * q + 2], ob[4 * q + 3]);
-      finish_row<C>(a, a.out + (int64_t)y * a.out_pitch, cb, a.row0 + y, R, luts + 512, center, o);
     }
+    uint32_t ob[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      int v = acc[j];
+      if constexpr (F::SOBEL) v = abs(acc[j]) + abs(acc2[j]);
+      ob[j] = (uint32_t)min(max(v, 0), 255);
+    }
+    uint32_t o[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = pack4(ob[4 * q], ob[4 * q + 1], ob[4 * q + 2], ob[4 * q + 3]);
+    if constexpr (SKIP) apply_skip<C>(a, cb, a.row0 + y, R, center, o);
+    if (a.has_epi) lut16(luts + 512, o);
+    const u32x4 ov = {o[0], o[1], o[2], o[3]};
+    __builtin_amdgcn_raw_buffer_store_b128(ov, rout, a.out_org + (uint32_t)((int64_t)y * a.out_pitch) + lane_out,
+                                           0, 0);
     s0 = s0 + 1 == S ? 0 : s0 + 1;
   }
+  band_margins<C>(a, ys, ye);
 }
 
 // ------------------------------------------------------------------------------
 // dispatch
 // ------------------------------------------------------------------------------
 template <int C, class F, int PRO>
-void launch_one(bool sep, dim3 grid, const KArgs& a, hipStream_t s) {
+void launch_one(bool skip, dim3 grid, const KArgs& a, hipStream_t s) {
   if constexpr (F::SEP) {
-    k_sep<C, F, PRO><<<grid, kNT, 0, s>>>(a);
+    if (skip) k_sep<C, F, PRO, true><<<grid, kNT, 0, s>>>(a);
+    else k_sep<C, F, PRO, false><<<grid, kNT, 0, s>>>(a);
   } else {
-    k_direct<C, F, PRO><<<grid, kNT, 0, s>>>(a);
+    if (skip) k_direct<C, F, PRO, true><<<grid, kNT, 0, s>>>(a);
+    else k_direct<C, F, PRO, false><<<grid, kNT, 0, s>>>(a);
   }
-  (void)sep;
 }
 
 template <class F>
 void launch_filter(const Pass& p, dim3 grid, const KArgs& a, hipStream_t s) {
   const bool gray = p.pro.gray;
   const bool lut = p.pro.has_post;
-  const bool sep = F::SEP;
+  const bool skip = p.border == Border::Skip;
   if (p.cmid == 3) {
     STRIPE_CHECK(!gray, "gray prologue must produce 1 channel");
-    if (lut) launch_one<3, F, PRO_LUT>(sep, grid, a, s);
-    else launch_one<3, F, PRO_NONE>(sep, grid, a, s);
+    if (lut) launch_one<3, F, PRO_LUT>(skip, grid, a, s);
+    else launch_one<3, F, PRO_NONE>(skip, grid, a, s);
   } else {
-    if (gray) launch_one<1, F, PRO_GRAY>(sep, grid, a, s);
-    else if (lut) launch_one<1, F, PRO_LUT>(sep, grid, a, s);
-    else launch_one<1, F, PRO_NONE>(sep, grid, a, s);
+    if (gray) launch_one<1, F, PRO_GRAY>(skip, grid, a, s);
+    else if (lut) launch_one<1, F, PRO_LUT>(skip, grid, a, s);
+    else launch_one<1, F, PRO_NONE>(skip, grid, a, s);
   }
 }
 
@@ -321,6 +462,19 @@ void launch_stencil(const Pass& p, const PassConsts& pc, const PassLaunch& L, hi
   }
   STRIPE_CHECK(p.cmid == 1 || p.cmid == 3, "stencil channels must be 1 or 3");
   STRIPE_CHECK(!(p.pro.gray && p.cin != 3), "gray prologue needs 3 input channels");
+  STRIPE_CHECK(L.in_base && L.out_base, "stencil launch needs the allocation view (in_base/out_base)");
+  STRIPE_CHECK(L.in_bytes > 0 && L.in_bytes < (int64_t)dev::kOOB && L.out_bytes > 0 &&
+                   L.out_bytes < (int64_t)dev::kOOB,
+               "stripe buffers must be < 2 GiB for buffer-descriptor addressing");
+  STRIPE_CHECK(L.in_org >= kMarginBytes && L.out_org >= kMarginBytes && L.in_zero >= kMarginBytes,
+               "bad origin offsets");
+  a.in_base = L.in_base;
+  a.out_base = L.out_base;
+  a.in_bytes = (uint32_t)L.in_bytes;
+  a.in_org = (uint32_t)L.in_org;
+  a.in_zero = (uint32_t)L.in_zero;
+  a.out_bytes = (uint32_t)L.out_bytes;
+  a.out_org = (uint32_t)L.out_org;
 
   const int n0 = std::max(0, L.ry[1] - L.ry[0]);
   const int n1 = L.nrange > 1 ? std::max(0, L.ry[3] - L.ry[2]) : 0;
@@ -334,6 +488,7 @@ void launch_stencil(const Pass& p, const PassConsts& pc, const PassLaunch& L, hi
     band = (int)div_up(n0 + n1, want_bands);
     band = std::max(band, std::max(8, 4 * p.R));
     band = std::min(band, 256);
+    band += band & 1;  // even: the separable kernel steps rows in pairs
   }
   a.band = band;
   a.ry0 = L.ry[0];

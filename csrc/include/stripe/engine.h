@@ -91,6 +91,9 @@ class Engine {
 
   // ---- compute ----
   void run(int iterations = 1);
+  // Make the input of the last run() the current input again (benchmarks of
+  // chains that change the channel count; the data may have been overwritten).
+  void rewind();
 
   // ---- output ----
   void store_packed(void* dst, bool dst_device);          // own output stripe, packed
@@ -138,6 +141,7 @@ class Engine {
   hipEvent_t ev_[8] = {};
   PhaseTimes times_;
   int out_buf_ = -1;        // buffer holding the last run's output
+  int run_in_buf_ = 0;      // buffer holding the last run's input
   int out_c_ = 0;
 };
 

@@ -42,6 +42,12 @@ struct PassLaunch {
   int ry[4] = {0, 0, 0, 0};      // [ry0, ry1) and [ry2, ry3)
   const uint8_t* zero_row = nullptr;  // origin of an all-zero row (Constant y-border)
   int band = 0;                  // rows per workgroup (0 = auto)
+  // Allocation view for buffer-descriptor kernels (branch-free OOB masking):
+  // origin = base + org, zero row origin = in_base + in_zero; sizes < 2 GiB.
+  const uint8_t* in_base = nullptr;
+  int64_t in_bytes = 0, in_org = 0, in_zero = 0;
+  uint8_t* out_base = nullptr;
+  int64_t out_bytes = 0, out_org = 0;
 };
 
 void launch_pass(const Pass& p, const PassConsts& pc, const PassLaunch& L, hipStream_t s);

@@ -20,6 +20,7 @@ namespace stripe {
 namespace sdef {
 
 struct Emboss3 {
+  static constexpr bool BINOM = false;
   static constexpr int K = 3, R = 1, DIV = 1;
   static constexpr bool SEP = false, SOBEL = false;
   STRIPE_HD static constexpr int w(int dy, int dx) {
@@ -29,6 +30,7 @@ struct Emboss3 {
 };
 
 struct Emboss5 {
+  static constexpr bool BINOM = false;
   static constexpr int K = 5, R = 2, DIV = 1;
   static constexpr bool SEP = false, SOBEL = false;
   STRIPE_HD static constexpr int w(int dy, int dx) {
@@ -38,6 +40,7 @@ struct Emboss5 {
 };
 
 struct Sharpen {
+  static constexpr bool BINOM = false;
   static constexpr int K = 3, R = 1, DIV = 1;
   static constexpr bool SEP = false, SOBEL = false;
   STRIPE_HD static constexpr int w(int dy, int dx) {
@@ -47,6 +50,7 @@ struct Sharpen {
 };
 
 struct Laplace {
+  static constexpr bool BINOM = false;
   static constexpr int K = 3, R = 1, DIV = 1;
   static constexpr bool SEP = false, SOBEL = false;
   STRIPE_HD static constexpr int w(int dy, int dx) {
@@ -57,6 +61,7 @@ struct Laplace {
 
 // Sobel: Gx = [1,2,1]^T (x) [-1,0,1],  Gy = [-1,0,1]^T (x) [1,2,1];  out = sat(|Gx|+|Gy|)
 struct Sobel {
+  static constexpr bool BINOM = false;
   static constexpr int K = 3, R = 1, DIV = 1;
   static constexpr bool SEP = false, SOBEL = true;
   STRIPE_HD static constexpr int wx(int dy, int dx) {
@@ -71,7 +76,8 @@ struct Sobel {
 };
 
 // Separable integer smoothing filters: out = (sum + DIV/2) / DIV, sum >= 0.
-struct Gaussian3 {
+struct Gaussian3 {  // binomial: cascade of K-1 two-tap sums
+  static constexpr bool BINOM = true;
   static constexpr int K = 3, R = 1, DIV = 16;
   static constexpr bool SEP = true, SOBEL = false;
   STRIPE_HD static constexpr int g(int i) {
@@ -81,7 +87,8 @@ struct Gaussian3 {
   STRIPE_HD static constexpr int w(int dy, int dx) { return g(dy) * g(dx); }
 };
 
-struct Gaussian5 {
+struct Gaussian5 {  // binomial: cascade of K-1 two-tap sums
+  static constexpr bool BINOM = true;
   static constexpr int K = 5, R = 2, DIV = 256;
   static constexpr bool SEP = true, SOBEL = false;
   STRIPE_HD static constexpr int g(int i) {
@@ -91,7 +98,8 @@ struct Gaussian5 {
   STRIPE_HD static constexpr int w(int dy, int dx) { return g(dy) * g(dx); }
 };
 
-struct Gaussian7 {
+struct Gaussian7 {  // binomial: cascade of K-1 two-tap sums
+  static constexpr bool BINOM = true;
   static constexpr int K = 7, R = 3, DIV = 4096;
   static constexpr bool SEP = true, SOBEL = false;
   STRIPE_HD static constexpr int g(int i) {
@@ -102,6 +110,7 @@ struct Gaussian7 {
 };
 
 struct Box3 {
+  static constexpr bool BINOM = false;
   static constexpr int K = 3, R = 1, DIV = 9;
   static constexpr bool SEP = true, SOBEL = false;
   STRIPE_HD static constexpr int g(int) { return 1; }
@@ -109,6 +118,7 @@ struct Box3 {
 };
 
 struct Box5 {
+  static constexpr bool BINOM = false;
   static constexpr int K = 5, R = 2, DIV = 25;
   static constexpr bool SEP = true, SOBEL = false;
   STRIPE_HD static constexpr int g(int) { return 1; }

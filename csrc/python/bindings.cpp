@@ -287,6 +287,7 @@ PYBIND11_MODULE(_C, m) {
         py::gil_scoped_release nogil;
         e.run(it);
       }, py::arg("iterations") = 1)
+      .def("rewind", &Engine::rewind)
       .def("gather", [](Engine& e) {
         py::gil_scoped_release nogil;
         e.gather();

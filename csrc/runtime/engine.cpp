@@ -68,7 +68,9 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
     own_streams_ = true;
     for (auto& e : ev_) HIP_CHECK(hipEventCreate(&e));
   }
-  for (auto& b : buf_) b = Buffer((size_t)std::max(1, rows_alloc_) * pmax, device());
+  // one extra all-zero row at the end of each stripe buffer: the Constant
+  // y-border row the buffer-descriptor kernels read (never written)
+  for (auto& b : buf_) b = Buffer((size_t)(std::max(1, rows_alloc_) + 1) * pmax, device());
   zero_ = Buffer((size_t)pmax, device());
   if (cfg_.root_buffers && rank_ == 0) {
     root_in_ = Buffer((size_t)cfg_.H * padded_pitch(cfg_.W, plan_.cin), device());
@@ -302,6 +304,19 @@ void Engine::run_pass(const Pass& p, const uint8_t* in, uint8_t* out) {
   L.Hg = g.Hg;
   L.zero_row = zero_.data() + kMarginBytes;
   L.band = cfg_.band;
+  {
+    const Buffer& bi = buf_[cur_];
+    const Buffer& bo = buf_[cur_ ^ 1];
+    STRIPE_CHECK(in >= bi.data() && in < bi.data() + bi.bytes() && out >= bo.data() && out < bo.data() + bo.bytes(),
+                 "pass buffers are not the engine's current ping-pong pair");
+    L.in_base = bi.data();
+    L.in_bytes = (int64_t)bi.bytes();
+    L.in_org = in - bi.data();
+    L.in_zero = (int64_t)std::max(1, rows_alloc_) * padded_pitch(cfg_.W, plan_.max_channels) + kMarginBytes;
+    L.out_base = bo.data();
+    L.out_bytes = (int64_t)bo.bytes();
+    L.out_org = out - bo.data();
+  }
   if (!xchg) {
     L.nrange = 1;
     L.ry[0] = 0;
@@ -338,6 +353,7 @@ void Engine::run(int iterations) {
   STRIPE_CHECK(iterations == 1 || plan_.cout == plan_.cin,
                "iterating a chain needs equal input/output channels (" << plan_.cin << "->" << plan_.cout << ")");
   record(ev_[0], s_compute_);
+  run_in_buf_ = cur_;
   for (int it = 0; it < iterations; ++it) {
     STRIPE_CHECK(cur_c_ == plan_.cin, "engine input has " << cur_c_ << " channels, chain expects " << plan_.cin);
     for (const Pass& p : plan_.passes) {
@@ -349,6 +365,11 @@ void Engine::run(int iterations) {
   record(ev_[1], s_compute_);
   out_buf_ = cur_;
   out_c_ = plan_.cout;
+}
+
+void Engine::rewind() {
+  cur_ = run_in_buf_;
+  cur_c_ = plan_.cin;
 }
 
 void Engine::store_packed(void* dst, bool dst_device) {

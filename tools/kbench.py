@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Single-GPU kernel benchmark: time `iters` resident passes of each chain.
+
+    python tools/kbench.py --chains gaussian5,sobel --shape 16384x16384x3 --iters 50
+
+Reports ms per pass, Mpixels/s and the effective HBM bandwidth (input + output
+bytes of every pass, counted once).  Used for tuning and under rocprofv3.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--chains", default="gaussian5")
+    ap.add_argument("--shape", default="16384x16384x3")
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--band", type=int, default=0)
+    ap.add_argument("--no-fuse", action="store_true")
+    a = ap.parse_args()
+    import torch
+
+    from mpi_cuda_imagemanipulation_amd._native import C
+    from mpi_cuda_imagemanipulation_amd.models import Pipeline
+
+    W, H, Cc = (int(v) for v in a.shape.split("x"))
+    for chain in a.chains.split(";"):
+        pipe = Pipeline(chain, fuse=not a.no_fuse)
+        cfg = pipe.config(W, H, Cc, "device", device=0)
+        cfg.band = a.band
+        e = C.Engine(cfg)
+        info = C.plan_info(chain, Cc)
+        e.load_synthetic(1)
+        iters = a.iters if info["cout"] == info["cin"] else 1
+        e.run(a.warmup if iters > 1 else 1)
+        e.synchronize()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(max(1, a.iters // iters)):
+            if iters == 1:
+                e.rewind()
+            e.run(iters)
+        e.synchronize()
+        t1 = time.perf_counter()
+        n = iters * max(1, a.iters // iters)
+        ms = (t1 - t0) * 1e3 / n
+        byts = sum(W * H * (p["cin"] + p["cout"]) for p in info["passes"])
+        print(json.dumps({"chain": chain, "shape": a.shape, "ms": round(ms, 4),
+                          "mpx_s": round(W * H / ms / 1e3, 1), "GBps": round(byts / ms / 1e6, 1),
+                          "passes": len(info["passes"])}), flush=True)
+        del e
+
+
+if __name__ == "__main__":
+    main()
