@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--band", type=int, default=0)
     ap.add_argument("--dist-steps", type=int, default=5, help="steps of the dist-scope measurement (0: skip)")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--no-autotune", action="store_true", help="skip the per-shape band-height autotune")
     return ap.parse_args()
 
 
@@ -77,7 +78,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    dp = parallel.DistributedPipeline(ctx, pipe, W, H, Cc, root_buffers=a.dist_steps > 0)
+    dp = parallel.DistributedPipeline(ctx, pipe, W, H, Cc, root_buffers=a.dist_steps > 0,
+                                      autotune=not a.no_autotune)
     row0, rows = dp.stripe
 
     # ---- correctness (untimed): one step vs the golden path on edge crops ----
@@ -172,6 +174,7 @@ def main():
             },
             "dist_scope_mpx_s": None if dist_mpx is None else round(dist_mpx, 1),
             "verified_vs_golden": verify,
+            "tuned_band_rows": dp.engine.bands,
         }
         print(json.dumps(rec), flush=True)
     if world > 1:

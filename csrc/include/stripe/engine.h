@@ -38,6 +38,7 @@ struct EngineConfig {
   BackendKind backend = BackendKind::Device;
   int band = 0;                 // stencil rows per workgroup (0 = auto)
   bool root_buffers = false;    // rank 0 allocates full-frame in/out buffers (scatter/gather)
+  bool autotune = false;        // time candidate band heights per stencil pass on first run()
 };
 
 // Device or host allocation freed on destruction.
@@ -94,6 +95,8 @@ class Engine {
   // Make the input of the last run() the current input again (benchmarks of
   // chains that change the channel count; the data may have been overwritten).
   void rewind();
+  // Tuned band heights per pass (after autotune), for reporting.
+  std::vector<int> bands() const;
 
   // ---- output ----
   void store_packed(void* dst, bool dst_device);          // own output stripe, packed
@@ -111,7 +114,10 @@ class Engine {
   struct PassRt {
     PassConsts pc;
     Buffer luts;
+    int band = 0;  // tuned stencil band height (0: kernel default / cfg.band)
   };
+  void autotune_bands();
+  bool tuned_ = false;
   uint8_t* origin(const Buffer& b, int C) const;
   uint8_t* root_origin(const Buffer& b, int C) const;
   void exchange_halo(uint8_t* org, int C, int R, hipStream_t s);

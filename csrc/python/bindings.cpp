@@ -234,7 +234,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("device", &EngineConfig::device)
       .def_readwrite("backend", &EngineConfig::backend)
       .def_readwrite("band", &EngineConfig::band)
-      .def_readwrite("root_buffers", &EngineConfig::root_buffers);
+      .def_readwrite("root_buffers", &EngineConfig::root_buffers)
+      .def_readwrite("autotune", &EngineConfig::autotune);
 
   py::class_<PhaseTimes>(m, "PhaseTimes")
       .def_readonly("run", &PhaseTimes::run)
@@ -288,6 +289,7 @@ PYBIND11_MODULE(_C, m) {
         e.run(it);
       }, py::arg("iterations") = 1)
       .def("rewind", &Engine::rewind)
+      .def_property_readonly("bands", &Engine::bands)
       .def("gather", [](Engine& e) {
         py::gil_scoped_release nogil;
         e.gather();

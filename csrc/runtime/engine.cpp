@@ -303,7 +303,7 @@ void Engine::run_pass(const Pass& p, const uint8_t* in, uint8_t* out) {
   L.row0 = g.row0;
   L.Hg = g.Hg;
   L.zero_row = zero_.data() + kMarginBytes;
-  L.band = cfg_.band;
+  L.band = prt_[pi].band > 0 ? prt_[pi].band : cfg_.band;
   {
     const Buffer& bi = buf_[cur_];
     const Buffer& bo = buf_[cur_ ^ 1];
@@ -348,8 +348,67 @@ void Engine::run_pass(const Pass& p, const uint8_t* in, uint8_t* out) {
   }
 }
 
+std::vector<int> Engine::bands() const {
+  std::vector<int> b;
+  for (const auto& p : prt_) b.push_back(p.band);
+  return b;
+}
+
+// Time each candidate band height on this rank's stripe (kernels only, no halo
+// exchange; outputs land in the scratch ping-pong buffer) and keep the fastest.
+void Engine::autotune_bands() {
+  tuned_ = true;
+  if (!device() || cfg_.band > 0 || stripe().rows == 0) return;
+  const int cand[] = {8, 12, 16, 24, 32};
+  hipEvent_t e0 = ev_[6], e1 = ev_[7];
+  for (size_t i = 0; i < plan_.passes.size(); ++i) {
+    const Pass& p = plan_.passes[i];
+    if (p.kind != PassKind::Separable && p.kind != PassKind::Direct) continue;
+    float best = 1e30f;
+    int best_band = 0;
+    for (int b : cand) {
+      prt_[i].band = b;
+      float tot = 0;
+      for (int rep = 0; rep < 4; ++rep) {
+        PassLaunch L;
+        L.in = origin(buf_[cur_], p.cin);
+        L.in_pitch = pitch(p.cin);
+        L.out = origin(buf_[cur_ ^ 1], p.cout);
+        L.out_pitch = pitch(p.cout);
+        L.W = cfg_.W;
+        L.rows = stripe().rows;
+        const RowGeom g = geom();
+        L.row0 = g.row0;
+        L.Hg = g.Hg;
+        L.zero_row = zero_.data() + kMarginBytes;
+        L.band = b;
+        L.in_base = buf_[cur_].data();
+        L.in_bytes = (int64_t)buf_[cur_].bytes();
+        L.in_org = L.in - buf_[cur_].data();
+        L.in_zero = (int64_t)std::max(1, rows_alloc_) * padded_pitch(cfg_.W, plan_.max_channels) + kMarginBytes;
+        L.out_base = buf_[cur_ ^ 1].data();
+        L.out_bytes = (int64_t)buf_[cur_ ^ 1].bytes();
+        L.out_org = L.out - buf_[cur_ ^ 1].data();
+        L.ry[0] = 0;
+        L.ry[1] = L.rows;
+        HIP_CHECK(hipEventRecord(e0, s_compute_));
+        launch_pass(p, prt_[i].pc, L, s_compute_);
+        HIP_CHECK(hipEventRecord(e1, s_compute_));
+        HIP_CHECK(hipEventSynchronize(e1));
+        if (rep > 0) tot += elapsed(e0, e1);  // first launch is a warmup
+      }
+      if (tot < best) {
+        best = tot;
+        best_band = b;
+      }
+    }
+    prt_[i].band = best_band;
+  }
+}
+
 void Engine::run(int iterations) {
   STRIPE_CHECK(iterations >= 1, "iterations must be >= 1");
+  if (cfg_.autotune && !tuned_) autotune_bands();
   STRIPE_CHECK(iterations == 1 || plan_.cout == plan_.cin,
                "iterating a chain needs equal input/output channels (" << plan_.cin << "->" << plan_.cout << ")");
   record(ev_[0], s_compute_);

@@ -86,7 +86,7 @@ class Pipeline:
 
         return ops.apply(image, self.spec.chain, self.spec.border, self.fuse)
 
-    def config(self, W: int, H: int, Cc: int, backend: str = "device", device: int = -1):
+    def config(self, W: int, H: int, Cc: int, backend: str = "device", device: int = -1, autotune: bool = False):
         cfg = C.EngineConfig()
         cfg.W, cfg.H, cfg.C = int(W), int(H), int(Cc)
         cfg.chain = self.spec.chain
@@ -97,6 +97,7 @@ class Pipeline:
         cfg.overlap = self.overlap
         cfg.device = int(device)
         cfg.backend = C.Backend.host if backend == "host" else C.Backend.device
+        cfg.autotune = bool(autotune)
         return cfg
 
     def run_distributed(self, image: np.ndarray, ranks: int, backend: str = "host", iterations: int = 1):

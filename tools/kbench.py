@@ -21,7 +21,7 @@ def main():
     ap.add_argument("--shape", default="16384x16384x3")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--band", type=int, default=0)
+    ap.add_argument("--bands", default="0", help="comma list of stencil band heights (0 = auto)")
     ap.add_argument("--no-fuse", action="store_true")
     a = ap.parse_args()
     import torch
@@ -30,10 +30,10 @@ def main():
     from mpi_cuda_imagemanipulation_amd.models import Pipeline
 
     W, H, Cc = (int(v) for v in a.shape.split("x"))
-    for chain in a.chains.split(";"):
+    for chain, band in [(c, int(b)) for c in a.chains.split(";") for b in a.bands.split(",")]:
         pipe = Pipeline(chain, fuse=not a.no_fuse)
         cfg = pipe.config(W, H, Cc, "device", device=0)
-        cfg.band = a.band
+        cfg.band = band
         e = C.Engine(cfg)
         info = C.plan_info(chain, Cc)
         e.load_synthetic(1)
@@ -51,7 +51,7 @@ def main():
         n = iters * max(1, a.iters // iters)
         ms = (t1 - t0) * 1e3 / n
         byts = sum(W * H * (p["cin"] + p["cout"]) for p in info["passes"])
-        print(json.dumps({"chain": chain, "shape": a.shape, "ms": round(ms, 4),
+        print(json.dumps({"chain": chain, "band": band, "shape": a.shape, "ms": round(ms, 4),
                           "mpx_s": round(W * H / ms / 1e3, 1), "GBps": round(byts / ms / 1e6, 1),
                           "passes": len(info["passes"])}), flush=True)
         del e
