@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--dist-steps", type=int, default=5, help="steps of the dist-scope measurement (0: skip)")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-autotune", action="store_true", help="skip the per-shape band-height autotune")
+    ap.add_argument("--backend", default="rccl", choices=["rccl", "host"],
+                    help="rccl: GPU engine + RCCL (the benchmark); host: CPU golden engine + gloo (plumbing tests)")
     return ap.parse_args()
 
 
@@ -60,7 +62,13 @@ def main():
     from mpi_cuda_imagemanipulation_amd._native import C
     from mpi_cuda_imagemanipulation_amd.models import Pipeline
 
-    ctx = parallel.init("rccl")
+    ctx = parallel.init("rccl" if a.backend == "rccl" else "gloo")
+    dev = ctx.device
+    tdev = "cuda" if dev else "cpu"
+
+    def sync():
+        if dev:
+            torch.cuda.synchronize()
     world, rank = ctx.world, ctx.rank
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
@@ -74,7 +82,7 @@ def main():
     def max_over_ranks(v: float) -> float:
         if world == 1:
             return v
-        t = torch.tensor([v], dtype=torch.float64, device="cuda")
+        t = torch.tensor([v], dtype=torch.float64, device=tdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -103,7 +111,7 @@ def main():
             band = C.synth_rows(a.seed, W, Cc, row0 - 8, 16)
             ref = C.golden_apply(band, a.chain, "reflect101", True)
             ok &= bool((out[0:4] == ref[8:12]).all())
-        okt = torch.tensor([1.0 if ok else 0.0], device="cuda")
+        okt = torch.tensor([1.0 if ok else 0.0], device=tdev)
         if world > 1:
             dist.all_reduce(okt, op=dist.ReduceOp.MIN)
         verify = bool(okt.item() == 1.0)
@@ -112,13 +120,13 @@ def main():
     dp.load_synthetic(a.seed)
     if a.warmup > 0:
         dp.run(a.warmup)
-    torch.cuda.synchronize()
+    sync()
     barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     dp.run(a.steps)
     dp.synchronize()
-    torch.cuda.synchronize()
+    sync()
     barrier()
     t1 = time.perf_counter()
     ms = max_over_ranks((t1 - t0) * 1e3)
@@ -136,7 +144,7 @@ def main():
             dp.run(1)
             dp.gather()
         dp.synchronize()
-        torch.cuda.synchronize()
+        sync()
         barrier()
         t0 = time.perf_counter()
         for _ in range(a.dist_steps):
@@ -144,7 +152,7 @@ def main():
             dp.run(1)
             dp.gather()
         dp.synchronize()
-        torch.cuda.synchronize()
+        sync()
         barrier()
         t1 = time.perf_counter()
         dms = max_over_ranks((t1 - t0) * 1e3) / a.dist_steps
@@ -163,6 +171,7 @@ def main():
             "scaling": "strong",
             "vs_baseline": None if BASELINE_MPX is None else round(mpx / BASELINE_MPX, 3),
             "dtype": "uint8 (int32 accumulate, exact)",
+            "backend": a.backend,
             "data": "synthetic (seeded random pixels)",
             "config": {
                 "model": a.chain,
