@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -190,8 +191,11 @@ int cmd_cmp(const Args& a) {
     std::printf("{\"same_shape\":false}\n");
     return 2;
   }
-  std::printf("{\"same_shape\":true,\"max_abs\":%d,\"n_diff\":%lld,\"psnr\":%.3f}\n", r.max_abs, (long long)r.n_diff,
-              r.psnr);
+  char psnr[32];
+  if (std::isfinite(r.psnr)) std::snprintf(psnr, sizeof psnr, "%.3f", r.psnr);
+  else std::snprintf(psnr, sizeof psnr, "null");  // identical images
+  std::printf("{\"same_shape\":true,\"max_abs\":%d,\"n_diff\":%lld,\"psnr\":%s}\n", r.max_abs, (long long)r.n_diff,
+              psnr);
   return r.max_abs <= tol ? 0 : 1;
 }
 

@@ -1,0 +1,105 @@
+"""Native `stripe` CLI (bin/stripe) on the CPU host backend.
+
+Config 1 of BASELINE.json (grayscale on a 512x512 PPM, CPU path, world_size=1)
+plus the reference presets run as multi-rank in-process groups.
+"""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import np_ref
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "bin", "stripe")
+
+pytestmark = pytest.mark.skipif(not os.path.exists(EXE), reason="bin/stripe not built")
+
+
+def run(*args, check=True):
+    r = subprocess.run([EXE, *map(str, args)], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, HIP_VISIBLE_DEVICES=os.environ.get("HIP_VISIBLE_DEVICES", "")))
+    if check:
+        assert r.returncode == 0, r.stdout + r.stderr
+    return r
+
+
+def test_config1_gray_512(tmp_path):
+    from mpi_cuda_imagemanipulation_amd import utils
+
+    src = tmp_path / "in.ppm"
+    run("gen", "--synthetic", "512x512x3", "--seed", "1", "--output", src)
+    img = utils.read_image(src)
+    assert img.shape == (512, 512, 3)
+    out = tmp_path / "gray.pgm"
+    r = run("run", "--input", src, "--output", out, "--chain", "gray", "--backend", "host", "--ranks", "1")
+    rec = json.loads(r.stdout.strip().splitlines()[-1])
+    assert rec["ranks"] == 1 and rec["backend"] == "host"
+    g = utils.read_image(out)
+    assert g.shape == (512, 512) and (g == np_ref.gray_bt601(img)).all()
+    assert out.read_bytes().startswith(b"P5\n512 512\n255\n")
+
+
+@pytest.mark.parametrize("ranks", [1, 3, 4])
+def test_presets_multi_rank(tmp_path, ranks):
+    from mpi_cuda_imagemanipulation_amd import utils
+
+    src = tmp_path / "in.ppm"
+    run("gen", "--synthetic", "96x50x3", "--seed", "4", "--output", src)
+    img = utils.read_image(src)
+    rows = 50 // ranks
+    out = tmp_path / "gpu.ppm"
+    run("run", "--input", src, "--output", out, "--preset", "ref-gpu", "--ranks", ranks, "--backend", "host")
+    got = utils.read_image(out)
+    assert got.shape == img.shape  # 3-channel output like the reference's GRAY2BGR (kernel.cu:210)
+    for r in range(ranks):
+        s = img[r * rows:(r + 1) * rows]
+        e = np_ref.stencil(np_ref.contrast_ref(np_ref.gray_ref(s), 3.5), "emboss3", "skip")
+        assert (got[r * rows:(r + 1) * rows] == np_ref.expand(e)).all()
+    assert (got[ranks * rows:] == 0).all()
+    out2 = tmp_path / "cpu.ppm"
+    run("run", "--input", src, "--output", out2, "--preset", "ref-cpu", "--ranks", ranks, "--backend", "host")
+    got2 = utils.read_image(out2)
+    for r in range(ranks):
+        s = img[r * rows:(r + 1) * rows]
+        e = np_ref.stencil(np_ref.contrast_cv(np_ref.gray_bt601(s), 3.0), "emboss3", "reflect101")
+        assert (got2[r * rows:(r + 1) * rows] == np_ref.expand(e)).all()
+
+
+def test_halo_run_equals_single_rank(tmp_path):
+    src = tmp_path / "in.ppm"
+    run("gen", "--synthetic", "77x64x3", "--seed", "2", "--output", src)
+    a, b = tmp_path / "a.ppm", tmp_path / "b.ppm"
+    run("run", "--input", src, "--output", a, "--chain", "gaussian5,sobel", "--ranks", "1", "--backend", "host")
+    run("run", "--input", src, "--output", b, "--chain", "gaussian5,sobel", "--ranks", "5", "--backend", "host")
+    r = run("cmp", a, b)
+    assert json.loads(r.stdout)["max_abs"] == 0
+    c = tmp_path / "c.ppm"
+    run("run", "--input", src, "--output", c, "--chain", "gaussian5,sobel", "--ranks", "5", "--backend", "host",
+        "--no-halo")
+    r = run("cmp", a, c, check=False)
+    assert r.returncode == 1 and json.loads(r.stdout)["n_diff"] > 0  # stripe seams (Q6)
+
+
+def test_cmp_and_errors(tmp_path):
+    src = tmp_path / "in.ppm"
+    run("gen", "--synthetic", "10x10x3", "--output", src)
+    assert run("cmp", src, src).returncode == 0
+    r = run("run", "--input", tmp_path / "missing.ppm", "--output", tmp_path / "o.ppm", check=False)
+    assert r.returncode != 0 and "cannot open" in r.stderr
+    r = run("run", "--input", src, "--output", tmp_path / "o.ppm", "--chain", "nope", "--backend", "host",
+            check=False)
+    assert r.returncode != 0 and "unknown filter" in r.stderr
+    r = run("info", "--chain", "gray:ref,contrast:3.5,emboss3")
+    assert "prologue[gray:ref,lut]" in r.stdout
+
+
+def test_bench_host(tmp_path):
+    js = tmp_path / "b.json"
+    r = run("bench", "--synthetic", "128x64x3", "--chain", "gaussian5", "--ranks", "1,2", "--iters", "2",
+            "--warmup", "1", "--scope", "resident,dist", "--backend", "host", "--json", js)
+    recs = [json.loads(l) for l in js.read_text().splitlines()]
+    assert [(x["n_ranks"], x["scope"]) for x in recs] == [(1, "resident"), (1, "dist"), (2, "resident"), (2, "dist")]
+    assert all(x["value"] > 0 for x in recs)
