@@ -25,8 +25,10 @@ struct KArgs {
   int row0, Hg;   // border geometry
   int border;     // Border enum
   int ry0, ry1, ry2, ry3;  // output row ranges [ry0,ry1) U [ry2,ry3)
-  int band;       // rows per workgroup
-  int nb0;        // workgroups (in y) covering range 0
+  int band;       // rows per wave task
+  int nb0;        // bands covering range 0
+  int ntx;        // wave tiles per row (stencil kernels)
+  int nbands;     // bands over both ranges
   int out_px;     // x-margin pixels to maintain on the output
   int out_border; // border mode encoded in those margins
   int has_pre, has_post, has_epi;

@@ -3,13 +3,15 @@
 // Reference: embossKernel (kernel.cu:64-94) - one thread per pixel, in place
 // (racy, Q1), runtime-indexed private weight arrays, off-by-one bounds (Q2), and
 // separate gray/contrast launches before it.  Here:
-//   * workgroup = 256 lanes x 16 output bytes = one 4 KiB row segment (254 output
-//     chunks + one halo chunk each side), marching down a band of rows;
+//   * every wave works on its own tile: 64 lanes x 16 bytes = a 1 KiB row segment
+//     (62 output chunks + one halo chunk each side) marching down a band of rows;
+//     waves never wait for each other (no workgroup barrier in the hot loop), and
+//     1 KiB tiles quantise wide rows finely (8192 gray: 9 tiles for 8.3 of work);
 //   * each lane loads its 16-byte chunk of every input row once (buffer dwordx4,
 //     two rows in flight), applies the fused prologue (gray / LUT) in registers;
 //   * separable filters: vertical taps in registers as packed-u16 adds - the
 //     binomial Gaussians as a cascade of K-1 two-tap sums (no row ring) - one row
-//     of vertical sums through LDS (double-buffered, one barrier per row), the
+//     of vertical sums through the wave's LDS slice (in-order within a wave), the
 //     horizontal taps as packed-u16 multiply-adds on v_alignbyte-shifted pairs;
 //   * non-separable filters: a (K+1)-row LDS ring of prologue-applied rows; taps
 //     are compile-time literals (zero taps vanish);
@@ -17,8 +19,8 @@
 //     get an offset that fails the descriptor range check (no divergent branches
 //     around memory ops -> exact vmcnt, prefetches survive the barriers);
 //   * out-of-place and deterministic; the x-border comes from the buffer margins,
-//     the y-border from a scalar row remap; edge workgroups rewrite the output
-//     margins after their band (one vmcnt(0) + barrier per band).
+//     the y-border from a scalar row remap; edge waves rewrite the output margins
+//     after their band (one vmcnt(0) per band).
 #include "dev_common.h"
 #include "stripe/kernels.h"
 #include "stripe/stencil_defs.h"
@@ -29,7 +31,41 @@
 namespace stripe {
 namespace dev {
 
-constexpr int kOutChunks = kNT - 2;  // output chunks per workgroup row segment
+constexpr int kW = 64;               // lanes per wave (one tile)
+constexpr int kWaves = kNT / kW;     // independent wave tiles per workgroup
+constexpr int kOutChunks = kW - 2;   // output chunks per wave tile
+
+// Orders this wave's LDS writes before its later LDS reads of other lanes' data
+// (LDS ops of one wave execute in order; this only stops compiler reordering).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+struct WaveTask {
+  int wave;   // wave index within the workgroup (scalar)
+  int lane;
+  int xt;     // tile column
+  int ys, ye; // rows
+  bool valid;
+};
+
+__device__ __forceinline__ WaveTask wave_task(const KArgs& a) {
+  WaveTask t;
+  t.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  t.lane = threadIdx.x & 63;
+  const int w = (int)blockIdx.x * kWaves + t.wave;
+  t.xt = w % a.ntx;
+  const int bt = w / a.ntx;
+  t.valid = bt < a.nbands;
+  t.ys = t.ye = 0;
+  if (t.valid) {
+    band_range(a, bt, t.ys, t.ye);
+    t.valid = t.ys < t.ye;
+  }
+  return t;
+}
 
 enum { PRO_NONE = 0, PRO_LUT = 1, PRO_GRAY = 2 };
 
@@ -85,28 +121,27 @@ __device__ __forceinline__ void apply_skip(const KArgs& a, int cb, int gy, int R
   }
 }
 
-// After a band: edge workgroups rewrite the x-margins of their output rows
-// (margin pixel m <- pixel border_index(m) of the same row).  Reads use sc0 so
-// they see this CU's completed stores.
+// After a band: edge waves rewrite the x-margins of their output rows (margin
+// pixel m <- pixel border_index(m) of the same row).  The wave's own stores are
+// complete after vmcnt(0); reads use sc0 (L2) so they see them.
 template <int C>
-__device__ __forceinline__ void band_margins(const KArgs& a, int ys, int ye) {
+__device__ __forceinline__ void band_margins(const KArgs& a, const WaveTask& t) {
   const int px = a.out_px;
   if (px == 0) return;
   const int E = a.W * C;
-  const bool left = blockIdx.x == 0;
-  const bool right = (int)(blockIdx.x + 1) * kOutChunks * 16 >= E;
+  const bool left = t.xt == 0;
+  const bool right = (t.xt + 1) * kOutChunks * 16 >= E;
   if (!left && !right) return;
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this band's stores are done
-  __syncthreads();
   const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
   const int nb = px * C;  // margin bytes per side
   const int per_row = 2 * nb;
-  for (int i = threadIdx.x; i < (ye - ys) * per_row; i += kNT) {
-    const int y = ys + i / per_row;
-    const int t = i % per_row;
-    const int side = t >= nb;
-    const int k = (side ? t - nb : t) / C + 1;
-    const int c = (side ? t - nb : t) % C;
+  for (int i = t.lane; i < (t.ye - t.ys) * per_row; i += kW) {
+    const int y = t.ys + i / per_row;
+    const int q = i % per_row;
+    const int side = q >= nb;
+    const int k = (side ? q - nb : q) / C + 1;
+    const int c = (side ? q - nb : q) % C;
     if ((side == 0 && !left) || (side == 1 && !right)) continue;
     const int m = side ? a.W - 1 + k : -k;
     const int src = border_index_dev(m, a.W, a.out_border);
@@ -194,27 +229,27 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : 4)) void k_sep(KArgs a) {
   constexpr int WDW = (2 * WLO + 16) / 2;     // window dwords
   constexpr int CIN = PRO == PRO_GRAY ? 3 : 1;  // input bytes per output byte
   using T = SepTraits<F>;
-  // vertical-sum rows, double-buffered, planar: plane h holds dwords 4h..4h+3 of
-  // every lane's 8, so each ds_write_b128 / ds_read_b128 has a 16-byte lane
-  // stride (conflict-free; the interleaved 32-byte stride was 2-way everywhere)
-  __shared__ __attribute__((aligned(16))) uint4 vbuf[2][2][kNT];
+  // per wave: one row of vertical sums, planar (plane h = dwords 4h..4h+3 of a
+  // lane's 8) so every ds_write_b128 / ds_read_b128 has a 16-byte lane stride
+  __shared__ __attribute__((aligned(16))) uint4 vbuf[kWaves][2][kW];
   __shared__ uint8_t luts[768];
-
-  const int tid = threadIdx.x;
-  const int cb = (int)blockIdx.x * (kOutChunks * 16) - 16 + tid * 16;
-  const bool st = tid >= 1 && tid <= kNT - 2 && cb < a.E;
-  const uint32_t lane_in = cb < a.E + 16 ? (uint32_t)(cb * CIN) : kOOB;
-  const uint32_t lane_out = st ? (uint32_t)cb : kOOB;
-  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);
-  const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
-  int ys, ye;
-  band_range(a, blockIdx.y, ys, ye);
-  if (ys >= ye) return;
   if (PRO != PRO_NONE || a.has_epi) {
     load_luts(a, luts);
     __syncthreads();
   }
+  const WaveTask t = wave_task(a);
+  if (!t.valid) return;
+  const int lane = t.lane;
+  const int ys = t.ys, ye = t.ye;
+  const int cb = t.xt * (kOutChunks * 16) - 16 + lane * 16;
+  const bool st = lane >= 1 && lane <= kW - 2 && cb < a.E;
+  const uint32_t lane_in = cb < a.E + 16 ? (uint32_t)(cb * CIN) : kOOB;
+  const uint32_t lane_out = st ? (uint32_t)cb : kOOB;
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);
+  const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
   const uint32_t last_row = in_row_off(a, ye - 1 + R);
+  uint4(*vb)[kW] = vbuf[t.wave];
+  const int rl = lane == 0 ? 1 : (lane == kW - 1 ? kW - 2 : lane);  // keep LDS reads in bounds
 
   VState<F> sa, sb;
 #pragma unroll
@@ -244,23 +279,22 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : 4)) void k_sep(KArgs a) {
     unpack16(nb, u);
     load_chunk<PRO>(a, rin, y + kPF < ye ? in_row_off(a, y + kPF + R) : last_row, lane_in, luts + 256, nb);
     vpush<F>(u, prev, next, vv);
-    uint4(*vb)[kNT] = vbuf[y & 1];
-    vb[0][tid] = make_uint4(vv[0], vv[1], vv[2], vv[3]);
-    vb[1][tid] = make_uint4(vv[4], vv[5], vv[6], vv[7]);
-    __syncthreads();
-    // lanes 0 and 255 (halo chunks) compute garbage and their store is masked
-    const int rl = tid == 0 ? 1 : (tid == kNT - 1 ? kNT - 2 : tid);  // keep LDS reads in bounds
+    vb[0][lane] = make_uint4(vv[0], vv[1], vv[2], vv[3]);
+    vb[1][lane] = make_uint4(vv[4], vv[5], vv[6], vv[7]);
+    wave_lds_sync();
+    // lanes 0 and 63 (halo chunks) compute garbage and their store is masked
     uint32_t w[WDW];
 #pragma unroll
     for (int q = 0; q < WDW / 4; ++q) {
       // window dword 4q is logical dword g = 8*rl - WLO/2 + 4q: lane g/8, plane (g/4)&1
       const int g = 8 * rl - WLO / 2 + 4 * q;
-      const uint4 t = vb[(g >> 2) & 1][g >> 3];
-      w[4 * q] = t.x;
-      w[4 * q + 1] = t.y;
-      w[4 * q + 2] = t.z;
-      w[4 * q + 3] = t.w;
+      const uint4 v = vb[(g >> 2) & 1][g >> 3];
+      w[4 * q] = v.x;
+      w[4 * q + 1] = v.y;
+      w[4 * q + 2] = v.z;
+      w[4 * q + 3] = v.w;
     }
+    wave_lds_sync();  // reads done before the next row's writes (program order)
     uint32_t o[4];
     if constexpr (T::H16) {
       uint32_t h[8];
@@ -299,15 +333,14 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : 4)) void k_sep(KArgs a) {
     }
     if (a.has_epi) lut16(luts + 512, o);
     const u32x4 ov = {o[0], o[1], o[2], o[3]};
-    // rows past the band (odd band tail) are computed but their store is masked
+    // rows past the band (tail of the 4-row group) are computed but not stored
     __builtin_amdgcn_raw_buffer_store_b128(
         ov, rout, valid ? a.out_org + (uint32_t)((int64_t)y * a.out_pitch) + lane_out : kOOB, 0, 0);
   };
 
-  // ping-pong the filter state so no register copies are needed
+  // rows go in groups of kPF with no branch around any step, ping-ponging the
+  // filter state so no register copies are needed
   constexpr bool live_in_b = ((K - 1) & 1) != 0;
-  // rows go in pairs with no branch around either step (the second one's store
-  // is masked at an odd band end), so hipcc keeps both prefetched rows in flight
   for (int y = ys; y < ye; y += kPF) {
 #pragma unroll
     for (int i = 0; i < kPF; i += 2) {
@@ -320,7 +353,7 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : 4)) void k_sep(KArgs a) {
       }
     }
   }
-  band_margins<C>(a, ys, ye);
+  band_margins<C>(a, t);
 }
 
 // ------------------------------------------------------------------------------
@@ -328,43 +361,43 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : 4)) void k_sep(KArgs a) {
 // ------------------------------------------------------------------------------
 template <int C, class F, int PRO, bool SKIP>
 __global__ __launch_bounds__(kNT, 4) void k_direct(KArgs a) {
-  constexpr int R = F::R, K = F::K, S = K + 1;
+  constexpr int R = F::R, K = F::K, S = K;  // in-order per wave: K slots suffice
   constexpr int CIN = PRO == PRO_GRAY ? 3 : 1;
-  __shared__ __attribute__((aligned(16))) uint4 ring[S][kNT];
+  __shared__ __attribute__((aligned(16))) uint4 ring[kWaves][S][kW];
   __shared__ uint8_t luts[768];
-
-  const int tid = threadIdx.x;
-  const int cb = (int)blockIdx.x * (kOutChunks * 16) - 16 + tid * 16;
-  const bool st = tid >= 1 && tid <= kNT - 2 && cb < a.E;
-  const uint32_t lane_in = cb < a.E + 16 ? (uint32_t)(cb * CIN) : kOOB;
-  const uint32_t lane_out = st ? (uint32_t)cb : kOOB;
-  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);
-  const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
-  int ys, ye;
-  band_range(a, blockIdx.y, ys, ye);
-  if (ys >= ye) return;
   if (PRO != PRO_NONE || a.has_epi) {
     load_luts(a, luts);
     __syncthreads();
   }
+  const WaveTask t = wave_task(a);
+  if (!t.valid) return;
+  const int lane = t.lane;
+  const int ys = t.ys, ye = t.ye;
+  const int cb = t.xt * (kOutChunks * 16) - 16 + lane * 16;
+  const bool st = lane >= 1 && lane <= kW - 2 && cb < a.E;
+  const uint32_t lane_in = cb < a.E + 16 ? (uint32_t)(cb * CIN) : kOOB;
+  const uint32_t lane_out = st ? (uint32_t)cb : kOOB;
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);
+  const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
   const uint32_t last_row = in_row_off(a, ye - 1 + R);
+  uint4(*rg)[kW] = ring[t.wave];
   // slot of row r is (r - (ys - R)) mod S; s0 tracks the slot of row y - R
 #pragma unroll
   for (int i = 0; i < K - 1; ++i) {
     uint32_t r[4];
     load_chunk<PRO>(a, rin, in_row_off(a, ys - R + i), lane_in, luts + 256, r);
-    ring[i][tid] = make_uint4(r[0], r[1], r[2], r[3]);
+    rg[i][lane] = make_uint4(r[0], r[1], r[2], r[3]);
   }
   uint32_t nxt[4];
   load_chunk<PRO>(a, rin, in_row_off(a, ys + R), lane_in, luts + 256, nxt);
-  const int rl = tid == 0 ? 1 : (tid == kNT - 1 ? kNT - 2 : tid);
+  const int rl = lane == 0 ? 1 : (lane == kW - 1 ? kW - 2 : lane);
   int s0 = 0;
   for (int y = ys; y < ye; ++y) {
     int sw = s0 + K - 1;
     if (sw >= S) sw -= S;
-    ring[sw][tid] = make_uint4(nxt[0], nxt[1], nxt[2], nxt[3]);
+    rg[sw][lane] = make_uint4(nxt[0], nxt[1], nxt[2], nxt[3]);
     load_chunk<PRO>(a, rin, y + 1 < ye ? in_row_off(a, y + 1 + R) : last_row, lane_in, luts + 256, nxt);
-    __syncthreads();
+    wave_lds_sync();
     int acc[16], acc2[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc[j] = acc2[j] = 0;
@@ -373,7 +406,7 @@ __global__ __launch_bounds__(kNT, 4) void k_direct(KArgs a) {
     for (int dy = 0; dy < K; ++dy) {
       int sl = s0 + dy;
       if (sl >= S) sl -= S;
-      const uint4 l = ring[sl][rl - 1], m = ring[sl][rl], r = ring[sl][rl + 1];
+      const uint4 l = rg[sl][rl - 1], m = rg[sl][rl], r = rg[sl][rl + 1];
       const uint32_t win[12] = {l.x, l.y, l.z, l.w, m.x, m.y, m.z, m.w, r.x, r.y, r.z, r.w};
       if (dy == R) {
         center[0] = m.x;
@@ -397,6 +430,7 @@ __global__ __launch_bounds__(kNT, 4) void k_direct(KArgs a) {
         }
       }
     }
+    wave_lds_sync();  // window reads done before the next row overwrites a slot
     uint32_t ob[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
@@ -414,7 +448,7 @@ __global__ __launch_bounds__(kNT, 4) void k_direct(KArgs a) {
                                            0, 0);
     s0 = s0 + 1 == S ? 0 : s0 + 1;
   }
-  band_margins<C>(a, ys, ye);
+  band_margins<C>(a, t);
 }
 
 // ------------------------------------------------------------------------------
@@ -449,8 +483,9 @@ inline void plan_bands(KArgs& a, dim3& grid, int tiles, int n0, int n1, int band
   band = (int)align_up(band, 4);
   a.band = band;
   a.nb0 = (int)div_up(n0, band);
-  const int nb1 = (int)div_up(n1, band);
-  grid = dim3((unsigned)tiles, (unsigned)(a.nb0 + nb1));
+  a.nbands = a.nb0 + (int)div_up(n1, band);
+  a.ntx = tiles;
+  grid = dim3((unsigned)div_up((int64_t)tiles * a.nbands, kWaves));
 }
 
 template <int C, class F, int PRO>
@@ -529,7 +564,7 @@ void launch_stencil(const Pass& p, const PassConsts& pc, const PassLaunch& L, hi
   const int n0 = std::max(0, L.ry[1] - L.ry[0]);
   const int n1 = L.nrange > 1 ? std::max(0, L.ry[3] - L.ry[2]) : 0;
   if (n0 + n1 == 0) return;
-  const int tiles = (int)div_up(a.E, dev::kOutChunks * 16);
+  const int tiles = (int)div_up(a.E, dev::kOutChunks * 16);  // wave tiles per row
   a.ry0 = L.ry[0];
   a.ry1 = L.ry[0] + n0;
   a.ry2 = n1 ? L.ry[2] : 0;
