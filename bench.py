@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--band", type=int, default=0)
     ap.add_argument("--dist-steps", type=int, default=5, help="steps of the dist-scope measurement (0: skip)")
+    ap.add_argument("--e2e-steps", type=int, default=3, help="steps of the e2e-scope measurement (0: skip)")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-autotune", action="store_true", help="skip the per-shape band-height autotune")
     ap.add_argument("--backend", default="rccl", choices=["rccl", "host"],
@@ -158,6 +159,25 @@ def main():
         dms = max_over_ranks((t1 - t0) * 1e3) / a.dist_steps
         dist_mpx = W * H / (dms * 1e-3) / 1e6
 
+    # ---- e2e scope (pinned host stripe -> H2D -> filter -> D2H -> pinned host) ----
+    e2e_mpx = None
+    if a.e2e_steps > 0 and dev:
+        eng = dp.engine
+        eng.alloc_host_io()
+        if rows > 0:
+            eng.host_input()[...] = C.synth_rows(a.seed, W, Cc, row0, rows)
+        eng.run_e2e(8)
+        eng.synchronize()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(a.e2e_steps):
+            eng.run_e2e(8)
+        eng.synchronize()
+        barrier()
+        t1 = time.perf_counter()
+        ems = max_over_ranks((t1 - t0) * 1e3) / a.e2e_steps
+        e2e_mpx = W * H / (ems * 1e-3) / 1e6
+
     if rank == 0:
         rec = {
             "metric": METRIC,
@@ -182,6 +202,7 @@ def main():
                 "scope": "resident: halo exchange + full-frame filter per step",
             },
             "dist_scope_mpx_s": None if dist_mpx is None else round(dist_mpx, 1),
+            "e2e_scope_mpx_s": None if e2e_mpx is None else round(e2e_mpx, 1),
             "verified_vs_golden": verify,
             "tuned_band_rows": dp.engine.bands,
         }

@@ -41,6 +41,26 @@ struct EngineConfig {
   bool autotune = false;        // time candidate band heights per stencil pass on first run()
 };
 
+// Page-locked host allocation (hipHostMalloc): the source/destination of the
+// asynchronous H2D/D2H copies of the e2e path (pageable memory would make
+// hipMemcpyAsync synchronous and serialise it with compute).
+class PinnedBuffer {
+ public:
+  PinnedBuffer() = default;
+  explicit PinnedBuffer(size_t bytes);
+  ~PinnedBuffer();
+  PinnedBuffer(const PinnedBuffer&) = delete;
+  PinnedBuffer& operator=(const PinnedBuffer&) = delete;
+  PinnedBuffer(PinnedBuffer&& o) noexcept { *this = std::move(o); }
+  PinnedBuffer& operator=(PinnedBuffer&& o) noexcept;
+  uint8_t* data() const { return p_; }
+  size_t bytes() const { return n_; }
+
+ private:
+  uint8_t* p_ = nullptr;
+  size_t n_ = 0;
+};
+
 // Device or host allocation freed on destruction.
 class Buffer {
  public:
@@ -103,6 +123,19 @@ class Engine {
   void gather();                                          // every stripe -> root output buffer
   void store_root(void* full, bool dst_device);           // rank 0: root output buffer, packed
 
+  // ---- end-to-end (host -> device -> host) ----
+  // Pinned host input/output stripes owned by the engine (packed rows).
+  void alloc_host_io();
+  uint8_t* host_in() const { return host_in_.data(); }
+  uint8_t* host_out() const { return host_out_.data(); }
+  size_t host_in_bytes() const { return host_in_.bytes(); }
+  size_t host_out_bytes() const { return host_out_.bytes(); }
+  // One e2e step: chunked pinned H2D on an upload stream, the chain, chunked D2H
+  // on a download stream.  Single-pass chains are pipelined: the rows of chunk
+  // i are filtered while chunk i+1 uploads and chunk i-1 downloads; the halo
+  // exchange waits only for the first and last chunks.
+  void run_e2e(int chunks = 8);
+
   void synchronize();
   const PhaseTimes& times() const { return times_; }
   // device pointer + pitch of the current input/output stripe origins (for tests)
@@ -143,7 +176,12 @@ class Engine {
   Buffer root_in_, root_out_;
   std::vector<PassRt> prt_;
   hipStream_t s_compute_ = nullptr, s_comm_ = nullptr;
-  bool own_streams_ = false;
+  hipStream_t s_h2d_ = nullptr, s_d2h_ = nullptr;
+  std::vector<hipEvent_t> ev_h2d_, ev_cmp_;
+  PinnedBuffer host_in_, host_out_;
+  PassLaunch make_launch(const Pass& p, const uint8_t* in, uint8_t* out, int pi) const;
+  bool own_streams_ = false;   // s_comm_ (and the e2e streams) are ours
+  bool own_compute_ = false;   // s_compute_ is ours (false after use_external_stream)
   hipEvent_t ev_[8] = {};
   PhaseTimes times_;
   int out_buf_ = -1;        // buffer holding the last run's output

@@ -289,6 +289,27 @@ PYBIND11_MODULE(_C, m) {
         e.run(it);
       }, py::arg("iterations") = 1)
       .def("rewind", &Engine::rewind)
+      .def("alloc_host_io", &Engine::alloc_host_io)
+      .def("host_input", [](py::object self) {
+        Engine& e = self.cast<Engine&>();
+        STRIPE_CHECK(e.host_in() != nullptr, "call alloc_host_io() first");
+        const auto& c = e.config();
+        std::vector<py::ssize_t> shape = {e.stripe().rows, c.W};
+        if (e.plan().cin != 1) shape.push_back(e.plan().cin);
+        return py::array_t<uint8_t>(shape, e.host_in(), self);  // pinned, zero-copy view
+      })
+      .def("host_output", [](py::object self) {
+        Engine& e = self.cast<Engine&>();
+        STRIPE_CHECK(e.host_out() != nullptr, "call alloc_host_io() first");
+        const auto& c = e.config();
+        std::vector<py::ssize_t> shape = {e.stripe().rows, c.W};
+        if (e.plan().cout != 1) shape.push_back(e.plan().cout);
+        return py::array_t<uint8_t>(shape, e.host_out(), self);
+      })
+      .def("run_e2e", [](Engine& e, int chunks) {
+        py::gil_scoped_release nogil;
+        e.run_e2e(chunks);
+      }, py::arg("chunks") = 8)
       .def_property_readonly("bands", &Engine::bands)
       .def("gather", [](Engine& e) {
         py::gil_scoped_release nogil;

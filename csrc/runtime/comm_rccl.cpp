@@ -35,6 +35,7 @@ class RcclComm final : public Comm {
     }
     if (bar_buf_) (void)hipFree(bar_buf_);
     if (bar_stream_) (void)hipStreamDestroy(bar_stream_);
+    (void)hipGetLastError();
   }
   int rank() const override { return rank_; }
   int size() const override { return world_; }

@@ -43,6 +43,25 @@ Buffer& Buffer::operator=(Buffer&& o) noexcept {
   return *this;
 }
 
+PinnedBuffer::PinnedBuffer(size_t bytes) : n_(bytes) {
+  if (bytes) HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p_), bytes, hipHostMallocDefault));
+}
+
+PinnedBuffer::~PinnedBuffer() {
+  if (p_) (void)hipHostFree(p_);
+}
+
+PinnedBuffer& PinnedBuffer::operator=(PinnedBuffer&& o) noexcept {
+  if (this != &o) {
+    if (p_) (void)hipHostFree(p_);
+    p_ = o.p_;
+    n_ = o.n_;
+    o.p_ = nullptr;
+    o.n_ = 0;
+  }
+  return *this;
+}
+
 // ---------------------------------------------------------------------------
 // Engine
 // ---------------------------------------------------------------------------
@@ -66,6 +85,7 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
     HIP_CHECK(hipStreamCreateWithFlags(&s_compute_, hipStreamNonBlocking));
     HIP_CHECK(hipStreamCreateWithFlags(&s_comm_, hipStreamNonBlocking));
     own_streams_ = true;
+    own_compute_ = true;
     for (auto& e : ev_) HIP_CHECK(hipEventCreate(&e));
   }
   // one extra all-zero row at the end of each stripe buffer: the Constant
@@ -106,19 +126,23 @@ Engine::~Engine() {
       if (p.pc.conv) (void)hipFree(p.pc.conv);
     for (auto& e : ev_)
       if (e) (void)hipEventDestroy(e);
-    if (own_streams_) {
-      (void)hipStreamDestroy(s_comm_);
-      if (s_compute_) (void)hipStreamDestroy(s_compute_);
-    }
+    for (auto& e : ev_h2d_) (void)hipEventDestroy(e);
+    for (auto& e : ev_cmp_) (void)hipEventDestroy(e);
+    if (s_h2d_) (void)hipStreamDestroy(s_h2d_);
+    if (s_d2h_) (void)hipStreamDestroy(s_d2h_);
+    if (own_streams_) (void)hipStreamDestroy(s_comm_);
+    if (own_compute_ && s_compute_) (void)hipStreamDestroy(s_compute_);
+    (void)hipGetLastError();  // teardown errors must not leak into the caller's next HIP check
   }
 }
 
 void Engine::use_external_stream(hipStream_t s) {
   STRIPE_CHECK(device(), "external streams need the device backend");
-  if (own_streams_ && s_compute_) {
+  if (own_compute_ && s_compute_) {
     HIP_CHECK(hipStreamSynchronize(s_compute_));
     HIP_CHECK(hipStreamDestroy(s_compute_));
   }
+  own_compute_ = false;  // never destroy a stream we do not own (e.g. torch's)
   s_compute_ = s;
 }
 
@@ -149,7 +173,10 @@ void Engine::record(hipEvent_t e, hipStream_t s) {
 
 float Engine::elapsed(hipEvent_t a, hipEvent_t b) {
   float ms = 0;
-  if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0;
+  if (hipEventElapsedTime(&ms, a, b) != hipSuccess) {
+    (void)hipGetLastError();  // an unrecorded event is not an error here; keep the sticky state clean
+    return 0;
+  }
   return ms;
 }
 
@@ -279,6 +306,36 @@ void Engine::exchange_halo(uint8_t* org, int C, int R, hipStream_t s) {
   comm_->group_end();
 }
 
+PassLaunch Engine::make_launch(const Pass& p, const uint8_t* in, uint8_t* out, int pi) const {
+  const RowGeom g = geom();
+  PassLaunch L;
+  L.in = in;
+  L.in_pitch = pitch(p.cin);
+  L.out = out;
+  L.out_pitch = pitch(p.cout);
+  L.W = cfg_.W;
+  L.rows = stripe().rows;
+  L.row0 = g.row0;
+  L.Hg = g.Hg;
+  L.zero_row = zero_.data() + kMarginBytes;
+  L.band = prt_[pi].band > 0 ? prt_[pi].band : cfg_.band;
+  const Buffer* bi = nullptr;
+  const Buffer* bo = nullptr;
+  for (const Buffer& b : buf_) {
+    if (in >= b.data() && in < b.data() + b.bytes()) bi = &b;
+    if (out >= b.data() && out < b.data() + b.bytes()) bo = &b;
+  }
+  STRIPE_CHECK(bi && bo && bi != bo, "pass buffers are not the engine's ping-pong pair");
+  L.in_base = bi->data();
+  L.in_bytes = (int64_t)bi->bytes();
+  L.in_org = in - bi->data();
+  L.in_zero = (int64_t)std::max(1, rows_alloc_) * padded_pitch(cfg_.W, plan_.max_channels) + kMarginBytes;
+  L.out_base = bo->data();
+  L.out_bytes = (int64_t)bo->bytes();
+  L.out_org = out - bo->data();
+  return L;
+}
+
 void Engine::run_pass(const Pass& p, const uint8_t* in, uint8_t* out) {
   const Stripe& st = stripe();
   const int rows = st.rows;
@@ -293,30 +350,7 @@ void Engine::run_pass(const Pass& p, const uint8_t* in, uint8_t* out) {
   }
   const size_t pi = (size_t)(&p - plan_.passes.data());
   const PassConsts& pc = prt_[pi].pc;
-  PassLaunch L;
-  L.in = in;
-  L.in_pitch = pitch(p.cin);
-  L.out = out;
-  L.out_pitch = pitch(p.cout);
-  L.W = cfg_.W;
-  L.rows = rows;
-  L.row0 = g.row0;
-  L.Hg = g.Hg;
-  L.zero_row = zero_.data() + kMarginBytes;
-  L.band = prt_[pi].band > 0 ? prt_[pi].band : cfg_.band;
-  {
-    const Buffer& bi = buf_[cur_];
-    const Buffer& bo = buf_[cur_ ^ 1];
-    STRIPE_CHECK(in >= bi.data() && in < bi.data() + bi.bytes() && out >= bo.data() && out < bo.data() + bo.bytes(),
-                 "pass buffers are not the engine's current ping-pong pair");
-    L.in_base = bi.data();
-    L.in_bytes = (int64_t)bi.bytes();
-    L.in_org = in - bi.data();
-    L.in_zero = (int64_t)std::max(1, rows_alloc_) * padded_pitch(cfg_.W, plan_.max_channels) + kMarginBytes;
-    L.out_base = bo.data();
-    L.out_bytes = (int64_t)bo.bytes();
-    L.out_org = out - bo.data();
-  }
+  PassLaunch L = make_launch(p, in, out, (int)pi);
   if (!xchg) {
     L.nrange = 1;
     L.ry[0] = 0;
@@ -370,25 +404,8 @@ void Engine::autotune_bands() {
       prt_[i].band = b;
       float tot = 0;
       for (int rep = 0; rep < 4; ++rep) {
-        PassLaunch L;
-        L.in = origin(buf_[cur_], p.cin);
-        L.in_pitch = pitch(p.cin);
-        L.out = origin(buf_[cur_ ^ 1], p.cout);
-        L.out_pitch = pitch(p.cout);
-        L.W = cfg_.W;
-        L.rows = stripe().rows;
-        const RowGeom g = geom();
-        L.row0 = g.row0;
-        L.Hg = g.Hg;
-        L.zero_row = zero_.data() + kMarginBytes;
+        PassLaunch L = make_launch(p, origin(buf_[cur_], p.cin), origin(buf_[cur_ ^ 1], p.cout), (int)i);
         L.band = b;
-        L.in_base = buf_[cur_].data();
-        L.in_bytes = (int64_t)buf_[cur_].bytes();
-        L.in_org = L.in - buf_[cur_].data();
-        L.in_zero = (int64_t)std::max(1, rows_alloc_) * padded_pitch(cfg_.W, plan_.max_channels) + kMarginBytes;
-        L.out_base = buf_[cur_ ^ 1].data();
-        L.out_bytes = (int64_t)buf_[cur_ ^ 1].bytes();
-        L.out_org = L.out - buf_[cur_ ^ 1].data();
         L.ry[0] = 0;
         L.ry[1] = L.rows;
         HIP_CHECK(hipEventRecord(e0, s_compute_));
@@ -429,6 +446,119 @@ void Engine::run(int iterations) {
 void Engine::rewind() {
   cur_ = run_in_buf_;
   cur_c_ = plan_.cin;
+}
+
+void Engine::alloc_host_io() {
+  const Stripe& st = stripe();
+  host_in_ = PinnedBuffer(std::max<size_t>(1, (size_t)st.rows * cfg_.W * plan_.cin));
+  host_out_ = PinnedBuffer(std::max<size_t>(1, (size_t)st.rows * cfg_.W * plan_.cout));
+}
+
+void Engine::run_e2e(int chunks) {
+  STRIPE_CHECK(device(), "run_e2e needs the device backend");
+  STRIPE_CHECK(host_in_.data() && host_out_.data(), "call alloc_host_io() first");
+  const Stripe& st = stripe();
+  const int rows = st.rows;
+  if (rows == 0) return;
+  if (!s_h2d_) {
+    HIP_CHECK(hipStreamCreateWithFlags(&s_h2d_, hipStreamNonBlocking));
+    HIP_CHECK(hipStreamCreateWithFlags(&s_d2h_, hipStreamNonBlocking));
+  }
+  chunks = std::max(1, std::min(chunks, rows));
+  while ((int)ev_h2d_.size() < chunks + 1) {
+    hipEvent_t e1, e2;
+    HIP_CHECK(hipEventCreateWithFlags(&e1, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&e2, hipEventDisableTiming));
+    ev_h2d_.push_back(e1);
+    ev_cmp_.push_back(e2);
+  }
+  const int cin = plan_.cin, cout = plan_.cout;
+  const int64_t Ein = (int64_t)cfg_.W * cin, Eout = (int64_t)cfg_.W * cout;
+  std::vector<int> cut(chunks + 1);
+  for (int i = 0; i <= chunks; ++i) cut[i] = (int)((int64_t)rows * i / chunks);
+  // previous step's download must finish before this step's output buffer is reused
+  HIP_CHECK(hipEventRecord(ev_[2], s_d2h_));
+  HIP_CHECK(hipStreamWaitEvent(s_compute_, ev_[2], 0));
+  HIP_CHECK(hipEventRecord(ev_[3], s_compute_));
+  HIP_CHECK(hipStreamWaitEvent(s_h2d_, ev_[3], 0));  // ...and this step's input buffer is free
+  cur_ = 0;
+  cur_c_ = cin;
+  uint8_t* in_org = origin(buf_[0], cin);
+  for (int i = 0; i < chunks; ++i) {
+    copy2d(in_org + (int64_t)cut[i] * pitch(cin), pitch(cin), host_in_.data() + (int64_t)cut[i] * Ein, Ein, Ein,
+           cut[i + 1] - cut[i], s_h2d_, 0);
+    fill_margins(in_org, cin, cut[i], cut[i + 1], plan_.in_margin_px, plan_.in_margin_border, s_h2d_);
+    HIP_CHECK(hipEventRecord(ev_h2d_[i], s_h2d_));
+  }
+  const bool single = plan_.passes.size() == 1;
+  if (!single) {
+    // multi-pass chains: upload overlapped with nothing but the download of the
+    // previous step; the chain itself runs as usual
+    HIP_CHECK(hipStreamWaitEvent(s_compute_, ev_h2d_[chunks - 1], 0));
+    run(1);
+    HIP_CHECK(hipEventRecord(ev_cmp_[0], s_compute_));
+    HIP_CHECK(hipStreamWaitEvent(s_d2h_, ev_cmp_[0], 0));
+    copy2d(host_out_.data(), Eout, origin(buf_[out_buf_], cout), pitch(cout), Eout, rows, s_d2h_, 0);
+    return;
+  }
+  const Pass& p = plan_.passes[0];
+  const int R = p.R;
+  const bool xchg = cfg_.halo && R > 0 && part_.active > 1;
+  const bool up = xchg && rank_ > 0;
+  const bool down = xchg && rank_ + 1 < part_.active;
+  uint8_t* out_org = origin(buf_[1], cout);
+  PassLaunch L = make_launch(p, in_org, out_org, 0);
+  if (xchg) {  // halo rows come from the first and last chunks
+    HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_h2d_[0], 0));
+    HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_h2d_[chunks - 1], 0));
+    exchange_halo(in_org, cin, R, s_comm_);
+    HIP_CHECK(hipEventRecord(ev_[5], s_comm_));
+  }
+  const int lo_lim = up ? std::min(R, rows) : 0;
+  const int hi_lim = down ? std::max(lo_lim, rows - R) : rows;
+  int done = lo_lim;
+  std::vector<std::pair<int, int>> ranges(chunks, {0, 0});
+  for (int i = 0; i < chunks; ++i) {
+    HIP_CHECK(hipStreamWaitEvent(s_compute_, ev_h2d_[i], 0));
+    const int avail = i == chunks - 1 ? rows : std::max(0, cut[i + 1] - R);  // inputs loaded for y + R
+    const int hi = std::min(avail, hi_lim);
+    if (hi > done) {
+      L.nrange = 1;
+      L.ry[0] = done;
+      L.ry[1] = hi;
+      launch_pass(p, prt_[0].pc, L, s_compute_);
+      ranges[i] = {done, hi};
+      done = hi;
+    }
+    HIP_CHECK(hipEventRecord(ev_cmp_[i], s_compute_));
+    HIP_CHECK(hipStreamWaitEvent(s_d2h_, ev_cmp_[i], 0));
+    if (ranges[i].second > ranges[i].first)
+      copy2d(host_out_.data() + (int64_t)ranges[i].first * Eout, Eout, out_org + (int64_t)ranges[i].first * pitch(cout),
+             pitch(cout), Eout, ranges[i].second - ranges[i].first, s_d2h_, 0);
+  }
+  if (xchg) {  // boundary rows once the neighbours' halos are in
+    HIP_CHECK(hipStreamWaitEvent(s_compute_, ev_[5], 0));
+    L.nrange = 0;
+    if (up) {
+      L.ry[2 * L.nrange] = 0;
+      L.ry[2 * L.nrange + 1] = lo_lim;
+      ++L.nrange;
+    }
+    if (down) {
+      L.ry[2 * L.nrange] = hi_lim;
+      L.ry[2 * L.nrange + 1] = rows;
+      ++L.nrange;
+    }
+    if (L.nrange > 0) launch_pass(p, prt_[0].pc, L, s_compute_);
+    HIP_CHECK(hipEventRecord(ev_cmp_[chunks], s_compute_));
+    HIP_CHECK(hipStreamWaitEvent(s_d2h_, ev_cmp_[chunks], 0));
+    if (up) copy2d(host_out_.data(), Eout, out_org, pitch(cout), Eout, lo_lim, s_d2h_, 0);
+    if (down)
+      copy2d(host_out_.data() + (int64_t)hi_lim * Eout, Eout, out_org + (int64_t)hi_lim * pitch(cout), pitch(cout),
+             Eout, rows - hi_lim, s_d2h_, 0);
+  }
+  out_buf_ = 1;
+  out_c_ = cout;
 }
 
 void Engine::store_packed(void* dst, bool dst_device) {
@@ -482,6 +612,8 @@ void Engine::synchronize() {
   if (!device()) return;
   HIP_CHECK(hipStreamSynchronize(s_compute_));
   HIP_CHECK(hipStreamSynchronize(s_comm_));
+  if (s_h2d_) HIP_CHECK(hipStreamSynchronize(s_h2d_));
+  if (s_d2h_) HIP_CHECK(hipStreamSynchronize(s_d2h_));
   times_.run = elapsed(ev_[0], ev_[1]);
 }
 
