@@ -156,8 +156,11 @@ Plan compile_chain(const std::vector<Op>& ops, int cin, Border default_border, b
       p.K = op.K;
       p.R = op.K / 2;
       p.conv_w = op.weights;
+      p.sep_h = op.sep_h;
+      p.sep_v = op.sep_v;
       p.cin = p.cmid = p.cout = c;
-      p.desc = "conv" + std::to_string(op.K) + "x" + std::to_string(op.K) + "(mfma) " +
+      p.desc = "conv" + std::to_string(op.K) + "x" + std::to_string(op.K) +
+               (p.sep_h.empty() ? "(mfma) " : "(mfma-separable) ") +
                std::to_string(c) + "ch border=" + border_name(p.border);
     } else {
       const StencilInfo& si = stencil_info(op.sid);

@@ -159,6 +159,9 @@ static Op make_conv_blur(int K, double sigma, const std::string& text) {
   op.weights.resize((size_t)K * K);
   for (int i = 0; i < K; ++i)
     for (int j = 0; j < K; ++j) op.weights[(size_t)i * K + j] = (float)(g[i] * g[j]);
+  op.sep_h.resize((size_t)K);
+  for (int i = 0; i < K; ++i) op.sep_h[(size_t)i] = (float)g[i];
+  op.sep_v = op.sep_h;
   op.text = text;
   return op;
 }
@@ -242,6 +245,21 @@ std::vector<Op> parse_chain(const std::string& spec_in) {
       STRIPE_CHECK((int)op.weights.size() == op.K * op.K,
                    "conv:" << op.K << " needs " << op.K * op.K << " weights, got " << op.weights.size());
       op.text = tok;
+    } else if (name == "sepconv") {
+      // sepconv:K:h0;...;h(K-1):v0;...;v(K-1)  rank-one KxK correlation
+      // weights[dy][dx] = v[dy] * h[dx] (separable MFMA path on the GPU)
+      STRIPE_CHECK(parts.size() == 4, "sepconv syntax: sepconv:K:h0;...;h(K-1):v0;...;v(K-1)");
+      op.kind = OpKind::Conv;
+      op.K = (int)parse_num(parts[1], tok);
+      STRIPE_CHECK(op.K >= 1 && op.K % 2 == 1 && op.K / 2 <= kMaxRadius, "sepconv K must be odd <= 33");
+      for (const auto& w : split(parts[2], ';')) op.sep_h.push_back((float)parse_num(trim(w), tok));
+      for (const auto& w : split(parts[3], ';')) op.sep_v.push_back((float)parse_num(trim(w), tok));
+      STRIPE_CHECK((int)op.sep_h.size() == op.K && (int)op.sep_v.size() == op.K,
+                   "sepconv:" << op.K << " needs " << op.K << " horizontal and " << op.K << " vertical weights");
+      op.weights.resize((size_t)op.K * op.K);
+      for (int i = 0; i < op.K; ++i)
+        for (int j = 0; j < op.K; ++j) op.weights[(size_t)i * op.K + j] = op.sep_v[(size_t)i] * op.sep_h[(size_t)j];
+      op.text = tok;
     } else if (stencil_from_name(name, &sid)) {
       op.kind = OpKind::Stencil;
       op.sid = sid;
@@ -249,7 +267,7 @@ std::vector<Op> parse_chain(const std::string& spec_in) {
     } else {
       fail("unknown filter '" + name +
            "' (gray[:ref|bt601], contrast:F[:cv], invert, brightness:D, threshold:T, expand, "
-           "emboss3, emboss5, gaussian3/5/7, box3/5, sharpen, laplace, sobel, blur:K[:sigma], conv:K:w..)");
+           "emboss3, emboss5, gaussian3/5/7, box3/5, sharpen, laplace, sobel, blur:K[:sigma], conv:K:w.., sepconv:K:h..:v..)");
     }
     if (op.has_border) op.text += std::string("@") + border_name(op.border);
     ops.push_back(op);

@@ -101,6 +101,7 @@ __global__ __launch_bounds__(256) void k_conv_mfma(ConvArgs ca) {
 // T_ky[k][n] = w[ky][k - n] for 0 <= k - n < K (k: window pixel, n: output pixel),
 // laid out as MFMA B fragments (lane l holds B[k = 8(l>>4)+j][n = l&15], j = 0..7).
 void prepare_conv_consts(const Pass& p, PassConsts* pc, hipStream_t s) {
+  if (sep_supported(p)) return prepare_sep_consts(p, pc, s);
   const int K = p.K;
   STRIPE_CHECK(K - 1 + dev::kCTN <= dev::kCTK, "conv K=" << K << " exceeds the 64-pixel window");
   std::vector<_Float16> host((size_t)K * 2 * 2 * 2 * 512);
@@ -127,6 +128,7 @@ void prepare_conv_consts(const Pass& p, PassConsts* pc, hipStream_t s) {
 }
 
 void launch_conv(const Pass& p, const PassConsts& pc, const PassLaunch& L, hipStream_t s) {
+  if (sep_supported(p)) return launch_blur_sep(p, pc, L, s);
   STRIPE_CHECK(pc.conv != nullptr, "conv pass constants not prepared");
   dev::ConvArgs ca{};
   dev::KArgs& a = ca.a;

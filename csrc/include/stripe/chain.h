@@ -47,6 +47,7 @@ struct Pass {
   int K = 1, R = 0;
   Border border = Border::Reflect101;
   std::vector<float> conv_w;  // Conv: K*K weights
+  std::vector<float> sep_h, sep_v;  // Conv: 1-D factors of a rank-one window (separable MFMA path)
   // x-margin contract for the output (what the next stencil consumer needs)
   int out_margin_px = 0;
   Border out_margin_border = Border::Reflect101;

@@ -70,6 +70,7 @@ struct Op {
   StencilId sid = StencilId::Gaussian5;
   int K = 0;                  // conv window
   std::vector<float> weights; // conv: K*K f32 weights
+  std::vector<float> sep_h, sep_v;  // conv: 1-D factors when weights[dy][dx] = sep_v[dy] * sep_h[dx]
   std::string text;           // canonical spelling
   bool has_border = false;    // per-op border override ("gaussian5@replicate")
   Border border = Border::Reflect101;

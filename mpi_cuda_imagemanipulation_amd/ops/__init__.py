@@ -41,6 +41,7 @@ FILTERS = {
     "sobel": "sat(|Gx| + |Gy|)",
     "blur:K[:sigma]": "KxK float Gaussian (MFMA implicit-GEMM path), K <= 33",
     "conv:K:w0;w1;...": "generic KxK float correlation (MFMA path)",
+    "sepconv:K:h..:v..": "rank-one KxK float correlation v (x) h (separable MFMA path)",
     "...@border": "per-stencil border: reflect101 | replicate | constant | skip",
 }
 
@@ -179,6 +180,18 @@ def conv2d(x, weights, border: str = "reflect101"):
     return apply(x, f"conv:{K}:{spec}", border)
 
 
+def sep_conv2d(x, h, v, border: str = "reflect101"):
+    """Rank-one KxK correlation, weights[dy][dx] = v[dy] * h[dx] (separable MFMA path)."""
+    h = np.asarray(h, dtype=np.float64).reshape(-1)
+    v = np.asarray(v, dtype=np.float64).reshape(-1)
+    K = h.shape[0]
+    if v.shape[0] != K or K % 2 == 0:
+        raise ValueError("h and v must have the same odd length")
+    hs = ";".join(repr(float(t)) for t in h)
+    vs = ";".join(repr(float(t)) for t in v)
+    return apply(x, f"sepconv:{K}:{hs}:{vs}", border)
+
+
 def large_blur(x, ksize: int = 31, sigma: float = 0.0, border: str = "reflect101"):
     return apply(x, f"blur:{ksize}:{sigma}" if sigma > 0 else f"blur:{ksize}", border)
 
@@ -190,5 +203,5 @@ def clear_cache() -> None:
 
 __all__ = [
     "FILTERS", "apply", "reference", "grayscale", "contrast", "invert", "brightness", "threshold",
-    "gaussian_blur", "box_blur", "sobel", "sharpen", "laplace", "emboss", "conv2d", "large_blur", "clear_cache",
+    "gaussian_blur", "box_blur", "sobel", "sharpen", "laplace", "emboss", "conv2d", "sep_conv2d", "large_blur", "clear_cache",
 ]

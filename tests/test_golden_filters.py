@@ -117,6 +117,21 @@ def test_conv_generic_equals_integer_stencil(rng):
     assert np.abs(got.astype(int) - ref.astype(int)).max() <= 1
 
 
+def test_sepconv_equals_outer_product_conv(rng):
+    x = img3(rng, 21, 18)
+    h = np.array([0.1, -0.2, 0.5, 0.3, 0.05])
+    v = np.array([0.25, 0.5, 0.125, 0.0625, 0.0625])
+    got = ops.sep_conv2d(x, h, v)
+    ref = ops.conv2d(x, np.outer(v, h).astype(np.float32).astype(np.float64))
+    assert np.abs(got.astype(int) - ref.astype(int)).max() <= 1
+
+
+@pytest.mark.parametrize("bad", ["sepconv:3:1;2;3", "sepconv:3:1;2:1;2;3", "sepconv:4:1;2;3;4:1;2;3;4"])
+def test_sepconv_parse_errors(bad):
+    with pytest.raises(Exception):
+        C.parse_chain(bad)
+
+
 def test_reference_chains(rng):
     x = img3(rng, 24, 20)
     g = np_ref.gray_ref(x)

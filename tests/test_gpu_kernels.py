@@ -64,14 +64,44 @@ def test_chains_exact(m, rng, chain, shape):
     assert got.shape == ref.shape and (got == ref).all(), chain
 
 
-@pytest.mark.parametrize("K", [3, 9, 31])
+@pytest.mark.parametrize("K", [3, 5, 9, 15, 25, 31, 33])
 @pytest.mark.parametrize("C", [1, 3])
-def test_mfma_conv_blur(m, rng, K, C):
-    img = rng.integers(0, 256, size=(70, 97, C) if C == 3 else (70, 97), dtype=np.uint8)
-    got = _run(m, img, f"blur:{K}")
-    ref = m._C.golden_apply(img, f"blur:{K}", "reflect101", True)
+@pytest.mark.parametrize("shape", [(70, 97), (1, 1), (3, 40), (161, 700), (40, 2100)])
+def test_mfma_conv_blur(m, rng, K, C, shape):
+    # blur:K takes the separable MFMA path (rank-one window)
+    img = rng.integers(0, 256, size=shape + (C,) if C == 3 else shape, dtype=np.uint8)
+    for border in ("reflect101", "replicate", "constant"):
+        got = _run(m, img, f"blur:{K}", border)
+        ref = m._C.golden_apply(img, f"blur:{K}", border, True)
+        d = np.abs(got.astype(int) - ref.astype(int))
+        assert d.max() <= 1 and (d == 0).mean() > 0.995, (K, C, shape, border, d.max(), (d == 0).mean())
+
+
+@pytest.mark.parametrize("C", [1, 3])
+@pytest.mark.parametrize("K", [5, 17, 33])
+def test_mfma_sepconv_asymmetric(m, rng, C, K):
+    # distinct, asymmetric h and v catch transposed / mirrored fragment maps
+    h = rng.uniform(-0.5, 1.0, K)
+    v = rng.uniform(-0.25, 1.0, K)
+    h /= h.sum()
+    v /= v.sum()
+    img = rng.integers(0, 256, size=(90, 333, C) if C == 3 else (90, 333), dtype=np.uint8)
+    got = m.ops.sep_conv2d(torch.from_numpy(img).cuda(), h, v).cpu().numpy()
+    ref = m.ops.sep_conv2d(img, h, v)
     d = np.abs(got.astype(int) - ref.astype(int))
-    assert d.max() <= 1 and (d == 0).mean() > 0.995
+    assert d.max() <= 1 and (d == 0).mean() > 0.99, (d.max(), (d == 0).mean())
+
+
+def test_mfma_sep_matches_general_conv(m, rng):
+    # the same rank-one window through the separable and the general (Toeplitz) MFMA kernels
+    K = 9
+    g = np.exp(-np.linspace(-2, 2, K) ** 2)
+    g /= g.sum()
+    img = rng.integers(0, 256, size=(64, 300, 3), dtype=np.uint8)
+    x = torch.from_numpy(img).cuda()
+    a = m.ops.sep_conv2d(x, g, g).cpu().numpy()
+    b = m.ops.conv2d(x, np.outer(g, g).astype(np.float32).astype(np.float64)).cpu().numpy()
+    assert np.abs(a.astype(int) - b.astype(int)).max() <= 1
 
 
 def test_mfma_conv_asymmetric_weights(m, rng):

@@ -37,6 +37,7 @@ CORE_SOURCES = [
     "hip/pointwise.hip",
     "hip/stencil.hip",
     "hip/conv.hip",
+    "hip/blur_sep.hip",
     "hip/dispatch.cpp",
     "runtime/comm_rccl.cpp",
     "runtime/comm_local.cpp",
