@@ -72,8 +72,12 @@ enum { PRO_NONE = 0, PRO_LUT = 1, PRO_GRAY = 2 };
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
+typedef short i16x2 __attribute__((ext_vector_type(2)));
+
 __device__ __forceinline__ u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
 __device__ __forceinline__ uint32_t as_u32(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ i16x2 as_i16x2(uint32_t x) { return __builtin_bit_cast(i16x2, x); }
+__device__ __forceinline__ uint32_t as_u32(i16x2 x) { return __builtin_bit_cast(uint32_t, x); }
 
 // Load the lane's 16 output-channel bytes of the input row at `row_off`
 // (after the prologue).  `lane_off` carries kOOB for lanes that must not load.
@@ -189,9 +193,24 @@ __device__ __forceinline__ uint32_t pair_at(const uint32_t (&w)[WDW], int k) {
 // s_k[y] = s_{k-1}[y] + s_{k-1}[y-1] (K-1 state rows); others: the last K rows.
 template <class F>
 struct VState {
-  static constexpr int NS = F::BINOM ? F::K - 1 : F::K;
+  static constexpr int NS = F::BINOM ? F::K - 1 : F::SOBEL ? 2 : F::K;
   uint32_t s[NS][8];
 };
+
+// Sobel: push one row; `sm` = r0 + 2 r1 + r2 (smoothing, u16) and `df` = r2 - r0
+// (difference, i16) of the row above it.  State: the two previous rows.
+template <class F>
+__device__ __forceinline__ void vpush_sobel(const uint32_t (&row)[8], const VState<F>& prev, VState<F>& next,
+                                            uint32_t (&sm)[8], uint32_t (&df)[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    next.s[0][k] = prev.s[1][k];
+    next.s[1][k] = row[k];
+    const u16x2 r0 = as_u16x2(prev.s[0][k]), r1 = as_u16x2(prev.s[1][k]), r2 = as_u16x2(row[k]);
+    sm[k] = as_u32(r0 + r2 + (r1 << (unsigned short)1));
+    df[k] = as_u32(as_i16x2(row[k]) - as_i16x2(prev.s[0][k]));
+  }
+}
 
 // Push one unpacked row; `v` receives the vertical sums of the row R above it.
 template <class F>
@@ -231,7 +250,9 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : 4)) void k_sep(KArgs a) {
   using T = SepTraits<F>;
   // per wave: one row of vertical sums, planar (plane h = dwords 4h..4h+3 of a
   // lane's 8) so every ds_write_b128 / ds_read_b128 has a 16-byte lane stride
-  __shared__ __attribute__((aligned(16))) uint4 vbuf[kWaves][2][kW];
+  // (sobel: planes 2..3 hold the difference row)
+  constexpr int NP = F::SOBEL ? 4 : 2;
+  __shared__ __attribute__((aligned(16))) uint4 vbuf[kWaves][NP][kW];
   __shared__ uint8_t luts[768];
   if (PRO != PRO_NONE || a.has_epi) {
     load_luts(a, luts);
@@ -262,8 +283,13 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : 4)) void k_sep(KArgs a) {
     uint32_t r[4], u[8];
     load_chunk<PRO>(a, rin, in_row_off(a, ys - R + i), lane_in, luts + 256, r);
     unpack16(r, u);
-    if (i & 1) vpush<F>(u, sb, sa, vdummy);
-    else vpush<F>(u, sa, sb, vdummy);
+    if constexpr (F::SOBEL) {
+      if (i & 1) vpush_sobel<F>(u, sb, sa, vdummy, vdummy);
+      else vpush_sobel<F>(u, sa, sb, vdummy, vdummy);
+    } else {
+      if (i & 1) vpush<F>(u, sb, sa, vdummy);
+      else vpush<F>(u, sa, sb, vdummy);
+    }
   }
   // kPF rows in flight per lane (memory-level parallelism is what this streaming
   // kernel is bound by); loads past the band re-read its last input row
@@ -275,10 +301,16 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : 4)) void k_sep(KArgs a) {
     load_chunk<PRO>(a, rin, ys + i < ye ? in_row_off(a, ys + i + R) : last_row, lane_in, luts + 256, nx[i]);
 
   auto row_step = [&](int y, const VState<F>& prev, VState<F>& next, uint32_t (&nb)[4], bool valid) {
-    uint32_t u[8], vv[8];
+    uint32_t u[8], vv[8], dd[8];
     unpack16(nb, u);
     load_chunk<PRO>(a, rin, y + kPF < ye ? in_row_off(a, y + kPF + R) : last_row, lane_in, luts + 256, nb);
-    vpush<F>(u, prev, next, vv);
+    if constexpr (F::SOBEL) {
+      vpush_sobel<F>(u, prev, next, vv, dd);
+      vb[2][lane] = make_uint4(dd[0], dd[1], dd[2], dd[3]);
+      vb[3][lane] = make_uint4(dd[4], dd[5], dd[6], dd[7]);
+    } else {
+      vpush<F>(u, prev, next, vv);
+    }
     vb[0][lane] = make_uint4(vv[0], vv[1], vv[2], vv[3]);
     vb[1][lane] = make_uint4(vv[4], vv[5], vv[6], vv[7]);
     wave_lds_sync();
@@ -294,9 +326,34 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : 4)) void k_sep(KArgs a) {
       w[4 * q + 2] = v.z;
       w[4 * q + 3] = v.w;
     }
+    uint32_t wd[F::SOBEL ? WDW : 1];
+    if constexpr (F::SOBEL) {
+#pragma unroll
+      for (int q = 0; q < WDW / 4; ++q) {
+        const int g = 8 * rl - WLO / 2 + 4 * q;
+        const uint4 v = vb[2 + ((g >> 2) & 1)][g >> 3];
+        wd[4 * q] = v.x;
+        wd[4 * q + 1] = v.y;
+        wd[4 * q + 2] = v.z;
+        wd[4 * q + 3] = v.w;
+      }
+    }
     wave_lds_sync();  // reads done before the next row's writes (program order)
     uint32_t o[4];
-    if constexpr (T::H16) {
+    if constexpr (F::SOBEL) {
+      // Gx = S[x+C] - S[x-C], Gy = D[x-C] + 2 D[x] + D[x+C], out = min(|Gx| + |Gy|, 255)
+      uint32_t h[8];
+#pragma unroll
+      for (int pp = 0; pp < 8; ++pp) {
+        const i16x2 gx = as_i16x2(pair_at(w, WLO + 2 * pp + C)) - as_i16x2(pair_at(w, WLO + 2 * pp - C));
+        const i16x2 gy = as_i16x2(pair_at(wd, WLO + 2 * pp - C)) + as_i16x2(pair_at(wd, WLO + 2 * pp + C)) +
+                         (as_i16x2(pair_at(wd, WLO + 2 * pp)) << (short)1);
+        const i16x2 m = __builtin_elementwise_max(gx, -gx) + __builtin_elementwise_max(gy, -gy);
+        h[pp] = as_u32(__builtin_elementwise_min(m, (i16x2)(short)255));
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = __builtin_amdgcn_perm(h[2 * q + 1], h[2 * q], 0x06040200u);
+    } else if constexpr (T::H16) {
       uint32_t h[8];
 #pragma unroll
       for (int pp = 0; pp < 8; ++pp) {

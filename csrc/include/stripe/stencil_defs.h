@@ -60,10 +60,13 @@ struct Laplace {
 };
 
 // Sobel: Gx = [1,2,1]^T (x) [-1,0,1],  Gy = [-1,0,1]^T (x) [1,2,1];  out = sat(|Gx|+|Gy|)
+// Both kernels are rank one: the GPU runs it as a separable pair (vertical
+// smoothing + difference rows, then horizontal difference + smoothing).
 struct Sobel {
   static constexpr bool BINOM = false;
   static constexpr int K = 3, R = 1, DIV = 1;
-  static constexpr bool SEP = false, SOBEL = true;
+  static constexpr bool SEP = true, SOBEL = true;
+  STRIPE_HD static constexpr int g(int i) { return i == 1 ? 2 : 1; }
   STRIPE_HD static constexpr int wx(int dy, int dx) {
     constexpr int s[3] = {1, 2, 1}, d[3] = {-1, 0, 1};
     return s[dy] * d[dx];
