@@ -133,6 +133,9 @@ def main():
     ms = max_over_ranks((t1 - t0) * 1e3)
     ms_per_step = ms / a.steps
     mpx = W * H / (ms_per_step * 1e-3) / 1e6
+    # device-event stage times of the last call on rank 0 (compute = the whole
+    # timed run(K) call, halo = its last exchange)
+    stages = {"resident": {k: round(v, 4) for k, v in dp.stage_times().items() if k in ("compute", "halo")}}
 
     # ---- dist scope (root -> scatter -> filter -> gather -> root) ----
     dist_mpx = None
@@ -158,6 +161,8 @@ def main():
         t1 = time.perf_counter()
         dms = max_over_ranks((t1 - t0) * 1e3) / a.dist_steps
         dist_mpx = W * H / (dms * 1e-3) / 1e6
+        stages["dist"] = {k: round(v, 4) for k, v in dp.stage_times().items()
+                          if k in ("scatter", "compute", "halo", "gather")}
 
     # ---- e2e scope (pinned host stripe -> H2D -> filter -> D2H -> pinned host) ----
     e2e_mpx = None
@@ -177,6 +182,8 @@ def main():
         t1 = time.perf_counter()
         ems = max_over_ranks((t1 - t0) * 1e3) / a.e2e_steps
         e2e_mpx = W * H / (ems * 1e-3) / 1e6
+        stages["e2e"] = {k: round(v, 4) for k, v in dp.stage_times().items()
+                         if k in ("h2d", "compute", "halo", "d2h", "e2e")}
 
     if rank == 0:
         rec = {
@@ -205,6 +212,7 @@ def main():
             "e2e_scope_mpx_s": None if e2e_mpx is None else round(e2e_mpx, 1),
             "verified_vs_golden": verify,
             "tuned_band_rows": dp.engine.bands,
+            "stage_ms_rank0": stages,
         }
         print(json.dumps(rec), flush=True)
     if world > 1:

@@ -138,7 +138,37 @@ __global__ __launch_bounds__(kNT) void k_synth(uint8_t* origin, int64_t pitch, i
   }
 }
 
+// Row copy between pitched buffers (packed staging <-> padded stripe), 16 bytes
+// per lane; ALIGNED: both row starts and E are 16-byte multiples.
+template <bool ALIGNED>
+__global__ __launch_bounds__(kNT) void k_copy_rows(uint8_t* dst, int64_t dpitch, const uint8_t* src, int64_t spitch,
+                                                   int64_t E) {
+  const int64_t y = blockIdx.y;
+  uint8_t* d = dst + y * dpitch;
+  const uint8_t* sr = src + y * spitch;
+  for (int64_t b = ((int64_t)blockIdx.x * kNT + threadIdx.x) * 16; b < E; b += (int64_t)gridDim.x * kNT * 16) {
+    if constexpr (ALIGNED) {
+      *reinterpret_cast<uint4*>(d + b) = *reinterpret_cast<const uint4*>(sr + b);
+    } else {
+      const int64_t n = E - b < 16 ? E - b : 16;
+      for (int64_t e = 0; e < n; ++e) d[b + e] = sr[b + e];
+    }
+  }
+}
+
 }  // namespace dev
+
+void launch_copy_rows(uint8_t* dst, int64_t dpitch, const uint8_t* src, int64_t spitch, int64_t E, int rows,
+                      hipStream_t s) {
+  if (rows <= 0 || E <= 0) return;
+  const bool aligned = ((uintptr_t)dst % 16 == 0) && ((uintptr_t)src % 16 == 0) && dpitch % 16 == 0 &&
+                       spitch % 16 == 0 && E % 16 == 0;
+  const unsigned gx = (unsigned)std::min<int64_t>(div_up(E, 16 * dev::kNT), 64);
+  (void)hipGetLastError();
+  if (aligned) dev::k_copy_rows<true><<<dim3(gx, (unsigned)rows), dev::kNT, 0, s>>>(dst, dpitch, src, spitch, E);
+  else dev::k_copy_rows<false><<<dim3(gx, (unsigned)rows), dev::kNT, 0, s>>>(dst, dpitch, src, spitch, E);
+  HIP_CHECK(hipGetLastError());
+}
 
 void launch_pointwise(const Pass& p, const PassConsts& pc, const PassLaunch& L, hipStream_t s) {
   dev::KArgs a{};

@@ -39,6 +39,11 @@ class Comm {
   virtual void group_end() = 0;
   virtual void barrier() = 0;  // host-blocking, all ranks
   virtual void abort(const std::string& why) = 0;
+  // Block until the work queued on `s` (including this rank's collectives) is
+  // done.  Backends with asynchronous failure modes bound the wait
+  // (comm_timeout_s(), STRIPE_COMM_TIMEOUT_S) and abort the group on timeout
+  // or on an asynchronous communicator error instead of hanging (Q9).
+  virtual void wait(hipStream_t s);
 };
 
 // ---- RCCL ----

@@ -80,9 +80,16 @@ class Buffer {
   bool dev_ = false;
 };
 
-struct PhaseTimes {  // milliseconds of the last call of each phase (device events)
-  double run = 0, scatter = 0, gather = 0, load = 0, store = 0;
+// Milliseconds of the last call of each stage, from device events on the
+// stream the stage ran on (SURVEY §5 "hipEvents per stage"): run = the whole
+// chain of the last run() (all iterations), halo = the last halo exchange
+// (comm stream), h2d / d2h = the upload / download of the last run_e2e().
+struct PhaseTimes {
+  double run = 0, scatter = 0, gather = 0, load = 0, store = 0, halo = 0, h2d = 0, d2h = 0, e2e = 0;
 };
+
+enum class Stage : int { Load = 0, Scatter, Halo, Compute, Gather, Store, H2D, D2H, E2E, kCount };
+const char* stage_name(Stage s);
 
 class Engine {
  public:
@@ -159,6 +166,10 @@ class Engine {
               hipStream_t s, int kind);
   void fill_margins(uint8_t* org, int C, int y0, int y1, int px, Border b, hipStream_t s);
   void record(hipEvent_t e, hipStream_t s);
+  void stage_begin(Stage st, hipStream_t s);
+  void stage_end(Stage st, hipStream_t s);
+  void collect_times();
+  void wait_stream(hipStream_t s);
   float elapsed(hipEvent_t a, hipEvent_t b);
   RowGeom geom() const;
 
@@ -179,10 +190,13 @@ class Engine {
   hipStream_t s_h2d_ = nullptr, s_d2h_ = nullptr;
   std::vector<hipEvent_t> ev_h2d_, ev_cmp_;
   PinnedBuffer host_in_, host_out_;
+  Buffer stage_in_, stage_out_;  // packed device staging rows of the e2e path
   PassLaunch make_launch(const Pass& p, const uint8_t* in, uint8_t* out, int pi) const;
   bool own_streams_ = false;   // s_comm_ (and the e2e streams) are ours
   bool own_compute_ = false;   // s_compute_ is ours (false after use_external_stream)
   hipEvent_t ev_[8] = {};
+  hipEvent_t sev_[(int)Stage::kCount][2] = {};  // stage timing events
+  bool sev_used_[(int)Stage::kCount] = {};
   PhaseTimes times_;
   int out_buf_ = -1;        // buffer holding the last run's output
   int run_in_buf_ = 0;      // buffer holding the last run's input

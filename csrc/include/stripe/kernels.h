@@ -59,6 +59,11 @@ void launch_conv(const Pass& p, const PassConsts& pc, const PassLaunch& L, hipSt
 void launch_fill_margins(uint8_t* origin, int64_t pitch, int W, int C, int y0, int y1, int px,
                          Border b, hipStream_t s);
 
+// Copy `rows` rows of E bytes between pitched device buffers (packed staging
+// buffers <-> padded stripes; the e2e path's SDMA-friendly 1-D transfers).
+void launch_copy_rows(uint8_t* dst, int64_t dpitch, const uint8_t* src, int64_t spitch, int64_t E, int rows,
+                      hipStream_t s);
+
 // Synthetic pixels for local rows [0, rows) (global row0..), margins included.
 void launch_synth(uint8_t* origin, int64_t pitch, int W, int C, int row0, int rows, uint64_t seed,
                   int margin_px, Border b, hipStream_t s);

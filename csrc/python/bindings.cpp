@@ -13,6 +13,7 @@
 #include "stripe/chain.h"
 #include "stripe/comm.h"
 #include "stripe/engine.h"
+#include "stripe/trace.h"
 #include "stripe/golden.h"
 #include "stripe/image.h"
 #include "stripe/partition.h"
@@ -240,7 +241,30 @@ PYBIND11_MODULE(_C, m) {
   py::class_<PhaseTimes>(m, "PhaseTimes")
       .def_readonly("run", &PhaseTimes::run)
       .def_readonly("scatter", &PhaseTimes::scatter)
-      .def_readonly("gather", &PhaseTimes::gather);
+      .def_readonly("gather", &PhaseTimes::gather)
+      .def_readonly("load", &PhaseTimes::load)
+      .def_readonly("store", &PhaseTimes::store)
+      .def_readonly("halo", &PhaseTimes::halo)
+      .def_readonly("h2d", &PhaseTimes::h2d)
+      .def_readonly("d2h", &PhaseTimes::d2h)
+      .def_readonly("e2e", &PhaseTimes::e2e)
+      .def("as_dict", [](const PhaseTimes& t) {
+        py::dict d;
+        d["compute"] = t.run;
+        d["scatter"] = t.scatter;
+        d["gather"] = t.gather;
+        d["load"] = t.load;
+        d["store"] = t.store;
+        d["halo"] = t.halo;
+        d["h2d"] = t.h2d;
+        d["d2h"] = t.d2h;
+        d["e2e"] = t.e2e;
+        return d;
+      });
+  m.def("fault_point", &fault_point, py::arg("stage"), py::arg("rank"),
+        "Raise if STRIPE_FAULT selects this stage/rank (failure-path tests).");
+  m.def("comm_timeout_s", &comm_timeout_s);
+  m.def("trace_mark", [](const std::string& s) { trace_mark(s.c_str()); });
 
   py::class_<Engine>(m, "Engine", py::dynamic_attr())
       .def(py::init([](const EngineConfig& cfg, PyComm* comm) {

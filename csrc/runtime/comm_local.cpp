@@ -14,6 +14,10 @@
 
 namespace stripe {
 
+void Comm::wait(hipStream_t s) {
+  if (device_buffers() && s) HIP_CHECK(hipStreamSynchronize(s));
+}
+
 struct Msg {
   const void* ptr = nullptr;
   size_t bytes = 0;

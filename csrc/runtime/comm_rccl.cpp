@@ -2,10 +2,13 @@
 // kernel.cu:137,223 and provides the halo exchange the reference lacks, Q6).
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstring>
+#include <thread>
 
 #include "stripe/comm.h"
 #include "stripe/kernels.h"
+#include "stripe/trace.h"
 
 namespace stripe {
 
@@ -43,17 +46,53 @@ class RcclComm final : public Comm {
   bool device_buffers() const override { return true; }
   void group_start() override { NCCL_CHECK(ncclGroupStart()); }
   void send(const void* buf, size_t bytes, int peer, hipStream_t s) override {
+    STRIPE_CHECK(comm_ != nullptr, "RCCL communicator was aborted");
     NCCL_CHECK(ncclSend(buf, bytes, ncclUint8, peer, comm_, s));
   }
   void recv(void* buf, size_t bytes, int peer, hipStream_t s) override {
+    STRIPE_CHECK(comm_ != nullptr, "RCCL communicator was aborted");
     NCCL_CHECK(ncclRecv(buf, bytes, ncclUint8, peer, comm_, s));
   }
   void group_end() override { NCCL_CHECK(ncclGroupEnd()); }
   void barrier() override {
+    STRIPE_CHECK(comm_ != nullptr, "RCCL communicator was aborted");
     NCCL_CHECK(ncclAllReduce(bar_buf_, bar_buf_, 1, ncclInt32, ncclSum, comm_, bar_stream_));
-    HIP_CHECK(hipStreamSynchronize(bar_stream_));
+    wait(bar_stream_);
   }
   void abort(const std::string&) override { aborted_ = true; }
+
+  // Bounded wait: poll the stream and the communicator's asynchronous error
+  // state; a peer that died or a transport error aborts the communicator and
+  // raises instead of blocking forever in hipStreamSynchronize.
+  void wait(hipStream_t s) override {
+    if (!s) return;
+    const auto t0 = std::chrono::steady_clock::now();
+    const double limit = comm_timeout_s();
+    for (int it = 0;; ++it) {
+      const hipError_t e = hipStreamQuery(s);
+      if (e == hipSuccess) return;
+      if (e != hipErrorNotReady) HIP_CHECK(e);
+      (void)hipGetLastError();  // NotReady is not an error; keep the sticky state clean
+      if (comm_) {
+        ncclResult_t ar = ncclSuccess;
+        ncclCommGetAsyncError(comm_, &ar);
+        if (ar != ncclSuccess && ar != ncclInProgress) {
+          ncclCommAbort(comm_);
+          comm_ = nullptr;
+          fail(std::string("RCCL asynchronous error on rank ") + std::to_string(rank_) + ": " +
+               ncclGetErrorString(ar) + " (communicator aborted)");
+        }
+      }
+      const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (el > limit) {
+        if (comm_) ncclCommAbort(comm_);
+        comm_ = nullptr;
+        fail("rank " + std::to_string(rank_) + ": collective did not complete within " + std::to_string(limit) +
+             " s (STRIPE_COMM_TIMEOUT_S); communicator aborted");
+      }
+      if (it > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+  }
 
  private:
   ncclComm_t comm_ = nullptr;

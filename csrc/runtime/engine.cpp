@@ -1,6 +1,10 @@
 // Per-rank stripe engine (see engine.h).
 #include "stripe/engine.h"
 
+#include "stripe/trace.h"
+
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <mutex>
@@ -87,6 +91,8 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
     own_streams_ = true;
     own_compute_ = true;
     for (auto& e : ev_) HIP_CHECK(hipEventCreate(&e));
+    for (auto& pr : sev_)
+      for (auto& e : pr) HIP_CHECK(hipEventCreate(&e));
   }
   // one extra all-zero row at the end of each stripe buffer: the Constant
   // y-border row the buffer-descriptor kernels read (never written)
@@ -126,6 +132,9 @@ Engine::~Engine() {
       if (p.pc.conv) (void)hipFree(p.pc.conv);
     for (auto& e : ev_)
       if (e) (void)hipEventDestroy(e);
+    for (auto& pr : sev_)
+      for (auto& e : pr)
+        if (e) (void)hipEventDestroy(e);
     for (auto& e : ev_h2d_) (void)hipEventDestroy(e);
     for (auto& e : ev_cmp_) (void)hipEventDestroy(e);
     if (s_h2d_) (void)hipStreamDestroy(s_h2d_);
@@ -171,6 +180,59 @@ void Engine::record(hipEvent_t e, hipStream_t s) {
   if (device()) HIP_CHECK(hipEventRecord(e, s));
 }
 
+const char* stage_name(Stage s) {
+  static const char* names[] = {"load", "scatter", "halo", "compute", "gather", "store", "h2d", "d2h", "e2e"};
+  return names[(int)s];
+}
+
+namespace {
+double host_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+double& phase_field(PhaseTimes& t, Stage s) {
+  switch (s) {
+    case Stage::Load: return t.load;
+    case Stage::Scatter: return t.scatter;
+    case Stage::Halo: return t.halo;
+    case Stage::Compute: return t.run;
+    case Stage::Gather: return t.gather;
+    case Stage::Store: return t.store;
+    case Stage::H2D: return t.h2d;
+    case Stage::D2H: return t.d2h;
+    default: return t.e2e;
+  }
+}
+thread_local double host_stage_t0[(int)Stage::kCount];
+}  // namespace
+
+// Device backend: events on the stage's stream, read after synchronize();
+// host backend: the stage ran synchronously, so the host clock is exact.
+void Engine::stage_begin(Stage st, hipStream_t s) {
+  if (device()) HIP_CHECK(hipEventRecord(sev_[(int)st][0], s));
+  else host_stage_t0[(int)st] = host_ms();
+}
+
+void Engine::stage_end(Stage st, hipStream_t s) {
+  if (device()) {
+    HIP_CHECK(hipEventRecord(sev_[(int)st][1], s));
+    sev_used_[(int)st] = true;
+  } else {
+    phase_field(times_, st) = host_ms() - host_stage_t0[(int)st];
+  }
+}
+
+void Engine::collect_times() {
+  if (!device()) return;
+  for (int i = 0; i < (int)Stage::kCount; ++i)
+    if (sev_used_[i]) phase_field(times_, (Stage)i) = elapsed(sev_[i][0], sev_[i][1]);
+}
+
+void Engine::wait_stream(hipStream_t s) {
+  if (!s) return;
+  if (comm_) comm_->wait(s);
+  else HIP_CHECK(hipStreamSynchronize(s));
+}
+
 float Engine::elapsed(hipEvent_t a, hipEvent_t b) {
   float ms = 0;
   if (hipEventElapsedTime(&ms, a, b) != hipSuccess) {
@@ -199,9 +261,12 @@ void Engine::fill_margins(uint8_t* org, int C, int y0, int y1, int px, Border b,
 }
 
 void Engine::load_synthetic(uint64_t seed) {
+  TraceRange tr("stripe.load");
+  fault_point("load", rank_);
   const Stripe& st = stripe();
   const int C = plan_.cin;
   uint8_t* org = origin(buf_[0], C);
+  stage_begin(Stage::Load, s_compute_);
   if (device()) {
     launch_synth(org, pitch(C), cfg_.W, C, st.row0, st.rows, seed, plan_.in_margin_px, plan_.in_margin_border,
                  s_compute_);
@@ -210,6 +275,7 @@ void Engine::load_synthetic(uint64_t seed) {
     synth_rows(seed, cfg_.W, C, st.row0, st.rows, tmp.data());
     copy2d(org, pitch(C), tmp.data(), (int64_t)cfg_.W * C, (int64_t)cfg_.W * C, st.rows, nullptr, 0);
   }
+  stage_end(Stage::Load, s_compute_);
   cur_ = 0;
   cur_c_ = C;
 }
@@ -220,10 +286,12 @@ void Engine::load_packed(const void* src, bool src_device) {
   const int C = plan_.cin;
   const int64_t E = (int64_t)cfg_.W * C;
   uint8_t* org = origin(buf_[0], C);
-  record(ev_[6], s_compute_);
+  TraceRange tr("stripe.load");
+  fault_point("load", rank_);
+  stage_begin(Stage::Load, s_compute_);
   copy2d(org, pitch(C), src, E, E, st.rows, s_compute_, 0);
   fill_margins(org, C, 0, st.rows, plan_.in_margin_px, plan_.in_margin_border, s_compute_);
-  record(ev_[7], s_compute_);
+  stage_end(Stage::Load, s_compute_);
   cur_ = 0;
   cur_c_ = C;
 }
@@ -258,7 +326,9 @@ void Engine::scatter() {
   const int C = plan_.cin;
   const int64_t P = pitch(C);
   const Stripe& st = stripe();
-  record(ev_[2], s_compute_);
+  TraceRange tr("stripe.scatter");
+  fault_point("scatter", rank_);
+  stage_begin(Stage::Scatter, s_compute_);
   if (rank_ == 0) {
     STRIPE_CHECK(root_in_.data() != nullptr, "root buffers not allocated (EngineConfig::root_buffers)");
     const uint8_t* src = root_origin(root_in_, C) - kMarginBytes;
@@ -281,7 +351,7 @@ void Engine::scatter() {
     comm_->recv(origin(buf_[0], C) - kMarginBytes, (size_t)(st.rows * P), 0, s_compute_);
     comm_->group_end();
   }
-  record(ev_[3], s_compute_);
+  stage_end(Stage::Scatter, s_compute_);
   cur_ = 0;
   cur_c_ = C;
 }
@@ -294,6 +364,9 @@ void Engine::exchange_halo(uint8_t* org, int C, int R, hipStream_t s) {
   uint8_t* base = org - kMarginBytes;
   const int up = rank_ > 0 ? rank_ - 1 : -1;
   const int down = rank_ + 1 < part_.active ? rank_ + 1 : -1;
+  TraceRange tr("stripe.halo");
+  fault_point("halo", rank_);
+  stage_begin(Stage::Halo, s);
   comm_->group_start();
   if (up >= 0) {
     comm_->send(base, bytes, up, s);
@@ -304,6 +377,7 @@ void Engine::exchange_halo(uint8_t* org, int C, int R, hipStream_t s) {
     comm_->recv(base + (int64_t)st.rows * P, bytes, down, s);
   }
   comm_->group_end();
+  stage_end(Stage::Halo, s);
 }
 
 PassLaunch Engine::make_launch(const Pass& p, const uint8_t* in, uint8_t* out, int pi) const {
@@ -428,7 +502,9 @@ void Engine::run(int iterations) {
   if (cfg_.autotune && !tuned_) autotune_bands();
   STRIPE_CHECK(iterations == 1 || plan_.cout == plan_.cin,
                "iterating a chain needs equal input/output channels (" << plan_.cin << "->" << plan_.cout << ")");
-  record(ev_[0], s_compute_);
+  TraceRange tr("stripe.compute");
+  fault_point("compute", rank_);
+  stage_begin(Stage::Compute, s_compute_);
   run_in_buf_ = cur_;
   for (int it = 0; it < iterations; ++it) {
     STRIPE_CHECK(cur_c_ == plan_.cin, "engine input has " << cur_c_ << " channels, chain expects " << plan_.cin);
@@ -438,7 +514,7 @@ void Engine::run(int iterations) {
     }
     cur_c_ = plan_.cout;
   }
-  record(ev_[1], s_compute_);
+  stage_end(Stage::Compute, s_compute_);
   out_buf_ = cur_;
   out_c_ = plan_.cout;
 }
@@ -452,7 +528,32 @@ void Engine::alloc_host_io() {
   const Stripe& st = stripe();
   host_in_ = PinnedBuffer(std::max<size_t>(1, (size_t)st.rows * cfg_.W * plan_.cin));
   host_out_ = PinnedBuffer(std::max<size_t>(1, (size_t)st.rows * cfg_.W * plan_.cout));
+  if (device()) {
+    stage_in_ = Buffer(std::max<size_t>(16, (size_t)st.rows * cfg_.W * plan_.cin), true);
+    stage_out_ = Buffer(std::max<size_t>(16, (size_t)st.rows * cfg_.W * plan_.cout), true);
+  }
 }
+
+namespace {
+// e2e transfer mode (STRIPE_E2E_MODE):
+//   zerocopy - the repack kernels read / write the pinned host rows directly
+//              over PCIe (no copy engine; uploads and downloads are ordinary
+//              kernels on two streams, so both directions can be in flight);
+//   staged   - 1-D pinned <-> packed device staging copies on the copy engines
+//              plus an on-device repack into the padded stripe;
+//   2d       - one pitched 2-D host copy per chunk (default).
+// Measured on one MI355X box (16K RGB, gaussian5): all three move 805 MB each
+// way in ~14.5 ms per direction (~55 GB/s) and the two directions do not
+// overlap on that host, so e2e is host-link bound (~29 ms/frame) in every mode;
+// 2d is the simplest and marginally fastest.
+enum class E2EMode { ZeroCopy, Staged, TwoD };
+E2EMode e2e_mode() {
+  const char* e = std::getenv("STRIPE_E2E_MODE");
+  if (e && std::strcmp(e, "staged") == 0) return E2EMode::Staged;
+  if (e && std::strcmp(e, "zerocopy") == 0) return E2EMode::ZeroCopy;
+  return E2EMode::TwoD;
+}
+}  // namespace
 
 void Engine::run_e2e(int chunks) {
   STRIPE_CHECK(device(), "run_e2e needs the device backend");
@@ -460,6 +561,9 @@ void Engine::run_e2e(int chunks) {
   const Stripe& st = stripe();
   const int rows = st.rows;
   if (rows == 0) return;
+  TraceRange tr("stripe.e2e");
+  fault_point("e2e", rank_);
+  const E2EMode mode = e2e_mode();
   if (!s_h2d_) {
     HIP_CHECK(hipStreamCreateWithFlags(&s_h2d_, hipStreamNonBlocking));
     HIP_CHECK(hipStreamCreateWithFlags(&s_d2h_, hipStreamNonBlocking));
@@ -484,12 +588,48 @@ void Engine::run_e2e(int chunks) {
   cur_ = 0;
   cur_c_ = cin;
   uint8_t* in_org = origin(buf_[0], cin);
+  uint8_t* hin_dev = nullptr;
+  uint8_t* hout_dev = nullptr;
+  if (mode == E2EMode::ZeroCopy) {
+    HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&hin_dev), host_in_.data(), 0));
+    HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&hout_dev), host_out_.data(), 0));
+  }
+  auto download = [&](const uint8_t* org, int r0, int r1) {
+    if (r1 <= r0) return;
+    const int n = r1 - r0;
+    if (mode == E2EMode::ZeroCopy) {
+      launch_copy_rows(hout_dev + (int64_t)r0 * Eout, Eout, org + (int64_t)r0 * pitch(cout), pitch(cout), Eout, n,
+                       s_d2h_);
+    } else if (mode == E2EMode::Staged) {
+      launch_copy_rows(stage_out_.data() + (int64_t)r0 * Eout, Eout, org + (int64_t)r0 * pitch(cout), pitch(cout),
+                       Eout, n, s_d2h_);
+      HIP_CHECK(hipMemcpyAsync(host_out_.data() + (int64_t)r0 * Eout, stage_out_.data() + (int64_t)r0 * Eout,
+                               (size_t)n * Eout, hipMemcpyDeviceToHost, s_d2h_));
+    } else {
+      copy2d(host_out_.data() + (int64_t)r0 * Eout, Eout, org + (int64_t)r0 * pitch(cout), pitch(cout), Eout, n,
+             s_d2h_, 0);
+    }
+  };
+  stage_begin(Stage::E2E, s_h2d_);
+  stage_begin(Stage::H2D, s_h2d_);
   for (int i = 0; i < chunks; ++i) {
-    copy2d(in_org + (int64_t)cut[i] * pitch(cin), pitch(cin), host_in_.data() + (int64_t)cut[i] * Ein, Ein, Ein,
-           cut[i + 1] - cut[i], s_h2d_, 0);
+    const int n = cut[i + 1] - cut[i];
+    if (mode == E2EMode::ZeroCopy) {
+      launch_copy_rows(in_org + (int64_t)cut[i] * pitch(cin), pitch(cin), hin_dev + (int64_t)cut[i] * Ein, Ein, Ein,
+                       n, s_h2d_);
+    } else if (mode == E2EMode::Staged) {
+      HIP_CHECK(hipMemcpyAsync(stage_in_.data() + (int64_t)cut[i] * Ein, host_in_.data() + (int64_t)cut[i] * Ein,
+                               (size_t)n * Ein, hipMemcpyHostToDevice, s_h2d_));
+      launch_copy_rows(in_org + (int64_t)cut[i] * pitch(cin), pitch(cin), stage_in_.data() + (int64_t)cut[i] * Ein,
+                       Ein, Ein, n, s_h2d_);
+    } else {
+      copy2d(in_org + (int64_t)cut[i] * pitch(cin), pitch(cin), host_in_.data() + (int64_t)cut[i] * Ein, Ein, Ein, n,
+             s_h2d_, 0);
+    }
     fill_margins(in_org, cin, cut[i], cut[i + 1], plan_.in_margin_px, plan_.in_margin_border, s_h2d_);
     HIP_CHECK(hipEventRecord(ev_h2d_[i], s_h2d_));
   }
+  stage_end(Stage::H2D, s_h2d_);
   const bool single = plan_.passes.size() == 1;
   if (!single) {
     // multi-pass chains: upload overlapped with nothing but the download of the
@@ -498,7 +638,10 @@ void Engine::run_e2e(int chunks) {
     run(1);
     HIP_CHECK(hipEventRecord(ev_cmp_[0], s_compute_));
     HIP_CHECK(hipStreamWaitEvent(s_d2h_, ev_cmp_[0], 0));
-    copy2d(host_out_.data(), Eout, origin(buf_[out_buf_], cout), pitch(cout), Eout, rows, s_d2h_, 0);
+    stage_begin(Stage::D2H, s_d2h_);
+    download(origin(buf_[out_buf_], cout), 0, rows);
+    stage_end(Stage::D2H, s_d2h_);
+    stage_end(Stage::E2E, s_d2h_);
     return;
   }
   const Pass& p = plan_.passes[0];
@@ -520,6 +663,7 @@ void Engine::run_e2e(int chunks) {
   std::vector<std::pair<int, int>> ranges(chunks, {0, 0});
   for (int i = 0; i < chunks; ++i) {
     HIP_CHECK(hipStreamWaitEvent(s_compute_, ev_h2d_[i], 0));
+    if (i == 0) stage_begin(Stage::Compute, s_compute_);
     const int avail = i == chunks - 1 ? rows : std::max(0, cut[i + 1] - R);  // inputs loaded for y + R
     const int hi = std::min(avail, hi_lim);
     if (hi > done) {
@@ -532,9 +676,8 @@ void Engine::run_e2e(int chunks) {
     }
     HIP_CHECK(hipEventRecord(ev_cmp_[i], s_compute_));
     HIP_CHECK(hipStreamWaitEvent(s_d2h_, ev_cmp_[i], 0));
-    if (ranges[i].second > ranges[i].first)
-      copy2d(host_out_.data() + (int64_t)ranges[i].first * Eout, Eout, out_org + (int64_t)ranges[i].first * pitch(cout),
-             pitch(cout), Eout, ranges[i].second - ranges[i].first, s_d2h_, 0);
+    if (i == 0) stage_begin(Stage::D2H, s_d2h_);
+    download(out_org, ranges[i].first, ranges[i].second);
   }
   if (xchg) {  // boundary rows once the neighbours' halos are in
     HIP_CHECK(hipStreamWaitEvent(s_compute_, ev_[5], 0));
@@ -552,11 +695,12 @@ void Engine::run_e2e(int chunks) {
     if (L.nrange > 0) launch_pass(p, prt_[0].pc, L, s_compute_);
     HIP_CHECK(hipEventRecord(ev_cmp_[chunks], s_compute_));
     HIP_CHECK(hipStreamWaitEvent(s_d2h_, ev_cmp_[chunks], 0));
-    if (up) copy2d(host_out_.data(), Eout, out_org, pitch(cout), Eout, lo_lim, s_d2h_, 0);
-    if (down)
-      copy2d(host_out_.data() + (int64_t)hi_lim * Eout, Eout, out_org + (int64_t)hi_lim * pitch(cout), pitch(cout),
-             Eout, rows - hi_lim, s_d2h_, 0);
+    if (up) download(out_org, 0, lo_lim);
+    if (down) download(out_org, hi_lim, rows);
   }
+  stage_end(Stage::Compute, s_compute_);
+  stage_end(Stage::D2H, s_d2h_);
+  stage_end(Stage::E2E, s_d2h_);
   out_buf_ = 1;
   out_c_ = cout;
 }
@@ -566,7 +710,11 @@ void Engine::store_packed(void* dst, bool dst_device) {
   STRIPE_CHECK(out_buf_ >= 0, "store_packed before run");
   const int C = out_c_;
   const int64_t E = (int64_t)cfg_.W * C;
+  TraceRange tr("stripe.store");
+  fault_point("store", rank_);
+  stage_begin(Stage::Store, s_compute_);
   copy2d(dst, E, origin(buf_[out_buf_], C), pitch(C), E, stripe().rows, s_compute_, 0);
+  stage_end(Stage::Store, s_compute_);
 }
 
 void Engine::gather() {
@@ -574,7 +722,9 @@ void Engine::gather() {
   const int C = out_c_;
   const int64_t P = pitch(C);
   const Stripe& st = stripe();
-  record(ev_[2], s_compute_);
+  TraceRange tr("stripe.gather");
+  fault_point("gather", rank_);
+  stage_begin(Stage::Gather, s_compute_);
   const uint8_t* src = origin(buf_[out_buf_], C) - kMarginBytes;
   if (rank_ == 0) {
     STRIPE_CHECK(root_out_.data() != nullptr, "root buffers not allocated (EngineConfig::root_buffers)");
@@ -597,7 +747,7 @@ void Engine::gather() {
     comm_->send(src, (size_t)(st.rows * P), 0, s_compute_);
     comm_->group_end();
   }
-  record(ev_[3], s_compute_);
+  stage_end(Stage::Gather, s_compute_);
 }
 
 void Engine::store_root(void* full, bool dst_device) {
@@ -605,16 +755,20 @@ void Engine::store_root(void* full, bool dst_device) {
   if (rank_ != 0) return;
   const int C = out_c_ > 0 ? out_c_ : plan_.cout;
   const int64_t E = (int64_t)cfg_.W * C;
+  TraceRange tr("stripe.store");
+  stage_begin(Stage::Store, s_compute_);
   copy2d(full, E, root_origin(root_out_, C), pitch(C), E, cfg_.H, s_compute_, 0);
+  stage_end(Stage::Store, s_compute_);
 }
 
 void Engine::synchronize() {
   if (!device()) return;
-  HIP_CHECK(hipStreamSynchronize(s_compute_));
-  HIP_CHECK(hipStreamSynchronize(s_comm_));
-  if (s_h2d_) HIP_CHECK(hipStreamSynchronize(s_h2d_));
-  if (s_d2h_) HIP_CHECK(hipStreamSynchronize(s_d2h_));
-  times_.run = elapsed(ev_[0], ev_[1]);
+  TraceRange tr("stripe.synchronize");
+  wait_stream(s_compute_);
+  wait_stream(s_comm_);
+  wait_stream(s_h2d_);
+  wait_stream(s_d2h_);
+  collect_times();
 }
 
 // ---------------------------------------------------------------------------

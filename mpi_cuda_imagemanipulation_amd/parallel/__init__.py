@@ -15,6 +15,7 @@ the golden path and moves halos through gloo (callback communicator).
 from __future__ import annotations
 
 import ctypes
+import datetime
 import os
 from dataclasses import dataclass
 
@@ -96,7 +97,10 @@ def init(backend: str = "auto") -> DistContext:
     comm = None
     if world > 1:
         if not dist.is_initialized():
-            dist.init_process_group("nccl" if device else "gloo", rank=rank, world_size=world)
+            # the process-group timeout follows the native collective bound
+            # (STRIPE_COMM_TIMEOUT_S): a dead peer surfaces as an error, not a hang
+            dist.init_process_group("nccl" if device else "gloo", rank=rank, world_size=world,
+                                    timeout=datetime.timedelta(seconds=C.comm_timeout_s()))
         if device:
             uid = [C.rccl_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
@@ -121,6 +125,10 @@ class DistributedPipeline:
     @property
     def stripe(self):
         return self.engine.stripe
+
+    def stage_times(self) -> dict:
+        """Milliseconds of the last call of each stage (device events / host clock)."""
+        return self.engine.times.as_dict()
 
     def load_synthetic(self, seed: int):
         self.engine.load_synthetic(seed)

@@ -32,7 +32,8 @@ def test_epilogue_and_pointwise_passes(C):
     info = C.plan_info("invert,brightness:3", 3)
     assert len(info["passes"]) == 1 and info["passes"][0]["kind"] == 0
     info = C.plan_info("gaussian5,gray,sobel", 3)
-    assert [p["kind"] for p in info["passes"]] == [1, 2]
+    assert [p["kind"] for p in info["passes"]] == [1, 1]  # sobel runs as a separable pair
+    assert "separable sobel" in info["passes"][1]["desc"]
     assert info["passes"][0]["out_margin_px"] == 0 or info["passes"][0]["out_margin_px"] == 1
     info = C.plan_info("gaussian5,expand", 1)
     assert [p["kind"] for p in info["passes"]] == [1, 0]

@@ -42,6 +42,7 @@ CORE_SOURCES = [
     "runtime/comm_rccl.cpp",
     "runtime/comm_local.cpp",
     "runtime/engine.cpp",
+    "runtime/trace.cpp",
 ]
 BINDING_SOURCES = ["python/bindings.cpp"]
 CLI_SOURCES = ["cli/main.cpp"]
@@ -120,7 +121,7 @@ def link(objs: list[Path], out: Path, shared: bool, verbose: bool) -> None:
     if shared:
         cmd += ["-shared"]
     cmd += [str(o) for o in objs]
-    cmd += ["-L/opt/rocm/lib", "-lrccl", "-lamdhip64", "-lpthread", "-Wl,-rpath,/opt/rocm/lib", "-o", str(tmp)]
+    cmd += ["-L/opt/rocm/lib", "-lrccl", "-lamdhip64", "-lrocprofiler-sdk-roctx", "-lpthread", "-Wl,-rpath,/opt/rocm/lib", "-o", str(tmp)]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
