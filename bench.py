@@ -98,34 +98,53 @@ def main():
         dp.run(1)
         out = dp.result_stripe()
         ok = True
-        R = 2
-        crop = 48
+        info = C.plan_info(a.chain, Cc)
+        R = max(1, info["max_radius"])
+        crop = max(48, 4 * R)
+        # float conv passes (blur:K, conv:K) match the f64 golden within 1 LSB (ties)
+        tol = 1 if any(p["kind"] == 3 for p in info["passes"]) else 0
+
+        def same(x, y):
+            return bool((np.abs(x.astype(np.int16) - y.astype(np.int16)) <= tol).all())
         for lo in ([0] if row0 == 0 else []) + ([H - crop] if row0 + rows == H else []):
             # golden on a band of full rows; rows far enough from the band edge are exact
             band = C.synth_rows(a.seed, W, Cc, lo, crop)
             ref = C.golden_apply(band, a.chain, "reflect101", True)
             sel = slice(0, crop - R) if lo == 0 else slice(R, crop)
             got = out[lo - row0:lo - row0 + crop][sel]
-            ok &= bool((got == ref[sel]).all())
-        if rows > 0 and row0 > 0 and rows >= 8:
-            # interior stripe seam: compare the first 4 rows (they depend on the halo)
-            band = C.synth_rows(a.seed, W, Cc, row0 - 8, 16)
+            ok &= same(got, ref[sel])
+        if rows > 0 and row0 > 0 and rows >= 2 * R:
+            # interior stripe seam: the first R rows depend on the halo
+            band = C.synth_rows(a.seed, W, Cc, row0 - 2 * R, 4 * R)
             ref = C.golden_apply(band, a.chain, "reflect101", True)
-            ok &= bool((out[0:4] == ref[8:12]).all())
+            ok &= same(out[0:R], ref[2 * R:3 * R])
         okt = torch.tensor([1.0 if ok else 0.0], device=tdev)
         if world > 1:
             dist.all_reduce(okt, op=dist.ReduceOp.MIN)
         verify = bool(okt.item() == 1.0)
 
     # ---- resident scope (headline) ----
+    pinfo = C.plan_info(a.chain, Cc)
+    iterable = pinfo["cin"] == pinfo["cout"]
+
+    def run_steps(n):
+        # iterable chains ping-pong in one call; a chain that changes the channel
+        # count re-reads its (unchanged) input each step instead
+        if iterable:
+            dp.run(n)
+        else:
+            for _ in range(n):
+                dp.engine.rewind()
+                dp.run(1)
+
     dp.load_synthetic(a.seed)
     if a.warmup > 0:
-        dp.run(a.warmup)
+        run_steps(a.warmup)
     sync()
     barrier()
     sync()
     t0 = time.perf_counter()
-    dp.run(a.steps)
+    run_steps(a.steps)
     dp.synchronize()
     sync()
     barrier()

@@ -266,12 +266,14 @@ int cmd_bench(const Args& a) {
             e.load_synthetic(seed);
           }
           e.synchronize();
+          const bool iterable = e.plan().cin == e.plan().cout;
           auto step = [&]() {
             if (scope == "dist") {
               e.scatter();
               e.run(1);
               e.gather();
             } else {
+              if (!iterable) e.rewind();  // re-read the unchanged input (e.g. gray: 3 -> 1 channels)
               e.run(1);
             }
           };
