@@ -32,6 +32,7 @@
 #include "dev_common.h"
 #include "stripe/kernels.h"
 
+#include <cstdlib>
 #include <type_traits>
 #include <vector>
 
@@ -104,7 +105,7 @@ __global__ __launch_bounds__(kSepWaves * 64, 2) void k_blur_sep(SepArgs sa) {
   // task = (strip, band of a.band rows); consecutive waves take horizontally
   // adjacent strips (their 256-byte windows overlap by half; measured ~2 %
   // faster than strip-major order)
-  const int task = blockIdx.x * kSepWaves + wave;
+  const int task = xcd_remap((int)blockIdx.x, (int)gridDim.x, a.nxcd) * kSepWaves + wave;
   if (task >= sa.nstrips * a.nbands) return;  // wave-uniform
   uint8_t* wl = lds + wave * kSepTile;
   const int strip = task % sa.nstrips, by = task / sa.nstrips;
@@ -364,6 +365,11 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
     const int band = (int)(32 * gpb);
 
     a.band = band;
+    static const int nxcd = [] {
+      const char* e = std::getenv("STRIPE_XCD");
+      return e ? std::atoi(e) : 0;
+    }();
+    a.nxcd = nxcd;
     a.nb0 = (int)div_up(n0, band);
     a.nbands = a.nb0 + (int)div_up(n1, band);
     const dim3 grid((unsigned)div_up((int64_t)sa.nstrips * a.nbands, dev::kSepWaves));

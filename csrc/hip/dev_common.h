@@ -36,6 +36,7 @@ struct KArgs {
   uint32_t gmul[3];
   int gshift[3];
   int cin;        // pointwise: input channels
+  int nxcd;       // > 1: XCD-aware workgroup remap over this many L2 domains
   // buffer-descriptor view (stencil kernels): offsets of the origins in the
   // allocations; every hot-loop load/store is a raw buffer op whose range check
   // masks inactive lanes (no divergent branches around memory ops, so hipcc's
@@ -84,6 +85,18 @@ __device__ __forceinline__ uint32_t in_row_off(const KArgs& a, int y) {
     g = m;
   }
   return a.in_org + (uint32_t)((int64_t)(g - a.row0) * a.in_pitch);
+}
+
+// Bijective XCD-aware remap of the workgroup index: the hardware hands
+// consecutive workgroups to the XCDs round-robin (blockIdx % 8 shares an L2),
+// so logical workgroup ranges are made contiguous per XCD: vertically /
+// horizontally adjacent tiles (which share halo rows / window bytes) then meet
+// in one L2 (cdna_hip_programming.md T1).
+__device__ __forceinline__ int xcd_remap(int bid, int nwg, int nxcd) {
+  if (nxcd <= 1 || nwg < nxcd) return bid;
+  const int q = nwg / nxcd, r = nwg % nxcd;
+  const int x = bid % nxcd, slot = bid / nxcd;
+  return x * q + min(x, r) + slot;
 }
 
 // Row range of workgroup row `by`.

@@ -21,6 +21,8 @@
 //   * out-of-place and deterministic; the x-border comes from the buffer margins,
 //     the y-border from a scalar row remap; edge waves rewrite the output margins
 //     after their band (one vmcnt(0) per band).
+#include <cstdlib>
+
 #include "dev_common.h"
 #include "stripe/kernels.h"
 #include "stripe/stencil_defs.h"
@@ -55,7 +57,7 @@ __device__ __forceinline__ WaveTask wave_task(const KArgs& a) {
   WaveTask t;
   t.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   t.lane = threadIdx.x & 63;
-  const int w = (int)blockIdx.x * kWaves + t.wave;
+  const int w = xcd_remap((int)blockIdx.x, (int)gridDim.x, a.nxcd) * kWaves + t.wave;
   t.xt = w % a.ntx;
   const int bt = w / a.ntx;
   t.valid = bt < a.nbands;
@@ -79,27 +81,54 @@ __device__ __forceinline__ uint32_t as_u32(u16x2 x) { return __builtin_bit_cast(
 __device__ __forceinline__ i16x2 as_i16x2(uint32_t x) { return __builtin_bit_cast(i16x2, x); }
 __device__ __forceinline__ uint32_t as_u32(i16x2 x) { return __builtin_bit_cast(uint32_t, x); }
 
-// Load the lane's 16 output-channel bytes of the input row at `row_off`
-// (after the prologue).  `lane_off` carries kOOB for lanes that must not load.
+// The lane's raw input bytes of one row: 16 bytes, or 48 for a gray prologue
+// (16 RGB pixels).  Loads are issued by load_raw and the prologue (gray / LUT)
+// is applied by cook when the row is consumed, so prefetched rows stay in
+// flight instead of being waited for at the load (a LUT or gray conversion at
+// the load site forces an s_waitcnt there).
 template <int PRO>
-__device__ __forceinline__ void load_chunk(const KArgs& a, __amdgpu_buffer_rsrc_t rin, uint32_t row_off,
-                                           uint32_t lane_off, const uint8_t* lut_post, uint32_t (&o)[4]) {
+struct RawChunk {
+  uint32_t d[PRO == PRO_GRAY ? 12 : 4];
+};
+
+template <int PRO>
+__device__ __forceinline__ void load_raw(__amdgpu_buffer_rsrc_t rin, uint32_t row_off, uint32_t lane_off,
+                                         RawChunk<PRO>& r) {
   if constexpr (PRO == PRO_GRAY) {
     const uint32_t off = row_off + lane_off;  // lane_off already scaled by 3
     const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(rin, off, 0, 0);
     const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(rin, off + 16, 0, 0);
     const u32x4 v2 = __builtin_amdgcn_raw_buffer_load_b128(rin, off + 32, 0, 0);
-    const uint32_t rgb[12] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, v2.z, v2.w};
-    gray16(a, rgb, o);
-    if (a.has_post) lut16(lut_post, o);
+    r.d[0] = v0.x; r.d[1] = v0.y; r.d[2] = v0.z; r.d[3] = v0.w;
+    r.d[4] = v1.x; r.d[5] = v1.y; r.d[6] = v1.z; r.d[7] = v1.w;
+    r.d[8] = v2.x; r.d[9] = v2.y; r.d[10] = v2.z; r.d[11] = v2.w;
   } else {
     const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rin, row_off + lane_off, 0, 0);
-    o[0] = v.x;
-    o[1] = v.y;
-    o[2] = v.z;
-    o[3] = v.w;
+    r.d[0] = v.x; r.d[1] = v.y; r.d[2] = v.z; r.d[3] = v.w;
+  }
+}
+
+// Prologue: the 16 output-channel bytes of a raw chunk.
+template <int PRO>
+__device__ __forceinline__ void cook(const KArgs& a, const RawChunk<PRO>& r, const uint8_t* lut_post,
+                                     uint32_t (&o)[4]) {
+  if constexpr (PRO == PRO_GRAY) {
+    gray16(a, r.d, o);
+    if (a.has_post) lut16(lut_post, o);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = r.d[q];
     if constexpr (PRO == PRO_LUT) lut16(lut_post, o);
   }
+}
+
+// Load + prologue in one step (rows that are consumed right away).
+template <int PRO>
+__device__ __forceinline__ void load_chunk(const KArgs& a, __amdgpu_buffer_rsrc_t rin, uint32_t row_off,
+                                           uint32_t lane_off, const uint8_t* lut_post, uint32_t (&o)[4]) {
+  RawChunk<PRO> r;
+  load_raw<PRO>(rin, row_off, lane_off, r);
+  cook<PRO>(a, r, lut_post, o);
 }
 
 __device__ __forceinline__ void load_luts(const KArgs& a, uint8_t* lds) {
@@ -294,16 +323,18 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : 4)) void k_sep(KArgs a) {
   // kPF rows in flight per lane (memory-level parallelism is what this streaming
   // kernel is bound by); loads past the band re-read its last input row
   // (unconditional: no branch around the load)
-  constexpr int kPF = 4;
-  uint32_t nx[kPF][4];
+  // (a gray prologue reads 48 bytes per row: 2 rows give more bytes in flight
+  // than 4 plain rows, at 24 fewer registers)
+  constexpr int kPF = PRO == PRO_GRAY ? 2 : 4;
+  RawChunk<PRO> nx[kPF];
 #pragma unroll
-  for (int i = 0; i < kPF; ++i)
-    load_chunk<PRO>(a, rin, ys + i < ye ? in_row_off(a, ys + i + R) : last_row, lane_in, luts + 256, nx[i]);
+  for (int i = 0; i < kPF; ++i) load_raw<PRO>(rin, ys + i < ye ? in_row_off(a, ys + i + R) : last_row, lane_in, nx[i]);
 
-  auto row_step = [&](int y, const VState<F>& prev, VState<F>& next, uint32_t (&nb)[4], bool valid) {
-    uint32_t u[8], vv[8], dd[8];
-    unpack16(nb, u);
-    load_chunk<PRO>(a, rin, y + kPF < ye ? in_row_off(a, y + kPF + R) : last_row, lane_in, luts + 256, nb);
+  auto row_step = [&](int y, const VState<F>& prev, VState<F>& next, RawChunk<PRO>& nb, bool valid) {
+    uint32_t u[8], vv[8], dd[8], c[4];
+    cook<PRO>(a, nb, luts + 256, c);
+    unpack16(c, u);
+    load_raw<PRO>(rin, y + kPF < ye ? in_row_off(a, y + kPF + R) : last_row, lane_in, nb);
     if constexpr (F::SOBEL) {
       vpush_sobel<F>(u, prev, next, vv, dd);
       vb[2][lane] = make_uint4(dd[0], dd[1], dd[2], dd[3]);
@@ -445,15 +476,19 @@ __global__ __launch_bounds__(kNT, 4) void k_direct(KArgs a) {
     load_chunk<PRO>(a, rin, in_row_off(a, ys - R + i), lane_in, luts + 256, r);
     rg[i][lane] = make_uint4(r[0], r[1], r[2], r[3]);
   }
-  uint32_t nxt[4];
-  load_chunk<PRO>(a, rin, in_row_off(a, ys + R), lane_in, luts + 256, nxt);
+  RawChunk<PRO> nxt;
+  load_raw<PRO>(rin, in_row_off(a, ys + R), lane_in, nxt);
   const int rl = lane == 0 ? 1 : (lane == kW - 1 ? kW - 2 : lane);
   int s0 = 0;
   for (int y = ys; y < ye; ++y) {
     int sw = s0 + K - 1;
     if (sw >= S) sw -= S;
-    rg[sw][lane] = make_uint4(nxt[0], nxt[1], nxt[2], nxt[3]);
-    load_chunk<PRO>(a, rin, y + 1 < ye ? in_row_off(a, y + 1 + R) : last_row, lane_in, luts + 256, nxt);
+    {
+      uint32_t c[4];
+      cook<PRO>(a, nxt, luts + 256, c);
+      rg[sw][lane] = make_uint4(c[0], c[1], c[2], c[3]);
+    }
+    load_raw<PRO>(rin, y + 1 < ye ? in_row_off(a, y + 1 + R) : last_row, lane_in, nxt);
     wave_lds_sync();
     int acc[16], acc2[16];
 #pragma unroll
@@ -534,8 +569,17 @@ inline int resident_slots(const void* fn) {
 // 0.323 ms/pass at 12 rows vs 0.370 ms with one tall band per workgroup, which
 // spreads the concurrent streams over the whole frame); the engine's autotuner
 // can override per shape.
+inline int env_nxcd() {
+  static const int v = [] {
+    const char* e = std::getenv("STRIPE_XCD");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+
 inline void plan_bands(KArgs& a, dim3& grid, int tiles, int n0, int n1, int band, int R, int slots) {
   (void)slots;
+  a.nxcd = env_nxcd();
   if (band <= 0) band = R >= 3 ? 16 : 12;
   band = (int)align_up(band, 4);
   a.band = band;

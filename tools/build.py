@@ -9,6 +9,15 @@ travels with the repository snapshot to the GPU box:
 
 Objects are cached under build/obj and rebuilt when their source or any header
 under csrc/ is newer.  Usage: python tools/build.py [-j N] [--clean] [--verbose]
+
+Every HIP translation unit is compiled with -Rpass-analysis=kernel-resource-usage;
+the per-kernel report (VGPRs/AGPRs, spills, scratch, LDS, occupancy) is written
+to build/kernel_resources.json and checked by tests/test_kernel_resources.py
+(no kernel may spill or use scratch).
+
+--sanitize builds a host-side ASan+UBSan variant of the CLI (bin/stripe-asan,
+objects under build/obj-asan): the sanitizers instrument host code only
+(-Xarch_host), device code is unchanged.
 """
 from __future__ import annotations
 
@@ -24,6 +33,9 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
 CSRC = ROOT / "csrc"
 BUILD = ROOT / "build" / "obj"
+RESOURCES = ROOT / "build" / "kernel_resources.json"
+SAN_FLAGS = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+             "-Xarch_host", "-fno-omit-frame-pointer", "-Xarch_host", "-fno-sanitize-recover=undefined"]
 PKG = ROOT / "mpi_cuda_imagemanipulation_amd"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("STRIPE_ARCH", "gfx950")
@@ -89,18 +101,49 @@ def newest_header() -> float:
     return m
 
 
-def obj_for(src: str) -> Path:
-    return BUILD / (src.replace("/", "__") + ".o")
+def obj_for(src: str, objdir: Path = BUILD) -> Path:
+    return objdir / (src.replace("/", "__") + ".o")
 
 
-def compile_one(src: str, extra: list[str], hdr_mtime: float, verbose: bool) -> Path:
+def remarks_for(o: Path) -> Path:
+    return o.with_suffix(".resources.txt")
+
+
+def parse_resource_remarks(text: str) -> dict:
+    """kernel-resource-usage remarks -> {kernel: {field: value}}.
+
+    Lines look like '<file>:<l>:<c>: remark:     VGPRs: 44 [-Rpass-analysis=...]'."""
+    import re
+
+    out: dict = {}
+    cur = None
+    for line in text.splitlines():
+        if "remark:" not in line:
+            continue
+        body = re.sub(r"\s*\[-Rpass-analysis=[^\]]*\]\s*$", "", line.split("remark:", 1)[1])
+        m = re.match(r"\s*([^:]+?):\s*(.*)$", body)
+        if not m:
+            continue
+        key, val = m.group(1).strip(), m.group(2).strip()
+        if key == "Function Name":
+            cur = val
+            out[cur] = {}
+        elif cur is not None:
+            try:
+                out[cur][key] = int(val)
+            except ValueError:
+                out[cur][key] = val
+    return out
+
+
+def compile_one(src: str, extra: list[str], hdr_mtime: float, verbose: bool, objdir: Path = BUILD) -> Path:
     s = CSRC / src
-    o = obj_for(src)
+    o = obj_for(src, objdir)
     if o.exists() and o.stat().st_mtime >= max(s.stat().st_mtime, hdr_mtime):
         return o
     cmd = [HIPCC, *common_flags(), *extra]
     if src.endswith(".hip"):
-        cmd += ["-x", "hip"]
+        cmd += ["-x", "hip", "-Rpass-analysis=kernel-resource-usage"]
     cmd += ["-c", str(s), "-o", str(o)]
     if verbose:
         print(" ".join(cmd), flush=True)
@@ -108,16 +151,36 @@ def compile_one(src: str, extra: list[str], hdr_mtime: float, verbose: bool) -> 
     if r.returncode != 0:
         sys.stderr.write(r.stdout + r.stderr)
         raise SystemExit(f"compile failed: {src}")
-    if r.stderr.strip() and verbose:
+    if src.endswith(".hip"):
+        remarks_for(o).write_text(r.stderr)
+        noise = "\n".join(l for l in r.stderr.splitlines() if "remark:" not in l)
+        if noise.strip() and verbose:
+            sys.stderr.write(noise + "\n")
+    elif r.stderr.strip() and verbose:
         sys.stderr.write(r.stderr)
     print(f"  compiled {src}", flush=True)
     return o
 
 
-def link(objs: list[Path], out: Path, shared: bool, verbose: bool) -> None:
+def write_resource_report() -> dict:
+    import json
+
+    rep: dict = {}
+    for src in CORE_SOURCES:
+        if src.endswith(".hip"):
+            f = remarks_for(obj_for(src))
+            if f.exists():
+                for k, v in parse_resource_remarks(f.read_text()).items():
+                    v["source"] = src
+                    rep[k] = v
+    RESOURCES.write_text(json.dumps(rep, indent=1, sort_keys=True))
+    return rep
+
+
+def link(objs: list[Path], out: Path, shared: bool, verbose: bool, extra: list[str] | None = None) -> None:
     out.parent.mkdir(parents=True, exist_ok=True)
     tmp = out.with_name(out.name + ".tmp")
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-fPIC"]
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-fPIC", *(extra or [])]
     if shared:
         cmd += ["-shared"]
     cmd += [str(o) for o in objs]
@@ -153,6 +216,22 @@ def build(jobs: int | None = None, verbose: bool = False, clean: bool = False, c
         exe = cli_path()
         if not exe.exists() or any(o.stat().st_mtime > exe.stat().st_mtime for o in core + [objs[CLI_SOURCES[0]]]):
             link(core + [objs[s] for s in CLI_SOURCES], exe, shared=False, verbose=verbose)
+    write_resource_report()
+
+
+def build_sanitized(jobs: int | None = None, verbose: bool = False) -> Path:
+    """Host ASan+UBSan build of the CLI (device code unchanged)."""
+    objdir = ROOT / "build" / "obj-asan"
+    objdir.mkdir(parents=True, exist_ok=True)
+    hdr = newest_header()
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    srcs = CORE_SOURCES + CLI_SOURCES
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(lambda s: compile_one(s, ["-O1", *SAN_FLAGS], hdr, verbose, objdir), srcs))
+    exe = ROOT / "bin" / "stripe-asan"
+    if not exe.exists() or any(o.stat().st_mtime > exe.stat().st_mtime for o in objs):
+        link(objs, exe, shared=False, verbose=verbose, extra=["-fsanitize=address,undefined"])
+    return exe
 
 
 def main() -> None:
@@ -161,8 +240,11 @@ def main() -> None:
     ap.add_argument("--clean", action="store_true")
     ap.add_argument("--verbose", "-v", action="store_true")
     ap.add_argument("--no-cli", action="store_true")
+    ap.add_argument("--sanitize", action="store_true", help="also build bin/stripe-asan (host ASan+UBSan)")
     a = ap.parse_args()
     build(a.jobs, a.verbose, a.clean, cli=not a.no_cli)
+    if a.sanitize:
+        build_sanitized(a.jobs, a.verbose)
 
 
 if __name__ == "__main__":
