@@ -54,14 +54,20 @@ Image decode_pnm(const std::string& bytes) {
   const long maxval = rd.read_int("maxval");
   STRIPE_CHECK(W >= 1 && H >= 1, "PNM: bad size " << W << "x" << H);
   STRIPE_CHECK(maxval == 255, "PNM: only maxval 255 supported, got " << maxval);
-  Image img((int)W, (int)H, C);
-  const size_t n = img.bytes();
+  // validate the payload size against the header before allocating (a forged
+  // header must not request a huge allocation; found by the ASan CLI tests)
+  const size_t n = (size_t)W * (size_t)H * (size_t)C;
+  const size_t avail = bytes.size() > rd.i ? bytes.size() - rd.i : 0;
   if (kind == '5' || kind == '6') {
     // exactly one whitespace byte after maxval, then raw samples
     STRIPE_CHECK(rd.i < bytes.size() && isspace((unsigned char)bytes[rd.i]), "PNM: header not terminated");
+    STRIPE_CHECK(avail - 1 >= n, "PNM: truncated pixel data (" << avail - 1 << " of " << n << " bytes)");
+  } else {
+    STRIPE_CHECK(avail >= 2 * n - 1, "PNM: truncated ASCII pixel data (" << n << " samples declared)");
+  }
+  Image img((int)W, (int)H, C);
+  if (kind == '5' || kind == '6') {
     rd.i += 1;
-    STRIPE_CHECK(bytes.size() - rd.i >= n, "PNM: truncated pixel data (" << bytes.size() - rd.i << " of "
-                                                                         << n << " bytes)");
     std::copy(bytes.begin() + rd.i, bytes.begin() + rd.i + n, img.data.begin());
   } else {
     for (size_t k = 0; k < n; ++k) {
