@@ -7,6 +7,7 @@
 // or N logical ranks on fewer GPUs / on the CPU), all parameters are flags:
 //
 //   stripe run   --input in.ppm --output out.ppm --chain gray:ref,contrast:3.5,emboss3
+//                (multi-process: --backend rccl --world N --rank r --rendezvous FILE [--device d])
 //                [--preset ref-gpu|ref-cpu] [--ranks N] [--backend rccl|local|host]
 //                [--devices 0,1,..] [--border reflect101|replicate|constant|skip]
 //                [--no-halo] [--expand-gray] [--legacy-partition] [--iterations K]
@@ -29,7 +30,10 @@
 #include <mutex>
 #include <thread>
 
+#include <unistd.h>
+
 #include "stripe/engine.h"
+#include "stripe/trace.h"
 
 using namespace stripe;
 
@@ -159,7 +163,77 @@ Group make_group(const std::string& backend, int N, const std::vector<int>& devl
   return g;
 }
 
+// Multi-process rendezvous through a shared file: rank 0 writes the RCCL
+// unique id (write + atomic rename), the other ranks poll for it (bounded).
+UniqueId file_rendezvous(const std::string& path, int rank) {
+  UniqueId id{};
+  if (rank == 0) {
+    id = rccl_unique_id();
+    const std::string tmp = path + ".tmp" + std::to_string(::getpid());
+    {
+      std::ofstream f(tmp, std::ios::binary);
+      f.write(id.data(), (std::streamsize)id.size());
+      STRIPE_CHECK(f.good(), "cannot write rendezvous file '" << tmp << "'");
+    }
+    STRIPE_CHECK(std::rename(tmp.c_str(), path.c_str()) == 0, "rename to '" << path << "' failed");
+    return id;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    std::ifstream f(path, std::ios::binary);
+    if (f.good()) {
+      f.read(id.data(), (std::streamsize)id.size());
+      if (f.gcount() == (std::streamsize)id.size()) return id;
+    }
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    STRIPE_CHECK(el < comm_timeout_s(), "rank " << rank << ": no rendezvous file '" << path << "' after " << el
+                                                << " s (STRIPE_COMM_TIMEOUT_S)");
+    std::this_thread::sleep_for(std::chrono::milliseconds(20));
+  }
+}
+
+// One rank of a multi-process job: `stripe run --backend rccl --world N --rank r
+// --rendezvous FILE [--device d]` (like the reference's `mpiexec -n N`, one
+// process per rank; only rank 0 reads the input and writes the output).
+int cmd_run_rank(const Args& a) {
+  const int world = a.geti("world", 1), rank = a.geti("rank", 0);
+  STRIPE_CHECK(rank >= 0 && rank < world, "--rank must be in [0, --world)");
+  STRIPE_CHECK(a.has("rendezvous"), "multi-process runs need --rendezvous FILE (shared by all ranks)");
+  const int ndev = device_count();
+  const int device = a.geti("device", ndev > 0 ? rank % ndev : 0);
+  Image img;
+  EngineConfig cfg;
+  if (rank == 0) {
+    STRIPE_CHECK(a.has("input") && a.has("output"), "rank 0 needs --input and --output");
+    img = read_pnm(a.get("input"));
+    cfg = config_from(a, img.W, img.H, img.C);
+  } else {
+    cfg = config_from(a, 1, 1, 3);  // geometry arrives with the metadata broadcast
+  }
+  STRIPE_CHECK(cfg.backend == BackendKind::Device, "multi-process runs use the rccl backend");
+  const UniqueId id = file_rendezvous(a.get("rendezvous"), rank);
+  auto comm = make_rccl_comm(id, rank, world, device);
+  PhaseTimes t;
+  const auto t0 = std::chrono::steady_clock::now();
+  Image out;
+  try {
+    out = run_rank(cfg, comm.get(), device, rank == 0 ? &img : nullptr, a.geti("iterations", 1), &t);
+  } catch (...) {
+    comm->abort("rank failed");
+    throw;
+  }
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (rank == 0) {
+    write_pnm(a.get("output"), out);
+    std::printf("{\"cmd\":\"run\",\"W\":%d,\"H\":%d,\"C\":%d,\"ranks\":%d,\"backend\":\"rccl\",\"processes\":%d,"
+                "\"chain\":\"%s\",\"wall_ms\":%.3f,\"kernel_ms\":%.4f,\"scatter_ms\":%.4f,\"gather_ms\":%.4f}\n",
+                img.W, img.H, img.C, world, world, cfg.chain.c_str(), ms, t.run, t.scatter, t.gather);
+  }
+  return 0;
+}
+
 int cmd_run(const Args& a) {
+  if (a.has("world")) return cmd_run_rank(a);
   STRIPE_CHECK(a.has("input") && a.has("output"), "run needs --input and --output");
   Image img = read_pnm(a.get("input"));
   EngineConfig cfg = config_from(a, img.W, img.H, img.C);
@@ -177,8 +251,8 @@ int cmd_run(const Args& a) {
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   write_pnm(a.get("output"), out);
   std::printf("{\"cmd\":\"run\",\"W\":%d,\"H\":%d,\"C\":%d,\"ranks\":%d,\"backend\":\"%s\",\"chain\":\"%s\","
-              "\"wall_ms\":%.3f,\"kernel_ms\":%.4f}\n",
-              img.W, img.H, img.C, N, backend.c_str(), cfg.chain.c_str(), ms, t.run);
+              "\"wall_ms\":%.3f,\"kernel_ms\":%.4f,\"scatter_ms\":%.4f,\"gather_ms\":%.4f}\n",
+              img.W, img.H, img.C, N, backend.c_str(), cfg.chain.c_str(), ms, t.run, t.scatter, t.gather);
   return 0;
 }
 
@@ -323,6 +397,7 @@ void usage() {
                "  run   --input in.ppm --output out.ppm [--chain C | --preset ref-gpu|ref-cpu] [--ranks N]\n"
                "        [--backend rccl|local|host] [--devices 0,1,..] [--border MODE] [--no-halo]\n"
                "        [--expand-gray] [--legacy-partition] [--iterations K] [--no-fuse] [--no-overlap]\n"
+               "        one process per rank: --backend rccl --world N --rank r --rendezvous FILE [--device d]\n"
                "  bench --synthetic WxHxC [--seed S] [--chain C] [--ranks 1,2,4,8] [--iters N] [--warmup N]\n"
                "        [--scope resident,dist] [--backend rccl|local|host] [--json out.json]\n"
                "  cmp   a.ppm b.ppm [--tol T]\n"

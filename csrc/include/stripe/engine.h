@@ -203,6 +203,14 @@ class Engine {
   int out_c_ = 0;
 };
 
+// One rank's whole pipeline (one process or thread per rank): metadata
+// broadcast from rank 0, scatter, chain, gather; returns the image on rank 0.
+// `input` is read on rank 0 only; `device` is this rank's GPU (-1: keep).
+Image run_rank(const EngineConfig& cfg, Comm* comm, int device, const Image* input, int iterations,
+               PhaseTimes* times = nullptr);
+// Small host buffer broadcast over a communicator (metadata, <= 256 bytes).
+void broadcast_small(Comm* comm, void* host, size_t bytes, int root, int device);
+
 // Convenience driver: run the whole distributed pipeline on `world` in-process
 // ranks (local device backend or host backend), root -> scatter -> run -> gather.
 Image run_local_group(const EngineConfig& cfg, int world, const Image& input, int iterations,

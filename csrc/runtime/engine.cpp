@@ -774,6 +774,72 @@ void Engine::synchronize() {
 // ---------------------------------------------------------------------------
 // In-process group driver
 // ---------------------------------------------------------------------------
+// Broadcast `bytes` (<= 256) from `root` to every rank through the group's
+// point-to-point channel (device staging for device communicators): the
+// analogue of the reference's MPI_Bcast of the image properties (kernel.cu:129).
+void broadcast_small(Comm* comm, void* host, size_t bytes, int root, int device) {
+  if (!comm || comm->size() <= 1) return;
+  STRIPE_CHECK(bytes <= 256, "broadcast_small is for metadata (<= 256 bytes)");
+  const bool dev = comm->device_buffers();
+  void* buf = host;
+  hipStream_t s = nullptr;
+  if (dev) {
+    if (device >= 0) HIP_CHECK(hipSetDevice(device));
+    HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    HIP_CHECK(hipMalloc(&buf, 256));
+    if (comm->rank() == root) HIP_CHECK(hipMemcpyAsync(buf, host, bytes, hipMemcpyHostToDevice, s));
+  }
+  comm->group_start();
+  if (comm->rank() == root) {
+    for (int r = 0; r < comm->size(); ++r)
+      if (r != root) comm->send(buf, bytes, r, s);
+  } else {
+    comm->recv(buf, bytes, root, s);
+  }
+  comm->group_end();
+  if (dev) {
+    if (comm->rank() != root) HIP_CHECK(hipMemcpyAsync(host, buf, bytes, hipMemcpyDeviceToHost, s));
+    comm->wait(s);
+    HIP_CHECK(hipFree(buf));
+    HIP_CHECK(hipStreamDestroy(s));
+  }
+}
+
+Image run_rank(const EngineConfig& cfg_in, Comm* comm, int device, const Image* input, int iterations,
+               PhaseTimes* times) {
+  const int rank = comm ? comm->rank() : 0;
+  EngineConfig c = cfg_in;
+  // the root knows the geometry (it read the image); everyone else learns it
+  // from the metadata broadcast
+  int meta[4] = {c.W, c.H, c.C, 0};
+  if (rank == 0) {
+    STRIPE_CHECK(input != nullptr, "rank 0 needs the input image");
+    meta[0] = input->W;
+    meta[1] = input->H;
+    meta[2] = input->C;
+  }
+  broadcast_small(comm, meta, sizeof meta, 0, device);
+  c.W = meta[0];
+  c.H = meta[1];
+  c.C = meta[2];
+  c.root_buffers = true;
+  if (device >= 0) c.device = device;
+  Engine e(c, comm);
+  if (rank == 0) e.load_root(input->data.data(), false);
+  e.scatter();
+  e.run(iterations);
+  e.gather();
+  Image out;
+  if (rank == 0) {
+    out = Image(c.W, c.H, e.out_channels());
+    e.store_root(out.data.data(), false);
+  }
+  e.synchronize();
+  if (times) *times = e.times();
+  if (comm) comm->barrier();
+  return out;
+}
+
 Image run_group(const EngineConfig& cfg, const std::vector<Comm*>& comms, const std::vector<int>& devices,
                 const Image& input, int iterations, PhaseTimes* times) {
   STRIPE_CHECK(input.W == cfg.W && input.H == cfg.H && input.C == cfg.C, "input does not match the config");
@@ -783,24 +849,14 @@ Image run_group(const EngineConfig& cfg, const std::vector<Comm*>& comms, const 
   std::exception_ptr err;
   auto body = [&](int r) {
     try {
-      EngineConfig c = cfg;
-      c.root_buffers = true;
-      if (!devices.empty()) c.device = devices[r];
-      Engine e(c, comms[r]);
-      if (r == 0) e.load_root(input.data.data(), false);
-      e.scatter();
-      e.run(iterations);
-      e.gather();
+      PhaseTimes t;
+      Image o = run_rank(cfg, comms[r], devices.empty() ? cfg.device : devices[r], r == 0 ? &input : nullptr,
+                         iterations, &t);
       if (r == 0) {
-        Image o(cfg.W, cfg.H, e.out_channels());
-        e.store_root(o.data.data(), false);
-        e.synchronize();
         std::lock_guard<std::mutex> lk(mu);
         out = std::move(o);
-        if (times) *times = e.times();
+        if (times) *times = t;
       }
-      e.synchronize();
-      comms[r]->barrier();
     } catch (...) {
       std::lock_guard<std::mutex> lk(mu);
       if (!err) err = std::current_exception();

@@ -103,3 +103,25 @@ def test_bench_host(tmp_path):
     recs = [json.loads(l) for l in js.read_text().splitlines()]
     assert [(x["n_ranks"], x["scope"]) for x in recs] == [(1, "resident"), (1, "dist"), (2, "resident"), (2, "dist")]
     assert all(x["value"] > 0 for x in recs)
+
+
+@pytest.mark.gpu
+def test_gpu_backends_and_file_rendezvous(tmp_path):
+    """local (4 logical ranks on one GPU), rccl (in-process) and the one-process-
+    per-rank rccl path with a file rendezvous (world 1 on a 1-GPU box) all match
+    the host golden run bit-for-bit."""
+    src = tmp_path / "in.ppm"
+    run("gen", "--synthetic", "700x333x3", "--seed", "4", "--output", src)
+    chain = "gray:ref,contrast:3.5,emboss3,expand"
+    ref = tmp_path / "ref.ppm"
+    run("run", "--input", src, "--output", ref, "--chain", chain, "--backend", "host", "--ranks", "3")
+    outs = []
+    for extra in (["--backend", "local", "--ranks", "4"], ["--backend", "rccl", "--ranks", "1"],
+                  ["--backend", "rccl", "--world", "1", "--rank", "0", "--rendezvous", tmp_path / "rv.id"]):
+        o = tmp_path / f"o{len(outs)}.ppm"
+        r = run("run", "--input", src, "--output", o, "--chain", chain, *extra)
+        rec = json.loads(r.stdout.strip().splitlines()[-1])
+        assert rec["kernel_ms"] >= 0
+        outs.append(o)
+    for o in outs:
+        assert run("cmp", ref, o, check=False).returncode == 0, o
