@@ -445,13 +445,32 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : 4)) void k_sep(KArgs a) {
 }
 
 // ------------------------------------------------------------------------------
-// Direct (non-separable) filters: emboss3/5, sharpen, laplace, sobel
+// Direct (non-separable) filters: emboss3/5, sharpen, laplace
 // ------------------------------------------------------------------------------
+// The last K input rows live in registers, unpacked to u16 pairs and extended
+// by the neighbour lanes' edge dwords (DPP wave shifts: no LDS, no wave sync);
+// every tap is one packed i16 multiply-add per two outputs (|sum| <= 17*255).
+// The y loop is unrolled K times so the register ring is indexed statically,
+// and the K raw rows of the next round are in flight meanwhile.
+template <int NX>
+__device__ __forceinline__ void extend_row(const uint32_t (&u)[8], uint32_t (&e)[8 + 2 * NX]) {
+#pragma unroll
+  for (int i = 0; i < NX; ++i) {
+    // lane l gets lane l-1's dword (wave_shr:1) / lane l+1's (wave_shl:1); the
+    // halo lanes 0 and 63 receive zeros and their outputs are never stored
+    e[i] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u[8 - NX + i], 0x138, 0xf, 0xf, false);
+    e[NX + 8 + i] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u[i], 0x130, 0xf, 0xf, false);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) e[NX + i] = u[i];
+}
+
 template <int C, class F, int PRO, bool SKIP>
-__global__ __launch_bounds__(kNT, 4) void k_direct(KArgs a) {
-  constexpr int R = F::R, K = F::K, S = K;  // in-order per wave: K slots suffice
+__global__ __launch_bounds__(kNT, (F::K >= 5 ? 3 : 4)) void k_direct(KArgs a) {
+  constexpr int R = F::R, K = F::K;
+  constexpr int NX = (R * C + 1) / 2;  // neighbour dwords per side
+  constexpr int NE = 8 + 2 * NX;       // extended row dwords
   constexpr int CIN = PRO == PRO_GRAY ? 3 : 1;
-  __shared__ __attribute__((aligned(16))) uint4 ring[kWaves][S][kW];
   __shared__ uint8_t luts[768];
   if (PRO != PRO_NONE || a.has_epi) {
     load_luts(a, luts);
@@ -468,77 +487,65 @@ __global__ __launch_bounds__(kNT, 4) void k_direct(KArgs a) {
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);
   const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
   const uint32_t last_row = in_row_off(a, ye - 1 + R);
-  uint4(*rg)[kW] = ring[t.wave];
-  // slot of row r is (r - (ys - R)) mod S; s0 tracks the slot of row y - R
+
+  uint32_t ring[K][NE];  // slot of input row r: (r - (ys - R)) mod K
+  auto push = [&](const RawChunk<PRO>& raw, uint32_t (&slot)[NE]) __attribute__((always_inline)) {
+    uint32_t c[4], u[8];
+    cook<PRO>(a, raw, luts + 256, c);
+    unpack16(c, u);
+    extend_row<NX>(u, slot);
+  };
 #pragma unroll
-  for (int i = 0; i < K - 1; ++i) {
-    uint32_t r[4];
-    load_chunk<PRO>(a, rin, in_row_off(a, ys - R + i), lane_in, luts + 256, r);
-    rg[i][lane] = make_uint4(r[0], r[1], r[2], r[3]);
+  for (int i = 0; i < K - 1; ++i) {  // rows ys-R .. ys+R-1
+    RawChunk<PRO> r;
+    load_raw<PRO>(rin, in_row_off(a, ys - R + i), lane_in, r);
+    push(r, ring[i]);
   }
-  RawChunk<PRO> nxt;
-  load_raw<PRO>(rin, in_row_off(a, ys + R), lane_in, nxt);
-  const int rl = lane == 0 ? 1 : (lane == kW - 1 ? kW - 2 : lane);
-  int s0 = 0;
-  for (int y = ys; y < ye; ++y) {
-    int sw = s0 + K - 1;
-    if (sw >= S) sw -= S;
-    {
-      uint32_t c[4];
-      cook<PRO>(a, nxt, luts + 256, c);
-      rg[sw][lane] = make_uint4(c[0], c[1], c[2], c[3]);
-    }
-    load_raw<PRO>(rin, y + 1 < ye ? in_row_off(a, y + 1 + R) : last_row, lane_in, nxt);
-    wave_lds_sync();
-    int acc[16], acc2[16];
+  RawChunk<PRO> nx[K];  // row y + o + R for the step o of the current round
 #pragma unroll
-    for (int j = 0; j < 16; ++j) acc[j] = acc2[j] = 0;
-    uint32_t center[4];
+  for (int o = 0; o < K; ++o) load_raw<PRO>(rin, ys + o < ye ? in_row_off(a, ys + o + R) : last_row, lane_in, nx[o]);
+
+  for (int y = ys; y < ye; y += K) {
 #pragma unroll
-    for (int dy = 0; dy < K; ++dy) {
-      int sl = s0 + dy;
-      if (sl >= S) sl -= S;
-      const uint4 l = rg[sl][rl - 1], m = rg[sl][rl], r = rg[sl][rl + 1];
-      const uint32_t win[12] = {l.x, l.y, l.z, l.w, m.x, m.y, m.z, m.w, r.x, r.y, r.z, r.w};
-      if (dy == R) {
-        center[0] = m.x;
-        center[1] = m.y;
-        center[2] = m.z;
-        center[3] = m.w;
+    for (int o = 0; o < K; ++o) {
+      const int yy = y + o;
+      push(nx[o], ring[(o + K - 1) % K]);
+      load_raw<PRO>(rin, yy + K < ye ? in_row_off(a, yy + K + R) : last_row, lane_in, nx[o]);
+      uint32_t h[8];
+#pragma unroll
+      for (int pp = 0; pp < 8; ++pp) {
+        i16x2 acc = {0, 0};
+#pragma unroll
+        for (int dy = 0; dy < K; ++dy)
+#pragma unroll
+          for (int dx = 0; dx < K; ++dx) {
+            constexpr int unused = 0;
+            (void)unused;
+            const int w = F::w(dy, dx);
+            if (w == 0) continue;
+            const i16x2 v = as_i16x2(pair_at(ring[(o + dy) % K], 2 * NX + 2 * pp + (dx - R) * C));
+            if (w == 1) acc += v;
+            else if (w == -1) acc -= v;
+            else acc += v * (short)w;
+          }
+        acc = __builtin_elementwise_max(acc, (i16x2)(short)0);
+        h[pp] = as_u32(__builtin_elementwise_min(acc, (i16x2)(short)255));
       }
+      uint32_t o4[4];
 #pragma unroll
-      for (int dx = 0; dx < K; ++dx) {
-        const int wx = F::w(dy, dx);
-        int wy = 0;
-        if constexpr (F::SOBEL) wy = F::wy(dy, dx);
-        if (wx == 0 && wy == 0) continue;
+      for (int q = 0; q < 4; ++q) o4[q] = __builtin_amdgcn_perm(h[2 * q + 1], h[2 * q], 0x06040200u);
+      if constexpr (SKIP) {
+        uint32_t center[4];
+        const uint32_t(&cr)[NE] = ring[(o + R) % K];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const int k = 16 + j + (dx - R) * C;
-          const int v = (int)((win[k >> 2] >> ((k & 3) * 8)) & 0xFFu);
-          if (wx != 0) acc[j] += wx * v;
-          if constexpr (F::SOBEL)
-            if (wy != 0) acc2[j] += wy * v;
-        }
+        for (int q = 0; q < 4; ++q) center[q] = __builtin_amdgcn_perm(cr[NX + 2 * q + 1], cr[NX + 2 * q], 0x06040200u);
+        apply_skip<C>(a, cb, a.row0 + yy, R, center, o4);
       }
+      if (a.has_epi) lut16(luts + 512, o4);
+      const u32x4 ov = {o4[0], o4[1], o4[2], o4[3]};
+      __builtin_amdgcn_raw_buffer_store_b128(
+          ov, rout, yy < ye ? a.out_org + (uint32_t)((int64_t)yy * a.out_pitch) + lane_out : kOOB, 0, 0);
     }
-    wave_lds_sync();  // window reads done before the next row overwrites a slot
-    uint32_t ob[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      int v = acc[j];
-      if constexpr (F::SOBEL) v = abs(acc[j]) + abs(acc2[j]);
-      ob[j] = (uint32_t)min(max(v, 0), 255);
-    }
-    uint32_t o[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) o[q] = pack4(ob[4 * q], ob[4 * q + 1], ob[4 * q + 2], ob[4 * q + 3]);
-    if constexpr (SKIP) apply_skip<C>(a, cb, a.row0 + y, R, center, o);
-    if (a.has_epi) lut16(luts + 512, o);
-    const u32x4 ov = {o[0], o[1], o[2], o[3]};
-    __builtin_amdgcn_raw_buffer_store_b128(ov, rout, a.out_org + (uint32_t)((int64_t)y * a.out_pitch) + lane_out,
-                                           0, 0);
-    s0 = s0 + 1 == S ? 0 : s0 + 1;
   }
   band_margins<C>(a, t);
 }
