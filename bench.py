@@ -54,6 +54,11 @@ def parse():
 
 def main():
     a = parse()
+    # libraries (RCCL's init banner, HIP warnings) print to stdout; keep stdout for
+    # the one JSON line of the driver contract and send everything else to stderr
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     import torch
     import torch.distributed as dist
 
@@ -233,7 +238,7 @@ def main():
             "tuned_band_rows": dp.engine.bands,
             "stage_ms_rank0": stages,
         }
-        print(json.dumps(rec), flush=True)
+        os.write(json_fd, (json.dumps(rec) + "\n").encode())
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -95,6 +95,10 @@ def init(backend: str = "auto") -> DistContext:
     if device:
         torch.cuda.set_device(local_rank)
     comm = None
+    if device and world == 1:
+        # a one-rank RCCL communicator: no traffic, but the same comm object,
+        # bounded waits and barrier as the multi-rank path (exercised on 1-GPU boxes)
+        comm = C.make_rccl_comm(C.rccl_unique_id(), 0, 1, local_rank)
     if world > 1:
         if not dist.is_initialized():
             # the process-group timeout follows the native collective bound
