@@ -351,7 +351,10 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : 4)) void k_sep(KArgs a) {
     for (int q = 0; q < WDW / 4; ++q) {
       // window dword 4q is logical dword g = 8*rl - WLO/2 + 4q: lane g/8, plane (g/4)&1
       const int g = 8 * rl - WLO / 2 + 4 * q;
-      const uint4 v = vb[(g >> 2) & 1][g >> 3];
+      // whole 16-byte chunks (volatile: the compiler would otherwise trim the
+      // window to the dwords it needs and issue ds_read_b32/b64/read2 pieces
+      // whose 16-byte lane stride conflicts 4-way under the (a/4)%32 banking)
+      const u32x4 v = *(volatile __attribute__((address_space(3))) u32x4*)(&vb[(g >> 2) & 1][g >> 3]);
       w[4 * q] = v.x;
       w[4 * q + 1] = v.y;
       w[4 * q + 2] = v.z;
@@ -362,7 +365,7 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : 4)) void k_sep(KArgs a) {
 #pragma unroll
       for (int q = 0; q < WDW / 4; ++q) {
         const int g = 8 * rl - WLO / 2 + 4 * q;
-        const uint4 v = vb[2 + ((g >> 2) & 1)][g >> 3];
+        const u32x4 v = *(volatile __attribute__((address_space(3))) u32x4*)(&vb[2 + ((g >> 2) & 1)][g >> 3]);
         wd[4 * q] = v.x;
         wd[4 * q + 1] = v.y;
         wd[4 * q + 2] = v.z;
