@@ -13,7 +13,7 @@
 //                [--no-halo] [--expand-gray] [--legacy-partition] [--iterations K]
 //                [--no-fuse] [--no-overlap] [--verbose]
 //   stripe bench --synthetic 16384x16384x3 --seed 1 --chain gaussian5 --ranks 1,2,4,8
-//                --iters 20 --warmup 5 --scope resident,dist [--backend rccl|local]
+//                --iters 20 --warmup 5 --scope resident,dist,e2e [--backend rccl|local]
 //                [--json out.json]
 //   stripe cmp   a.ppm b.ppm [--tol 0]
 //   stripe gen   --synthetic WxHxC --seed S --output x.ppm
@@ -323,8 +323,10 @@ int cmd_bench(const Args& a) {
   if (scopes.find("dist") != std::string::npos) full = synth_image(seed, W, H, C);
   for (int N : ranks) {
     Group g = make_group(backend, N, parse_int_list(a.get("devices")));
-    for (const std::string scope : {"resident", "dist"}) {
-      if (scopes.find(scope) == std::string::npos) continue;
+    for (const std::string scope : {"resident", "dist", "e2e"}) {
+      if (scopes.find(scope) == std::string::npos && !(scope == "resident" && scopes.find("device") != std::string::npos))
+        continue;
+      if (scope == "e2e" && cfg.backend != BackendKind::Device) continue;  // host backend has no transfers
       std::vector<double> per_rank(N, 0);
       std::mutex mu;
       std::exception_ptr err;
@@ -336,6 +338,11 @@ int cmd_bench(const Args& a) {
           Engine e(c, g.comms[r]);
           if (scope == "dist") {
             if (r == 0) e.load_root(full.data.data(), false);
+          } else if (scope == "e2e") {
+            // per-rank pinned host stripes (SURVEY §6 e2e scope): H2D -> chain -> D2H
+            e.alloc_host_io();
+            const Stripe& st = e.stripe();
+            synth_rows(seed, W, C, st.row0, st.rows, e.host_in());
           } else {
             e.load_synthetic(seed);
           }
@@ -346,6 +353,8 @@ int cmd_bench(const Args& a) {
               e.scatter();
               e.run(1);
               e.gather();
+            } else if (scope == "e2e") {
+              e.run_e2e(8);
             } else {
               if (!iterable) e.rewind();  // re-read the unchanged input (e.g. gray: 3 -> 1 channels)
               e.run(1);
@@ -399,7 +408,7 @@ void usage() {
                "        [--expand-gray] [--legacy-partition] [--iterations K] [--no-fuse] [--no-overlap]\n"
                "        one process per rank: --backend rccl --world N --rank r --rendezvous FILE [--device d]\n"
                "  bench --synthetic WxHxC [--seed S] [--chain C] [--ranks 1,2,4,8] [--iters N] [--warmup N]\n"
-               "        [--scope resident,dist] [--backend rccl|local|host] [--json out.json]\n"
+               "        [--scope resident|device,dist,e2e] [--backend rccl|local|host] [--json out.json]\n"
                "  cmp   a.ppm b.ppm [--tol T]\n"
                "  gen   --synthetic WxHxC [--seed S] --output out.ppm\n"
                "  info  [--chain C] [--channels C]\n");
