@@ -236,7 +236,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("backend", &EngineConfig::backend)
       .def_readwrite("band", &EngineConfig::band)
       .def_readwrite("root_buffers", &EngineConfig::root_buffers)
-      .def_readwrite("autotune", &EngineConfig::autotune);
+      .def_readwrite("autotune", &EngineConfig::autotune)
+      .def_readwrite("graphs", &EngineConfig::graphs);
 
   py::class_<PhaseTimes>(m, "PhaseTimes")
       .def_readonly("run", &PhaseTimes::run)
@@ -372,7 +373,8 @@ PYBIND11_MODULE(_C, m) {
         py::gil_scoped_release nogil;
         e.synchronize();
       })
-      .def_property_readonly("times", [](const Engine& e) { return e.times(); });
+      .def_property_readonly("times", [](const Engine& e) { return e.times(); })
+      .def_property_readonly("graph_launches", &Engine::graph_launches);
 
   m.def("run_local_group", [](const EngineConfig& cfg, int world, const U8Array& a, int iterations) {
     Image img = image_from_numpy(a);

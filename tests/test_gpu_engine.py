@@ -108,3 +108,25 @@ def test_e2e_pinned_pipeline(m, chain, chunks):
             assert np.abs(out.astype(int) - ref.astype(int)).max() <= 1
         else:
             assert (out == ref).all()
+
+
+@pytest.mark.parametrize("chain", ["gaussian5", "gaussian5,sobel", "invert,gaussian3,emboss3", "blur:9"])
+@pytest.mark.parametrize("iters", [2, 5, 8])
+def test_graph_replay_matches_eager(m, chain, iters):
+    """Iterated chains replay a captured hipGraph (one cycle of 1 or 2
+    iterations); results equal the eager launches bit-for-bit."""
+    C = m._C
+    outs = []
+    for graphs in (True, False):
+        cfg = m.Pipeline(chain).config(257, 131, 3, "device", device=0)
+        cfg.graphs = graphs
+        e = C.Engine(cfg, None)
+        e.load_synthetic(3)
+        e.run(iters)
+        e.run(iters)  # second call replays the already-captured graph
+        e.synchronize()
+        outs.append(e.store_packed())
+        cycle = 1 if len(C.plan_info(chain, 3)["passes"]) % 2 == 0 else 2
+        expect = graphs and iters >= 2 * cycle
+        assert (e.graph_launches > 0) == expect, (chain, iters, e.graph_launches)
+    assert (outs[0] == outs[1]).all()

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--bands", default="0", help="comma list of stencil band heights (0 = auto)")
     ap.add_argument("--no-fuse", action="store_true")
+    ap.add_argument("--no-graphs", action="store_true", help="eager launches instead of hipGraph replay")
     a = ap.parse_args()
     import torch
 
@@ -34,6 +35,7 @@ def main():
         pipe = Pipeline(chain, fuse=not a.no_fuse)
         cfg = pipe.config(W, H, Cc, "device", device=0)
         cfg.band = band
+        cfg.graphs = not a.no_graphs
         e = C.Engine(cfg)
         info = C.plan_info(chain, Cc)
         e.load_synthetic(1)
@@ -53,7 +55,7 @@ def main():
         byts = sum(W * H * (p["cin"] + p["cout"]) for p in info["passes"])
         print(json.dumps({"chain": chain, "band": band, "shape": a.shape, "ms": round(ms, 4),
                           "mpx_s": round(W * H / ms / 1e3, 1), "GBps": round(byts / ms / 1e6, 1),
-                          "passes": len(info["passes"])}), flush=True)
+                          "passes": len(info["passes"]), "graphs": e.graph_launches > 0}), flush=True)
         del e
 
 
