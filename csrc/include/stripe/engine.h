@@ -168,6 +168,7 @@ class Engine {
   uint8_t* origin(const Buffer& b, int C) const;
   uint8_t* root_origin(const Buffer& b, int C) const;
   void exchange_halo(uint8_t* org, int C, int R, hipStream_t s);
+  bool time_halo_ = true;  // record the halo stage events (last iteration of a run only)
   void run_pass(const Pass& p, const uint8_t* in, uint8_t* out);
   void copy2d(void* dst, int64_t dpitch, const void* src, int64_t spitch, int64_t width, int64_t rows,
               hipStream_t s, int kind);
