@@ -59,6 +59,7 @@ struct SepArgs {
   KArgs a;
   const u4* tw;  // [entry][lane] weight fragments (8 halves each)
   int R, L, nstrips;
+  int a0, a2;  // group-grid origins of ranges 0 / 1 (global row multiple of 32)
 };
 
 __device__ __forceinline__ void sep_lds_sync() {
@@ -109,8 +110,20 @@ __global__ __launch_bounds__(kSepWaves * 64, 2) void k_blur_sep(SepArgs sa) {
   if (task >= sa.nstrips * a.nbands) return;  // wave-uniform
   uint8_t* wl = lds + wave * kSepTile;
   const int strip = task % sa.nstrips, by = task / sa.nstrips;
-  int ys, ye;
-  band_range(a, by, ys, ye);
+  // bands and 32-row groups sit on a grid of global rows (multiples of 32), so
+  // every output row is summed in the same order whatever the launch's row
+  // ranges (interior/boundary split, rank count): results are independent of
+  // the partition, bit for bit
+  int base, ys, ye;
+  if (by < a.nb0) {
+    base = sa.a0 + by * a.band;
+    ys = max(base, a.ry0);
+    ye = min(base + a.band, a.ry1);
+  } else {
+    base = sa.a2 + (by - a.nb0) * a.band;
+    ys = max(base, a.ry2);
+    ye = min(base + a.band, a.ry3);
+  }
   const int R = sa.R;
 
   // ---- weights (per-lane MFMA fragments, see prepare_sep_consts) ----
@@ -140,8 +153,8 @@ __global__ __launch_bounds__(kSepWaves * 64, 2) void k_blur_sep(SepArgs sa) {
 
   const int sx = strip * kSepSB;           // first output byte of the strip
   const int x_in = sx - sa.L + 8 * chunk;  // byte offset of the lane's chunk in a row
-  const int yh0 = ys - 16;                 // input row of X row 0
-  const int ngroups = (ye - ys + 31) >> 5; // 32-row output groups
+  const int yh0 = base - 16;               // input row of X row 0
+  const int ngroups = (ye - base + 31) >> 5;  // 32-row output groups
   const int npairs = ngroups + 1;          // 32-row X pairs (tiles 2k, 2k+1)
 
   u2 pf[kSepLoads];
@@ -181,7 +194,7 @@ __global__ __launch_bounds__(kSepWaves * 64, 2) void k_blur_sep(SepArgs sa) {
     }
     sep_lds_sync();
     if (START) prefetch(k + 1);  // pair k + 1 exists iff group k does
-    const int yg = ys + 32 * (k - 1);  // first row of the group being finished
+    const int yg = base + 32 * (k - 1);  // first row of the group being finished
 #pragma unroll
     for (int j = 0; j < kSepNJ; ++j) {
       // horizontal: X tiles 2k (rows 0..15 of the pair) and 2k+1 (16..31), column j
@@ -214,7 +227,7 @@ __global__ __launch_bounds__(kSepWaves * 64, 2) void k_blur_sep(SepArgs sa) {
           const int y = yg + 16 * q + m;
           const int x = xo + 16 * j;
           const uint32_t off =
-              (y < ye && x < a.E) ? a.out_org + (uint32_t)((int64_t)y * a.out_pitch) + (uint32_t)x : kOOB;
+              (y >= ys && y < ye && x < a.E) ? a.out_org + (uint32_t)((int64_t)y * a.out_pitch) + (uint32_t)x : kOOB;
           __builtin_amdgcn_raw_buffer_store_b32(o, rout, off, 0, 0);
         }
         if constexpr (START) {
@@ -370,8 +383,11 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
       return e ? std::atoi(e) : 0;
     }();
     a.nxcd = nxcd;
-    a.nb0 = (int)div_up(n0, band);
-    a.nbands = a.nb0 + (int)div_up(n1, band);
+    auto grid0 = [&](int y0) { return y0 - (int)(((int64_t)L.row0 + y0) & 31); };
+    sa.a0 = grid0(a.ry0);
+    sa.a2 = n1 ? grid0(a.ry2) : 0;
+    a.nb0 = (int)div_up(a.ry1 - sa.a0, band);
+    a.nbands = a.nb0 + (n1 ? (int)div_up(a.ry3 - sa.a2, band) : 0);
     const dim3 grid((unsigned)div_up((int64_t)sa.nstrips * a.nbands, dev::kSepWaves));
     const size_t lds = (size_t)dev::kSepWaves * dev::kSepTile;
     // the kernel is channel-agnostic: the tap stride lives in the weight fragments

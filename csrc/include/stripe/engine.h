@@ -39,6 +39,8 @@ struct EngineConfig {
   int band = 0;                 // stencil rows per workgroup (0 = auto)
   bool root_buffers = false;    // rank 0 allocates full-frame in/out buffers (scatter/gather)
   bool autotune = false;        // time candidate band heights per stencil pass on first run()
+  bool pipeline = true;         // iterated single-pass chains over > 1 ranks: core / rim /
+                                // boundary rows on two streams (Engine::run_pipelined)
   bool graphs = false;          // replay iterated chains from a captured hipGraph when a run()
                                 // involves no collective (single rank, or no halo exchange).
                                 // Off by default: measured on MI355X/ROCm 7, graph replay of
@@ -170,6 +172,10 @@ class Engine {
   void exchange_halo(uint8_t* org, int C, int R, hipStream_t s);
   bool time_halo_ = true;  // record the halo stage events (last iteration of a run only)
   void run_pass(const Pass& p, const uint8_t* in, uint8_t* out);
+  bool pipelined_ok() const;
+  void run_pipelined(int iterations);
+  hipStream_t s_edge_ = nullptr;   // rim + boundary rows of the pipelined halo schedule
+  hipEvent_t pev_[7] = {};         // core[2], rim[2], boundary, exchange, start
   void copy2d(void* dst, int64_t dpitch, const void* src, int64_t spitch, int64_t width, int64_t rows,
               hipStream_t s, int kind);
   void fill_margins(uint8_t* org, int C, int y0, int y1, int px, Border b, hipStream_t s);

@@ -237,7 +237,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("band", &EngineConfig::band)
       .def_readwrite("root_buffers", &EngineConfig::root_buffers)
       .def_readwrite("autotune", &EngineConfig::autotune)
-      .def_readwrite("graphs", &EngineConfig::graphs);
+      .def_readwrite("graphs", &EngineConfig::graphs)
+      .def_readwrite("pipeline", &EngineConfig::pipeline);
 
   py::class_<PhaseTimes>(m, "PhaseTimes")
       .def_readonly("run", &PhaseTimes::run)

@@ -137,6 +137,9 @@ Engine::~Engine() {
         if (e) (void)hipEventDestroy(e);
     for (auto& g : gexec_)
       if (g) (void)hipGraphExecDestroy(g);
+    for (auto& e : pev_)
+      if (e) (void)hipEventDestroy(e);
+    if (s_edge_) (void)hipStreamDestroy(s_edge_);
     for (auto& e : ev_h2d_) (void)hipEventDestroy(e);
     for (auto& e : ev_cmp_) (void)hipEventDestroy(e);
     if (s_h2d_) (void)hipStreamDestroy(s_h2d_);
@@ -458,6 +461,90 @@ void Engine::run_pass(const Pass& p, const uint8_t* in, uint8_t* out) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Pipelined halo schedule (iterated single-pass chains over > 1 ranks).
+//
+// Per step k (input A, output B, radius R) the output rows split three ways:
+//   core  [2R, rows-2R)                main stream; reads A[R, rows-R): the
+//                                      previous step's core + rim rows only
+//   rim   [R, 2R) u [rows-2R, rows-R)  edge stream; reads A[0, 3R) (+ bottom)
+//   edge  [0, R) u [rows-R, rows)      edge stream after the halo exchange
+// so the exchange and the boundary rows run beside the next core instead of
+// between consecutive cores.  Cross-stream hazards (A/B ping-pong):
+//   core_k  waits rim_{k-1}   (RAW on A[R,2R); WAR: rim_{k-1} read B[2R,3R))
+//   rim_k   waits core_{k-1}  (RAW on A[2R,3R); WAR: core_{k-1} read B[R,2R))
+//   xchg_k  waits edge_{k-1}  (sends A[0,R), A[rows-R,rows))
+//   edge_k  waits xchg_k      (halo rows), edge stream order covers the rest
+// core/rim events alternate by step parity so core_k never waits rim_k.
+// ---------------------------------------------------------------------------
+bool Engine::pipelined_ok() const {
+  if (!device() || !cfg_.halo || !cfg_.overlap || part_.active <= 1) return false;
+  if (plan_.passes.size() != 1 || plan_.cin != plan_.cout) return false;
+  const int R = plan_.passes[0].R;
+  const int rows = stripe().rows;
+  return R > 0 && rows > 4 * R && comm_ != nullptr;
+}
+
+void Engine::run_pipelined(int iterations) {
+  const Pass& p = plan_.passes[0];
+  const int R = p.R, rows = stripe().rows;
+  if (!s_edge_) {
+    HIP_CHECK(hipStreamCreateWithFlags(&s_edge_, hipStreamNonBlocking));
+    for (auto& e : pev_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  hipEvent_t* ev_core = &pev_[0];
+  hipEvent_t* ev_rim = &pev_[2];
+  hipEvent_t& ev_bnd = pev_[4];
+  hipEvent_t& ev_x = pev_[5];
+  hipEvent_t& ev_start = pev_[6];
+  // everything queued before (input load, previous runs) precedes the first step
+  HIP_CHECK(hipEventRecord(ev_start, s_compute_));
+  HIP_CHECK(hipStreamWaitEvent(s_edge_, ev_start, 0));
+  HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_start, 0));
+  for (hipEvent_t e : {ev_core[1], ev_rim[1], ev_bnd}) HIP_CHECK(hipEventRecord(e, s_compute_));
+  const PassConsts& pc = prt_[0].pc;
+  for (int k = 0; k < iterations; ++k) {
+    time_halo_ = k == iterations - 1;
+    const int par = k & 1;
+    uint8_t* in = origin(buf_[cur_], p.cin);
+    uint8_t* out = origin(buf_[cur_ ^ 1], p.cout);
+    PassLaunch L = make_launch(p, in, out, 0);
+    // core (main stream)
+    HIP_CHECK(hipStreamWaitEvent(s_compute_, ev_rim[par ^ 1], 0));
+    L.nrange = 1;
+    L.ry[0] = 2 * R;
+    L.ry[1] = rows - 2 * R;
+    launch_pass(p, pc, L, s_compute_);
+    HIP_CHECK(hipEventRecord(ev_core[par], s_compute_));
+    // halo exchange (comm stream) once the previous boundary rows exist
+    HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_bnd, 0));
+    exchange_halo(in, p.cin, R, s_comm_);
+    HIP_CHECK(hipEventRecord(ev_x, s_comm_));
+    // rim (edge stream)
+    HIP_CHECK(hipStreamWaitEvent(s_edge_, ev_core[par ^ 1], 0));
+    L.nrange = 2;
+    L.ry[0] = R;
+    L.ry[1] = 2 * R;
+    L.ry[2] = rows - 2 * R;
+    L.ry[3] = rows - R;
+    launch_pass(p, pc, L, s_edge_);
+    HIP_CHECK(hipEventRecord(ev_rim[par], s_edge_));
+    // boundary rows (edge stream) after the halo arrived
+    HIP_CHECK(hipStreamWaitEvent(s_edge_, ev_x, 0));
+    L.ry[0] = 0;
+    L.ry[1] = R;
+    L.ry[2] = rows - R;
+    L.ry[3] = rows;
+    launch_pass(p, pc, L, s_edge_);
+    HIP_CHECK(hipEventRecord(ev_bnd, s_edge_));
+    cur_ ^= 1;
+    cur_c_ = plan_.cout;
+  }
+  // later work on the compute stream sees every region of the last step
+  HIP_CHECK(hipStreamWaitEvent(s_compute_, ev_bnd, 0));
+  time_halo_ = true;
+}
+
 std::vector<int> Engine::bands() const {
   std::vector<int> b;
   for (const auto& p : prt_) b.push_back(p.band);
@@ -528,7 +615,9 @@ void Engine::run(int iterations) {
     }
   };
   const int cycle = plan_.passes.size() % 2 == 0 ? 1 : 2;
-  if (graph_ok() && cur_c_ == plan_.cin && iterations >= (gexec_[cur_] ? cycle : 2 * cycle)) {
+  if (cfg_.pipeline && pipelined_ok() && cur_c_ == plan_.cin) {
+    run_pipelined(iterations);
+  } else if (graph_ok() && cur_c_ == plan_.cin && iterations >= (gexec_[cur_] ? cycle : 2 * cycle)) {
     // launch-bound inner loop: capture one cycle of iterations once, replay it
     const int start = cur_;
     if (!gexec_[start]) {
@@ -812,6 +901,7 @@ void Engine::synchronize() {
   TraceRange tr("stripe.synchronize");
   wait_stream(s_compute_);
   wait_stream(s_comm_);
+  wait_stream(s_edge_);
   wait_stream(s_h2d_);
   wait_stream(s_d2h_);
   collect_times();

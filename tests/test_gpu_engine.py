@@ -130,3 +130,22 @@ def test_graph_replay_matches_eager(m, chain, iters):
         expect = graphs and iters >= 2 * cycle
         assert (e.graph_launches > 0) == expect, (chain, iters, e.graph_launches)
     assert (outs[0] == outs[1]).all()
+
+
+@pytest.mark.parametrize("chain", ["gaussian5", "sobel", "emboss3", "blur:9", "gaussian7"])
+@pytest.mark.parametrize("ranks,H", [(2, 96), (4, 130), (8, 97), (5, 40)])
+def test_pipelined_halo_schedule(m, chain, ranks, H):
+    """Iterated single-pass chains over several ranks run the core / rim /
+    boundary schedule on two streams; it must equal the plain schedule and the
+    1-rank result (H=40 with 5 ranks: stripes too short to pipeline mix with
+    pipelined ones)."""
+    img = m.utils.synthetic_image(7, 203, H, 3)
+    C = m._C
+    res = []
+    for pipeline, nr in ((True, ranks), (False, ranks), (True, 1)):
+        pipe = m.Pipeline(chain)
+        cfg = pipe.config(203, H, 3, "device", device=0)
+        cfg.pipeline = pipeline
+        res.append(C.run_local_group(cfg, nr, img, 4))
+    assert (res[0] == res[1]).all()
+    assert (res[0] == res[2]).all()

@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--bands", default="0", help="comma list of stencil band heights (0 = auto)")
     ap.add_argument("--no-fuse", action="store_true")
-    ap.add_argument("--no-graphs", action="store_true", help="eager launches instead of hipGraph replay")
+    ap.add_argument("--graphs", action="store_true", help="replay iterations from a captured hipGraph")
     a = ap.parse_args()
     import torch
 
@@ -35,7 +35,7 @@ def main():
         pipe = Pipeline(chain, fuse=not a.no_fuse)
         cfg = pipe.config(W, H, Cc, "device", device=0)
         cfg.band = band
-        cfg.graphs = not a.no_graphs
+        cfg.graphs = a.graphs
         e = C.Engine(cfg)
         info = C.plan_info(chain, Cc)
         e.load_synthetic(1)
