@@ -52,7 +52,7 @@ struct Args {
 };
 
 const std::vector<std::string> kFlags = {"no-halo", "expand-gray", "legacy-partition", "no-fuse",
-                                         "no-overlap", "verbose", "help"};
+                                         "no-overlap", "no-pipeline", "graphs", "verbose", "help"};
 
 Args parse_args(int argc, char** argv) {
   Args a;
@@ -129,6 +129,13 @@ EngineConfig config_from(const Args& a, int W, int H, int C) {
   if (a.has("legacy-partition")) cfg.legacy_partition = true;
   if (a.has("no-fuse")) cfg.fuse = false;
   if (a.has("no-overlap")) cfg.overlap = false;
+  if (a.has("no-pipeline")) cfg.pipeline = false;
+  if (const char* e = std::getenv("STRIPE_HALO_SCHEDULE")) {  // tuning: overlap | pipeline | serial
+    const std::string v = e;
+    cfg.pipeline = v == "pipeline";
+    cfg.overlap = v != "serial";
+  }
+  if (a.has("graphs")) cfg.graphs = true;
   if (a.has("expand-gray") && cfg.chain.find("expand") == std::string::npos) cfg.chain += ",expand";
   cfg.band = a.geti("band", 0);
   const std::string be = a.get("backend", device_count() > 0 ? "local" : "host");
@@ -409,6 +416,7 @@ void usage() {
                "        one process per rank: --backend rccl --world N --rank r --rendezvous FILE [--device d]\n"
                "  bench --synthetic WxHxC [--seed S] [--chain C] [--ranks 1,2,4,8] [--iters N] [--warmup N]\n"
                "        [--scope resident|device,dist,e2e] [--backend rccl|local|host] [--json out.json]\n"
+               "        [--no-overlap] [--no-pipeline] [--graphs] [--band ROWS]\n"
                "  cmp   a.ppm b.ppm [--tol T]\n"
                "  gen   --synthetic WxHxC [--seed S] --output out.ppm\n"
                "  info  [--chain C] [--channels C]\n");

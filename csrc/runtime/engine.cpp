@@ -12,6 +12,23 @@
 
 namespace stripe {
 
+// STRIPE_SCHEDULE_EMU=split|pipe|split1 runs the multi-rank schedules on one
+// rank (without the exchange) to time their launch/stream overhead on one GPU.
+// Measured, gaussian5 on a 16384x2048 RGB stripe (the N=8 share): one launch
+// 43.0 us/step; interior+boundary on one stream 46.9; the overlap schedule
+// (cross-stream events around the exchange) 54.4; the pipelined schedule 51.5.
+// Cross-queue event waits cost ~7 us per step on this stack, so the pipelined
+// schedule (one cross-queue wait on the critical path) is the default.
+static int schedule_emu() {
+  static const int v = [] {
+    const char* e = std::getenv("STRIPE_SCHEDULE_EMU");
+    if (!e) return 0;
+    return std::strcmp(e, "split") == 0 ? 1 : std::strcmp(e, "pipe") == 0 ? 2 : std::strcmp(e, "split1") == 0 ? 3 : 0;
+  }();
+  return v;
+}
+
+
 // ---------------------------------------------------------------------------
 // Buffer
 // ---------------------------------------------------------------------------
@@ -421,7 +438,22 @@ void Engine::run_pass(const Pass& p, const uint8_t* in, uint8_t* out) {
   if (rows == 0) return;
   const RowGeom g = geom();
   const int R = p.R;
-  const bool xchg = cfg_.halo && R > 0 && part_.active > 1;
+  const bool xchg = (cfg_.halo && R > 0 && part_.active > 1) || (device() && schedule_emu() == 1 && R > 0);
+  if (device() && schedule_emu() == 3 && R > 0 && rows > 2 * R) {  // two launches, one stream, no events
+    const size_t pi3 = (size_t)(&p - plan_.passes.data());
+    PassLaunch L3 = make_launch(p, in, out, (int)pi3);
+    L3.nrange = 1;
+    L3.ry[0] = R;
+    L3.ry[1] = rows - R;
+    launch_pass(p, prt_[pi3].pc, L3, s_compute_);
+    L3.nrange = 2;
+    L3.ry[0] = 0;
+    L3.ry[1] = R;
+    L3.ry[2] = rows - R;
+    L3.ry[3] = rows;
+    launch_pass(p, prt_[pi3].pc, L3, s_compute_);
+    return;
+  }
   if (!device()) {
     if (xchg) exchange_halo(const_cast<uint8_t*>(in), p.cin, R, nullptr);
     golden_pass(p, ConstView{in, pitch(p.cin)}, MutView{out, pitch(p.cout)}, cfg_.W, g, 0, rows);
@@ -478,6 +510,9 @@ void Engine::run_pass(const Pass& p, const uint8_t* in, uint8_t* out) {
 // core/rim events alternate by step parity so core_k never waits rim_k.
 // ---------------------------------------------------------------------------
 bool Engine::pipelined_ok() const {
+  if (device() && schedule_emu() == 2 && plan_.passes.size() == 1 && plan_.cin == plan_.cout &&
+      stripe().rows > 4 * plan_.passes[0].R && plan_.passes[0].R > 0)
+    return true;
   if (!device() || !cfg_.halo || !cfg_.overlap || part_.active <= 1) return false;
   if (plan_.passes.size() != 1 || plan_.cin != plan_.cout) return false;
   const int R = plan_.passes[0].R;
@@ -615,7 +650,7 @@ void Engine::run(int iterations) {
     }
   };
   const int cycle = plan_.passes.size() % 2 == 0 ? 1 : 2;
-  if (cfg_.pipeline && pipelined_ok() && cur_c_ == plan_.cin) {
+  if (cfg_.pipeline && cfg_.overlap && pipelined_ok() && cur_c_ == plan_.cin) {
     run_pipelined(iterations);
   } else if (graph_ok() && cur_c_ == plan_.cin && iterations >= (gexec_[cur_] ? cycle : 2 * cycle)) {
     // launch-bound inner loop: capture one cycle of iterations once, replay it

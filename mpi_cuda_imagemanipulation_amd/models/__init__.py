@@ -7,6 +7,7 @@ Appendix A), next to the BASELINE.json benchmark configurations.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field, replace
 
 import numpy as np
@@ -98,6 +99,10 @@ class Pipeline:
         cfg.device = int(device)
         cfg.backend = C.Backend.host if backend == "host" else C.Backend.device
         cfg.autotune = bool(autotune)
+        sched = os.environ.get("STRIPE_HALO_SCHEDULE")  # tuning: overlap | pipeline | serial
+        if sched:
+            cfg.pipeline = sched == "pipeline"
+            cfg.overlap = sched != "serial"
         return cfg
 
     def run_distributed(self, image: np.ndarray, ranks: int, backend: str = "host", iterations: int = 1):
