@@ -516,6 +516,9 @@ bool Engine::pipelined_ok() const {
   if (!device() || !cfg_.halo || !cfg_.overlap || part_.active <= 1) return false;
   if (plan_.passes.size() != 1 || plan_.cin != plan_.cout) return false;
   const int R = plan_.passes[0].R;
+  // large windows (MFMA blur) pay a whole 32-row group per thin rim range:
+  // the three-way split costs more than it hides (blur:31 stripe 0.124 vs 0.114 ms)
+  if (plan_.passes[0].kind == PassKind::Conv && schedule_emu() != 2) return false;
   const int rows = stripe().rows;
   return R > 0 && rows > 4 * R && comm_ != nullptr;
 }
