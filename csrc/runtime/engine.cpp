@@ -3,6 +3,7 @@
 
 #include "stripe/trace.h"
 
+#include <algorithm>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -603,8 +604,10 @@ void Engine::autotune_bands() {
     int best_band = 0;
     for (int b : cand) {
       prt_[i].band = b;
-      float tot = 0;
-      for (int rep = 0; rep < 4; ++rep) {
+      // median of 7 timed launches after one warmup: single launches of a
+      // 40-300 us kernel jitter by a few percent, about the gap between bands
+      std::vector<float> t;
+      for (int rep = 0; rep < 8; ++rep) {
         PassLaunch L = make_launch(p, origin(buf_[cur_], p.cin), origin(buf_[cur_ ^ 1], p.cout), (int)i);
         L.band = b;
         L.ry[0] = 0;
@@ -613,10 +616,12 @@ void Engine::autotune_bands() {
         launch_pass(p, prt_[i].pc, L, s_compute_);
         HIP_CHECK(hipEventRecord(e1, s_compute_));
         HIP_CHECK(hipEventSynchronize(e1));
-        if (rep > 0) tot += elapsed(e0, e1);  // first launch is a warmup
+        if (rep > 0) t.push_back(elapsed(e0, e1));
       }
-      if (tot < best) {
-        best = tot;
+      std::nth_element(t.begin(), t.begin() + t.size() / 2, t.end());
+      const float med = t[t.size() / 2];
+      if (med < best) {
+        best = med;
         best_band = b;
       }
     }
