@@ -8,7 +8,11 @@ row-partitioned over N MI355X (one process per GPU, RCCL over xGMI).
 One step = one full-frame gaussian5 pass over the distributed frame: every rank
 exchanges its 2 halo rows with its neighbours (ncclSend/ncclRecv on a side
 stream) while its interior rows are filtered, then filters its boundary rows.
-Steps are iterated (ping-pong), so each step's halo exchange is required work.
+Steps are iterated (ping-pong), so each step's halo rows are required work.
+With k = halo_depth > 1 (auto on > 1 rank) the exchange is communication-
+avoiding: k*2 rows travel once per k steps and each step also recomputes the
+shrinking band of neighbour rows the next step needs (more arithmetic, same
+bytes on the wire, bit-identical output); --halo-depth 1 exchanges every step.
 The frame stays resident in HBM ("resident" scope); the "dist" scope
 (root GPU -> scatter -> filter -> gather -> root GPU, the analogue of the
 reference's timed window kernel.cu:190-226) and a bit-exactness check against
@@ -43,6 +47,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--band", type=int, default=0)
+    ap.add_argument("--halo-depth", type=int, default=0,
+                    help="steps per halo exchange (0: auto, 1: exchange every step)")
     ap.add_argument("--dist-steps", type=int, default=5, help="steps of the dist-scope measurement (0: skip)")
     ap.add_argument("--e2e-steps", type=int, default=3, help="steps of the e2e-scope measurement (0: skip)")
     ap.add_argument("--no-verify", action="store_true")
@@ -79,7 +85,7 @@ def main():
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     W, H, Cc = a.width, a.height, a.channels
-    pipe = Pipeline(a.chain, overlap=not a.no_overlap)
+    pipe = Pipeline(a.chain, overlap=not a.no_overlap, halo_depth=a.halo_depth)
 
     def barrier():
         if world > 1:
@@ -236,6 +242,7 @@ def main():
             "e2e_scope_mpx_s": None if e2e_mpx is None else round(e2e_mpx, 1),
             "verified_vs_golden": verify,
             "tuned_band_rows": dp.engine.bands,
+            "halo_depth": dp.engine.halo_depth,
             "stage_ms_rank0": stages,
         }
         os.write(json_fd, (json.dumps(rec) + "\n").encode())

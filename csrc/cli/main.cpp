@@ -136,6 +136,7 @@ EngineConfig config_from(const Args& a, int W, int H, int C) {
     cfg.overlap = v != "serial";
   }
   if (a.has("graphs")) cfg.graphs = true;
+  cfg.halo_depth = a.geti("halo-depth", 0);
   if (a.has("expand-gray") && cfg.chain.find("expand") == std::string::npos) cfg.chain += ",expand";
   cfg.band = a.geti("band", 0);
   const std::string be = a.get("backend", device_count() > 0 ? "local" : "host");
@@ -416,7 +417,7 @@ void usage() {
                "        one process per rank: --backend rccl --world N --rank r --rendezvous FILE [--device d]\n"
                "  bench --synthetic WxHxC [--seed S] [--chain C] [--ranks 1,2,4,8] [--iters N] [--warmup N]\n"
                "        [--scope resident|device,dist,e2e] [--backend rccl|local|host] [--json out.json]\n"
-               "        [--no-overlap] [--no-pipeline] [--graphs] [--band ROWS]\n"
+               "        [--no-overlap] [--no-pipeline] [--graphs] [--band ROWS] [--halo-depth K]\n"
                "  cmp   a.ppm b.ppm [--tol T]\n"
                "  gen   --synthetic WxHxC [--seed S] --output out.ppm\n"
                "  info  [--chain C] [--channels C]\n");

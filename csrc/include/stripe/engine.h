@@ -41,6 +41,11 @@ struct EngineConfig {
   bool autotune = false;        // time candidate band heights per stencil pass on first run()
   bool pipeline = true;         // iterated single-pass chains over > 1 ranks: core / rim /
                                 // boundary rows on two streams (Engine::run_pipelined)
+  int halo_depth = 0;           // iterated single-pass chains over > 1 ranks: iterations per
+                                // halo exchange ("deep halo": k*R rows exchanged once, the
+                                // k steps recompute a shrinking band of the neighbours' rows;
+                                // bit-exact).  0 = auto (STRIPE_HALO_DEPTH or a size rule),
+                                // 1 = exchange every iteration (overlap / pipelined schedules)
   bool graphs = false;          // replay iterated chains from a captured hipGraph when a run()
                                 // involves no collective (single rank, or no halo exchange).
                                 // Off by default: measured on MI355X/ROCm 7, graph replay of
@@ -131,6 +136,8 @@ class Engine {
   void rewind();
   // hipGraph replays so far (tests / reporting).
   int graph_launches() const { return graph_launches_; }
+  // Iterations per halo exchange of iterated runs (1: every iteration).
+  int halo_depth() const { return depth_; }
   // Tuned band heights per pass (after autotune), for reporting.
   std::vector<int> bands() const;
 
@@ -173,6 +180,9 @@ class Engine {
   bool time_halo_ = true;  // record the halo stage events (last iteration of a run only)
   void run_pass(const Pass& p, const uint8_t* in, uint8_t* out);
   bool pipelined_ok() const;
+  int choose_depth() const;
+  void run_deep(int iterations);
+  int depth_ = 1;                  // iterations per halo exchange (deep halo)
   void run_pipelined(int iterations);
   hipStream_t s_edge_ = nullptr;   // rim + boundary rows of the pipelined halo schedule
   hipEvent_t pev_[7] = {};         // core[2], rim[2], boundary, exchange, start

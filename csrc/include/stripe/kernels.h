@@ -40,6 +40,8 @@ struct PassLaunch {
   int row0 = 0, Hg = 0;          // border geometry (global row of local 0, global H)
   int nrange = 1;                // 1 or 2 output row ranges
   int ry[4] = {0, 0, 0, 0};      // [ry0, ry1) and [ry2, ry3)
+  int ext = 0;                   // halo rows above/below the stripe that an output range may
+                                 // cover (deep-halo schedule; stencil passes only)
   const uint8_t* zero_row = nullptr;  // origin of an all-zero row (Constant y-border)
   int band = 0;                  // rows per workgroup (0 = auto)
   // Allocation view for buffer-descriptor kernels (branch-free OOB masking):

@@ -238,7 +238,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("root_buffers", &EngineConfig::root_buffers)
       .def_readwrite("autotune", &EngineConfig::autotune)
       .def_readwrite("graphs", &EngineConfig::graphs)
-      .def_readwrite("pipeline", &EngineConfig::pipeline);
+      .def_readwrite("pipeline", &EngineConfig::pipeline)
+      .def_readwrite("halo_depth", &EngineConfig::halo_depth);
 
   py::class_<PhaseTimes>(m, "PhaseTimes")
       .def_readonly("run", &PhaseTimes::run)
@@ -277,6 +278,7 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("rank", &Engine::rank)
       .def_property_readonly("world", &Engine::world)
       .def_property_readonly("out_channels", &Engine::out_channels)
+      .def_property_readonly("halo_depth", &Engine::halo_depth)
       .def_property_readonly("plan", [](const Engine& e) { return e.plan().describe(); })
       .def_property_readonly("partition", [](const Engine& e) { return e.partition().describe(); })
       .def_property_readonly("stripe", [](const Engine& e) {

@@ -62,10 +62,12 @@ class Pipeline:
     """
 
     def __init__(self, chain: str = "gaussian5", border: str = "reflect101", halo: bool = True,
-                 legacy_partition: bool = False, fuse: bool = True, overlap: bool = True):
+                 legacy_partition: bool = False, fuse: bool = True, overlap: bool = True, halo_depth: int = 0):
         self.spec = PipelineSpec(chain, border, halo, legacy_partition)
         self.fuse = fuse
         self.overlap = overlap
+        # iterations per halo exchange of iterated multi-rank runs (0 = auto, 1 = every step)
+        self.halo_depth = int(halo_depth)
         C.parse_chain(chain)  # validate early
 
     @classmethod
@@ -99,6 +101,7 @@ class Pipeline:
         cfg.device = int(device)
         cfg.backend = C.Backend.host if backend == "host" else C.Backend.device
         cfg.autotune = bool(autotune)
+        cfg.halo_depth = self.halo_depth
         sched = os.environ.get("STRIPE_HALO_SCHEDULE")  # tuning: overlap | pipeline | serial
         if sched:
             cfg.pipeline = sched == "pipeline"

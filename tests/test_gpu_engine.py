@@ -146,6 +146,27 @@ def test_pipelined_halo_schedule(m, chain, ranks, H):
         pipe = m.Pipeline(chain)
         cfg = pipe.config(203, H, 3, "device", device=0)
         cfg.pipeline = pipeline
+        cfg.halo_depth = 1  # exchange every iteration (the deep-halo schedule is tested below)
         res.append(C.run_local_group(cfg, nr, img, 4))
+    assert (res[0] == res[1]).all()
+    assert (res[0] == res[2]).all()
+
+
+@pytest.mark.parametrize("chain", ["gaussian5", "sobel", "emboss3", "gaussian7", "gray:ref,contrast:3.5,emboss5"])
+@pytest.mark.parametrize("ranks,H,depth", [(2, 96, 2), (4, 130, 3), (8, 233, 4), (3, 300, 8)])
+@pytest.mark.parametrize("iters", [1, 6, 7])
+def test_deep_halo_schedule(m, chain, ranks, H, depth, iters):
+    """Deep halo on the GPU: the stencil kernels write output rows inside the
+    halo (negative / past-the-end local rows); N ranks at depth k equal the
+    1-rank result and the per-iteration exchange bit-for-bit."""
+    C = m._C
+    W = 203
+    img = m.utils.synthetic_image(13, W, H, 3)
+    if C.plan_info(chain, 3)["cin"] != C.plan_info(chain, 3)["cout"] and iters > 1:
+        pytest.skip("chain changes the channel count: not iterable")
+    res = []
+    for d, nr in ((depth, ranks), (1, ranks), (1, 1)):
+        pipe = m.Pipeline(chain, halo_depth=d)
+        res.append(C.run_local_group(pipe.config(W, H, 3, "device", device=0), nr, img, iters))
     assert (res[0] == res[1]).all()
     assert (res[0] == res[2]).all()
