@@ -368,11 +368,21 @@ int cmd_bench(const Args& a) {
               e.run(1);
             }
           };
-          for (int i = 0; i < warmup; ++i) step();
+          // resident iterable chains ping-pong inside one run(n) call (as bench.py
+          // does), so the multi-step halo schedules (pipelined / deep) apply
+          const bool batched = scope == "resident" && iterable;
+          if (batched) {
+            if (warmup > 0) e.run(warmup);
+          } else {
+            for (int i = 0; i < warmup; ++i) step();
+          }
           e.synchronize();
           g.comms[r]->barrier();
           const double t0 = now_ms();
-          for (int i = 0; i < iters; ++i) step();
+          if (batched)
+            e.run(iters);
+          else
+            for (int i = 0; i < iters; ++i) step();
           e.synchronize();
           g.comms[r]->barrier();
           const double t1 = now_ms();
