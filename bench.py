@@ -102,39 +102,6 @@ def main():
                                       autotune=not a.no_autotune)
     row0, rows = dp.stripe
 
-    # ---- correctness (untimed): one step vs the golden path on edge crops ----
-    verify = None
-    if not a.no_verify:
-        dp.load_synthetic(a.seed)
-        dp.run(1)
-        out = dp.result_stripe()
-        ok = True
-        info = C.plan_info(a.chain, Cc)
-        R = max(1, info["max_radius"])
-        crop = max(48, 4 * R)
-        # float conv passes (blur:K, conv:K) match the f64 golden within 1 LSB (ties)
-        tol = 1 if any(p["kind"] == 3 for p in info["passes"]) else 0
-
-        def same(x, y):
-            return bool((np.abs(x.astype(np.int16) - y.astype(np.int16)) <= tol).all())
-        for lo in ([0] if row0 == 0 else []) + ([H - crop] if row0 + rows == H else []):
-            # golden on a band of full rows; rows far enough from the band edge are exact
-            band = C.synth_rows(a.seed, W, Cc, lo, crop)
-            ref = C.golden_apply(band, a.chain, "reflect101", True)
-            sel = slice(0, crop - R) if lo == 0 else slice(R, crop)
-            got = out[lo - row0:lo - row0 + crop][sel]
-            ok &= same(got, ref[sel])
-        if rows > 0 and row0 > 0 and rows >= 2 * R:
-            # interior stripe seam: the first R rows depend on the halo
-            band = C.synth_rows(a.seed, W, Cc, row0 - 2 * R, 4 * R)
-            ref = C.golden_apply(band, a.chain, "reflect101", True)
-            ok &= same(out[0:R], ref[2 * R:3 * R])
-        okt = torch.tensor([1.0 if ok else 0.0], device=tdev)
-        if world > 1:
-            dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-        verify = bool(okt.item() == 1.0)
-
-    # ---- resident scope (headline) ----
     pinfo = C.plan_info(a.chain, Cc)
     iterable = pinfo["cin"] == pinfo["cout"]
 
@@ -148,6 +115,49 @@ def main():
                 dp.engine.rewind()
                 dp.run(1)
 
+    # ---- correctness (untimed): n_it iterated steps through the same schedule
+    # as the timed loop (deep halo included) vs the golden path on edge crops
+    # and on this stripe's upper seam ----
+    verify = None
+    if not a.no_verify:
+        n_it = max(2, dp.engine.halo_depth + 1) if iterable else 1
+        dp.load_synthetic(a.seed)
+        if iterable:
+            dp.run(n_it)
+        else:
+            dp.run(1)
+        out = dp.result_stripe()
+        ok = True
+        R = max(1, pinfo["max_radius"])
+        reach = n_it * R  # rows a band-edge border error travels in n_it steps
+        crop = max(48, 4 * reach)
+        # float conv passes (blur:K, conv:K) match the f64 golden within 1 LSB (ties)
+        tol = 1 if any(p["kind"] == 3 for p in pinfo["passes"]) else 0
+
+        def gold(band):
+            for _ in range(n_it):
+                band = C.golden_apply(band, a.chain, "reflect101", True)
+            return band
+
+        def same(x, y):
+            return bool((np.abs(x.astype(np.int16) - y.astype(np.int16)) <= tol).all())
+        edges = ([0] if row0 == 0 else []) + ([H - crop] if row0 + rows == H else [])
+        for lo in [e for e in edges if row0 <= e and e + crop <= row0 + rows]:  # crops inside this stripe
+            # golden on a band of full rows; rows far enough from the band edge are exact
+            ref = gold(C.synth_rows(a.seed, W, Cc, lo, crop))
+            sel = slice(0, crop - reach) if lo == 0 else slice(reach, crop)
+            got = out[lo - row0:lo - row0 + crop][sel]
+            ok &= same(got, ref[sel])
+        if rows >= reach and row0 >= 2 * reach and row0 + 2 * reach <= H:
+            # interior stripe seam: the first rows depend on the neighbour's halo
+            ref = gold(C.synth_rows(a.seed, W, Cc, row0 - 2 * reach, 4 * reach))
+            ok &= same(out[0:reach], ref[2 * reach:3 * reach])
+        okt = torch.tensor([1.0 if ok else 0.0], device=tdev)
+        if world > 1:
+            dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        verify = bool(okt.item() == 1.0)
+
+    # ---- resident scope (headline) ----
     dp.load_synthetic(a.seed)
     if a.warmup > 0:
         run_steps(a.warmup)

@@ -100,12 +100,15 @@ def test_gloo_iterated(tmp_path, C):
     assert (out == ref).all()
 
 
-def test_bench_host_backend_two_ranks(tmp_path):
+@pytest.mark.parametrize("nproc,depth", [(2, 0), (3, 3)])
+def test_bench_host_backend_multi_rank(tmp_path, nproc, depth):
+    """bench.py under torchrun on the host engine + gloo; depth 3 runs the
+    deep-halo schedule across processes (exchange every 3 steps, 7 steps)."""
     port = _free_port()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2",
-           "--steps", "3", "--warmup", "1", "--width", "200", "--height", "96", "--backend", "host",
-           "--dist-steps", "2"]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus",
+           str(nproc), "--steps", "7" if depth else "3", "--warmup", "1", "--width", "200", "--height", "96",
+           "--backend", "host", "--dist-steps", "2", "--halo-depth", str(depth)]
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
     assert r.returncode == 0, r.stdout + r.stderr
@@ -115,5 +118,7 @@ def test_bench_host_backend_two_ranks(tmp_path):
     for k in ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
               "vs_baseline", "dtype", "data", "config"]:
         assert k in rec
-    assert rec["n_gpus"] == 2 and rec["steps"] == 3 and rec["value"] > 0
+    assert rec["n_gpus"] == nproc and rec["steps"] == (7 if depth else 3) and rec["value"] > 0
     assert rec["verified_vs_golden"] is True
+    if depth:
+        assert rec["halo_depth"] == depth
