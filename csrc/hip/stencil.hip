@@ -210,6 +210,17 @@ struct SepTraits {
   }
   // horizontal sums (+ rounding) fit 16 bits and the division is a shift
   static constexpr bool H16 = log2div() >= 0 && gsum() * gsum() * 255 + F::DIV / 2 < 65536;
+  // binomial H16 filters: the rounding term DIV/2 rides on the vertical sums
+  // (+DIV/2/gsum on each, summed gsum times by the horizontal taps), added by
+  // the cascade's last stage as a third operand (v_add3_u32: the packed u16
+  // fields never carry, every partial sum is < 2^16)
+  static constexpr bool FOLD = H16 && F::BINOM && (F::DIV / 2) % gsum() == 0;
+  static constexpr uint32_t kFold = FOLD ? (uint32_t)(F::DIV / 2 / gsum()) * 0x00010001u : 0u;
+  static constexpr bool SYM = [] {
+    for (int i = 0; i < F::K; ++i)
+      if (F::g(i) != F::g(F::K - 1 - i)) return false;
+    return true;
+  }();
 };
 
 // u16 pair (v[k], v[k+1]) of the window (k: u16 index, compile-time after unroll)
@@ -246,13 +257,17 @@ template <class F>
 __device__ __forceinline__ void vpush(const uint32_t (&row)[8], const VState<F>& prev, VState<F>& next,
                                       uint32_t (&v)[8]) {
   if constexpr (F::BINOM) {
+    constexpr uint32_t kf = SepTraits<F>::kFold;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       uint32_t cur = row[k];
 #pragma unroll
       for (int st = 0; st < F::K - 1; ++st) {
         next.s[st][k] = cur;
-        cur = as_u32(as_u16x2(cur) + as_u16x2(prev.s[st][k]));
+        if (kf != 0 && st == F::K - 2)  // fields stay < 2^16: no carry between them
+          asm("v_add3_u32 %0, %1, %2, %3" : "=v"(cur) : "v"(cur), "v"(prev.s[st][k]), "s"(kf));
+        else
+          cur = as_u32(as_u16x2(cur) + as_u16x2(prev.s[st][k]));
       }
       v[k] = cur;
     }
@@ -391,10 +406,34 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : 4)) void k_sep(KArgs a) {
       uint32_t h[8];
 #pragma unroll
       for (int pp = 0; pp < 8; ++pp) {
-        u16x2 sacc = (u16x2)(unsigned short)(F::DIV / 2);
+        u16x2 sacc;
+        if constexpr (T::SYM && F::g(0) == 1) {
+          // mirrored taps share a weight: (x[-i] + x[+i]) * g, outermost pair
+          // (weight 1) first, centre last: 2R ops per output pair.  Plain u32
+          // arithmetic on the packed pair is exact (H16: every partial sum and
+          // product is < 2^16, so nothing crosses into the high field), which
+          // turns power-of-two weights into one v_lshl_add_u32.
+          auto madd = [](uint32_t s, uint32_t acc, int g) __attribute__((always_inline)) {
+            if ((g & (g - 1)) == 0) {
+              int k = 0;
+              while ((1 << k) < g) ++k;
+              return (s << k) + acc;
+            }
+            return as_u32(as_u16x2(s) * (unsigned short)g + as_u16x2(acc));
+          };
+          uint32_t acc = pair_at(w, WLO + 2 * pp - R * C) + pair_at(w, WLO + 2 * pp + R * C);
 #pragma unroll
-        for (int i = 0; i < K; ++i)
-          sacc += as_u16x2(pair_at(w, WLO + 2 * pp + (i - R) * C)) * (unsigned short)F::g(i);
+          for (int i = 1; i < R; ++i)
+            acc = madd(pair_at(w, WLO + 2 * pp + (i - R) * C) + pair_at(w, WLO + 2 * pp + (R - i) * C), acc, F::g(i));
+          acc = madd(pair_at(w, WLO + 2 * pp), acc, F::g(R));
+          sacc = as_u16x2(acc);
+          if constexpr (!T::FOLD) sacc += (u16x2)(unsigned short)(F::DIV / 2);
+        } else {
+          sacc = (u16x2)(unsigned short)(F::DIV / 2);
+#pragma unroll
+          for (int i = 0; i < K; ++i)
+            sacc += as_u16x2(pair_at(w, WLO + 2 * pp + (i - R) * C)) * (unsigned short)F::g(i);
+        }
         if constexpr (T::log2div() != 8) sacc = sacc >> (unsigned short)T::log2div();
         h[pp] = as_u32(sacc);
       }
