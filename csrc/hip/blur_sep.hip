@@ -80,13 +80,14 @@ __device__ __forceinline__ void split_h2(float x, float y, uint32_t& hi, uint32_
   lo = __builtin_bit_cast(uint32_t, l);
 }
 
-// 4 f32 -> 4 saturated, round-half-even u8 in one dword: v_cvt_pk_u8_f32 rounds
-// in the MODE rounding mode (nearest-even by default); the clamp makes the
-// saturation explicit.  (Measured equal to the add-1.5*2^23 + byte-gather form.)
+// 4 f32 -> 4 saturated, round-half-even u8 in one dword: v_cvt_pk_u8_f32
+// rounds in the MODE rounding mode (nearest-even by default) and saturates to
+// [0, 255] itself (tools/cvt_probe.hip on gfx950: -5 -> 0, 2.5 -> 2, 256 -> 255,
+// 1e9 -> 255), so no clamp instruction is needed.
 __device__ __forceinline__ uint32_t pack_u8x4(f4 v) {
   uint32_t o = 0;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) o = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(v[r], 0.f, 255.f), r, o);
+  for (int r = 0; r < 4; ++r) o = __builtin_amdgcn_cvt_pk_u8_f32(v[r], r, o);
   return o;
 }
 
@@ -176,6 +177,11 @@ __global__ __launch_bounds__(kSepWaves * 64, 2) void k_blur_sep(SepArgs sa) {
   };
 
   const int xo = sx + 4 * g;  // first output byte of the lane's dword (+16 j)
+  // column tiles past the row end (last strip only): their stores get the
+  // range-check-failing bit (offsets stay < 2^31 - 2^16, checked on the host)
+  uint32_t colbad[kSepNJ];
+#pragma unroll
+  for (int j = 0; j < kSepNJ; ++j) colbad[j] = xo + 16 * j < a.E ? 0u : kOOB;
 
   f4 acc[2][kSepNJ];  // running vertical sums of the current output group
   // One 32-row X pair: FIN = it is k-step 1 of group k - 1 (finish + store),
@@ -195,6 +201,16 @@ __global__ __launch_bounds__(kSepWaves * 64, 2) void k_blur_sep(SepArgs sa) {
     sep_lds_sync();
     if (START) prefetch(k + 1);  // pair k + 1 exists iff group k does
     const int yg = base + 32 * (k - 1);  // first row of the group being finished
+    // per output-row-half byte offset of (row, xo), or kOOB for rows outside
+    // [ys, ye): one v_or per store instead of a predicate + exec mask
+    uint32_t rowoff[2];
+    if constexpr (FIN) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int y = yg + 16 * q + m;
+        rowoff[q] = (y >= ys && y < ye) ? a.out_org + (uint32_t)((int64_t)y * a.out_pitch) + (uint32_t)xo : kOOB;
+      }
+    }
 #pragma unroll
     for (int j = 0; j < kSepNJ; ++j) {
       // horizontal: X tiles 2k (rows 0..15 of the pair) and 2k+1 (16..31), column j
@@ -224,11 +240,7 @@ __global__ __launch_bounds__(kSepWaves * 64, 2) void k_blur_sep(SepArgs sa) {
           o4 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bv[q][1][1], o4, 0, 0, 0);
           o4 = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bv[q][1][0], o4, 0, 0, 0);
           const uint32_t o = pack_u8x4(o4);
-          const int y = yg + 16 * q + m;
-          const int x = xo + 16 * j;
-          const uint32_t off =
-              (y >= ys && y < ye && x < a.E) ? a.out_org + (uint32_t)((int64_t)y * a.out_pitch) + (uint32_t)x : kOOB;
-          __builtin_amdgcn_raw_buffer_store_b32(o, rout, off, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(o, rout, (rowoff[q] | colbad[j]) + 16 * j, 0, 0);
         }
         if constexpr (START) {
           f4 n4 = {0.f, 0.f, 0.f, 0.f};
@@ -309,19 +321,16 @@ void prepare_sep_consts(const Pass& p, PassConsts* pc, hipStream_t s) {
   HIP_CHECK(hipStreamSynchronize(s));
 }
 
-// Waves of k_blur_sep resident at once on the current device (occupancy x CUs).
-static int64_t resident_waves() {
+// SIMDs of the current device (CUs x 4), cached per device.
+static int64_t resident_simds() {
   static thread_local int cached_dev = -1;
   static thread_local int64_t cached = 0;
   int dev = 0;
   HIP_CHECK(hipGetDevice(&dev));
   if (dev != cached_dev) {
-    int blocks = 0, cus = 0;
-    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, (const void*)dev::k_blur_sep<4>,
-                                                           dev::kSepWaves * 64,
-                                                           (size_t)dev::kSepWaves * dev::kSepTile));
+    int cus = 0;
     HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    cached = (int64_t)std::max(1, blocks) * cus * dev::kSepWaves;
+    cached = (int64_t)std::max(1, cus) * 4;
     cached_dev = dev;
   }
   return cached;
@@ -331,8 +340,8 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
   STRIPE_CHECK(pc.conv != nullptr, "blur pass constants not prepared");
   STRIPE_CHECK(L.in_base && L.out_base, "blur launch needs the allocation view (in_base/out_base)");
   STRIPE_CHECK(L.in_bytes > 0 && L.in_bytes < (int64_t)dev::kOOB && L.out_bytes > 0 &&
-                   L.out_bytes < (int64_t)dev::kOOB,
-               "stripe buffers must be < 2 GiB for buffer-descriptor addressing");
+                   L.out_bytes < (int64_t)dev::kOOB - 65536,
+               "stripe buffers must be < 2 GiB - 64 KiB for buffer-descriptor addressing");
   STRIPE_CHECK(L.in_org >= kMarginBytes && L.out_org >= kMarginBytes && L.in_zero >= kMarginBytes,
                "bad origin offsets");
   dev::SepArgs sa{};
@@ -369,11 +378,23 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
     a.ry1 = L.ry[0] + n0;
     a.ry2 = n1 ? L.ry[2] : 0;
     a.ry3 = n1 ? L.ry[3] : 0;
-    // band: 256 rows by default (the 32 warm-up rows of a band cost 12 %),
-    // shorter when that would leave resident wave slots idle; L.band (rows,
-    // >= 32) overrides for tuning
-    const int64_t groups = div_up(n0, 32) + div_up(n1, 32);
-    int64_t gpb = std::min<int64_t>(8, std::max<int64_t>(1, div_up(groups * sa.nstrips, resident_waves())));
+    // band = gpb 32-row groups.  A task costs gpb + 1 pair steps (one warm-up
+    // pair per band).  A SIMD's resident waves share its MFMA and VALU pipes,
+    // so the kernel takes about ceil(tasks / SIMDs) x (gpb + 1) pair times
+    // (measured: a 16384x2048 RGB stripe at 8 groups = 3 tasks per SIMD x 9,
+    // 0.090 ms; at 13 groups = 2 x 14, 0.0975 ms): pick gpb minimising that.
+    // L.band (rows, >= 32) overrides for tuning.
+    const int64_t g0 = div_up(n0 + 31, 32), g1 = n1 ? div_up(n1 + 31, 32) : 0;  // groups incl. grid offset
+    const int64_t simds = resident_simds();
+    int64_t gpb = 1, best = -1;
+    for (int64_t c = 1; c <= 16; ++c) {
+      const int64_t tasks = (int64_t)sa.nstrips * (div_up(g0, c) + div_up(g1, c));
+      const int64_t cost = div_up(tasks, simds) * (c + 1);
+      if (best < 0 || cost < best) {
+        best = cost;
+        gpb = c;
+      }
+    }
     if (L.band >= 32) gpb = L.band / 32;
     const int band = (int)(32 * gpb);
 
