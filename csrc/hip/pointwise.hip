@@ -7,6 +7,8 @@
 // per-channel truncation, kernel.cu:40-42, is reproduced with verified
 // multiply-shift constants).  Margins are processed like pixels, so the output
 // keeps the x-border contract of the next stencil.
+#include <cstdlib>
+
 #include "dev_common.h"
 #include "stripe/image.h"
 #include "stripe/kernels.h"
@@ -14,7 +16,7 @@
 namespace stripe {
 namespace dev {
 
-template <int CIN, int COUT, bool GRAY>
+template <int CIN, int COUT, bool GRAY, bool NT>
 __global__ __launch_bounds__(kNT) void k_pointwise(KArgs a, int ngroups, int g0) {
   __shared__ uint8_t lut[512];
   for (int i = threadIdx.x; i < 512; i += kNT) lut[i] = a.luts[i];
@@ -101,8 +103,12 @@ __global__ __launch_bounds__(kNT) void k_pointwise(KArgs a, int ngroups, int g0)
     }
   }
 #pragma unroll
-  for (int q = 0; q < COUT; ++q)
-    reinterpret_cast<uint4*>(dst)[q] = make_uint4(out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]);
+  for (int q = 0; q < COUT; ++q) {
+    typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+    const u32x4v v = {out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]};
+    if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4v*>(dst) + q);
+    else reinterpret_cast<u32x4v*>(dst)[q] = v;
+  }
 }
 
 // Margin fill: margin byte (m, c) of row y <- pixel border_index(m) of the same row.
@@ -191,22 +197,36 @@ void launch_pointwise(const Pass& p, const PassConsts& pc, const PassLaunch& L, 
   const int px = std::min(p.out_margin_px, kMaxRadius);
   const int g0 = px > 0 ? -1 : 0;  // one 16-pixel group of left margin
   const int ngroups = (int)div_up(L.W + px, 16) - g0;
+  const int n0_rows = std::max(0, L.ry[1] - L.ry[0]);
+  const int n1_rows = L.nrange > 1 ? std::max(0, L.ry[3] - L.ry[2]) : 0;
   for (int r = 0; r < L.nrange; ++r) {
     const int y0 = L.ry[2 * r], y1 = L.ry[2 * r + 1];
     if (y1 <= y0) continue;
     a.ry0 = y0;
     dim3 grid((unsigned)div_up(ngroups, dev::kNT), (unsigned)(y1 - y0));
     const bool gray = p.pro.gray;
+    // nt stores when the pass streams more than the Infinity Cache (as the
+    // stencil kernels; a smaller set is read back from the cache by the next
+    // pass) and only for 1-channel output, where one store instruction covers
+    // 1 KiB contiguously: the 3-channel store pattern (16 B per lane at a 48 B
+    // stride) writes partial lines that nt sends to HBM unmerged (16K RGB
+    // invert 0.295 -> 0.322 ms with nt; 16K gray:ref 0.192 -> 0.184 ms)
+    bool nt = p.cout == 1 && (int64_t)(n0_rows + n1_rows) * L.W * (p.cin + p.cout) > dev::kNtMinBytes;
+    if (const char* e = std::getenv("STRIPE_NT")) nt = std::atoi(e) != 0;
+    auto go = [&](auto k_nt, auto k_t) {
+      if (nt) k_nt<<<grid, dev::kNT, 0, s>>>(a, ngroups, g0);
+      else k_t<<<grid, dev::kNT, 0, s>>>(a, ngroups, g0);
+    };
     if (p.cin == 3 && p.cout == 3 && !gray)
-      dev::k_pointwise<3, 3, false><<<grid, dev::kNT, 0, s>>>(a, ngroups, g0);
+      go(dev::k_pointwise<3, 3, false, true>, dev::k_pointwise<3, 3, false, false>);
     else if (p.cin == 1 && p.cout == 1 && !gray)
-      dev::k_pointwise<1, 1, false><<<grid, dev::kNT, 0, s>>>(a, ngroups, g0);
+      go(dev::k_pointwise<1, 1, false, true>, dev::k_pointwise<1, 1, false, false>);
     else if (p.cin == 3 && p.cout == 1 && gray)
-      dev::k_pointwise<3, 1, true><<<grid, dev::kNT, 0, s>>>(a, ngroups, g0);
+      go(dev::k_pointwise<3, 1, true, true>, dev::k_pointwise<3, 1, true, false>);
     else if (p.cin == 3 && p.cout == 3 && gray)
-      dev::k_pointwise<3, 3, true><<<grid, dev::kNT, 0, s>>>(a, ngroups, g0);
+      go(dev::k_pointwise<3, 3, true, true>, dev::k_pointwise<3, 3, true, false>);
     else if (p.cin == 1 && p.cout == 3 && !gray)
-      dev::k_pointwise<1, 3, false><<<grid, dev::kNT, 0, s>>>(a, ngroups, g0);
+      go(dev::k_pointwise<1, 3, false, true>, dev::k_pointwise<1, 3, false, false>);
     else
       fail("pointwise: unsupported channel combination " + std::to_string(p.cin) + "->" + std::to_string(p.cout));
     HIP_CHECK(hipGetLastError());
