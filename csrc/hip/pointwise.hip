@@ -111,6 +111,51 @@ __global__ __launch_bounds__(kNT) void k_pointwise(KArgs a, int ngroups, int g0)
   }
 }
 
+// Channel-preserving byte-wise pass (LUT / invert / brightness / contrast on 1
+// or 3 channels): the row is a flat byte stream, 16 contiguous bytes per lane,
+// so every load/store instruction covers 1 KiB contiguously (the per-pixel
+// form above moves 48-byte RGB groups at a 48-byte lane stride) and nt stores
+// write whole lines.  Group g covers row bytes [16 (g + g0), +16).
+constexpr int kFlatU = 4;  // 16-byte groups per lane (k_pointwise_flat)
+
+template <bool NT>
+__global__ __launch_bounds__(kNT) void k_pointwise_flat(KArgs a, int ngroups, int g0, int C) {
+  __shared__ uint8_t lut[512];
+  for (int i = threadIdx.x; i < 512; i += kNT) lut[i] = a.luts[i];
+  const int y = a.ry0 + blockIdx.y;
+  const uint8_t* srow = a.in + (int64_t)y * a.in_pitch;
+  uint8_t* drow = a.out + (int64_t)y * a.out_pitch;
+  // kFlatU groups per lane, kNT apart: the loads are issued before the LUT
+  // barrier, so one LUT fill per workgroup is amortised over 4 KiB per wave
+  typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+  u32x4v v[kFlatU];
+#pragma unroll
+  for (int u = 0; u < kFlatU; ++u) {
+    const int g = (blockIdx.x * kFlatU + u) * kNT + threadIdx.x;
+    if (g < ngroups) v[u] = *reinterpret_cast<const u32x4v*>(srow + (g + g0) * 16);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < kFlatU; ++u) {
+    const int g = (blockIdx.x * kFlatU + u) * kNT + threadIdx.x;
+    if (g >= ngroups) break;
+    const int b0 = (g + g0) * 16;  // first byte (negative: left margin)
+    uint32_t t[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+    if (a.has_pre) lut16(lut, t);
+    if (a.has_post) lut16(lut + 256, t);
+    if (a.out_border == (int)Border::Constant && (b0 < 0 || b0 + 16 > a.W * C)) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int bb = b0 + i;
+        if (bb < 0 || bb >= a.W * C) t[i >> 2] &= ~(0xFFu << (8 * (i & 3)));
+      }
+    }
+    const u32x4v o = {t[0], t[1], t[2], t[3]};
+    if constexpr (NT) __builtin_nontemporal_store(o, reinterpret_cast<u32x4v*>(drow + b0));
+    else *reinterpret_cast<u32x4v*>(drow + b0) = o;
+  }
+}
+
 // Margin fill: margin byte (m, c) of row y <- pixel border_index(m) of the same row.
 __global__ __launch_bounds__(kNT) void k_fill_margins(uint8_t* origin, int64_t pitch, int W, int C, int y0,
                                                       int px, int border) {
@@ -217,11 +262,17 @@ void launch_pointwise(const Pass& p, const PassConsts& pc, const PassLaunch& L, 
       if (nt) k_nt<<<grid, dev::kNT, 0, s>>>(a, ngroups, g0);
       else k_t<<<grid, dev::kNT, 0, s>>>(a, ngroups, g0);
     };
-    if (p.cin == 3 && p.cout == 3 && !gray)
-      go(dev::k_pointwise<3, 3, false, true>, dev::k_pointwise<3, 3, false, false>);
-    else if (p.cin == 1 && p.cout == 1 && !gray)
-      go(dev::k_pointwise<1, 1, false, true>, dev::k_pointwise<1, 1, false, false>);
-    else if (p.cin == 3 && p.cout == 1 && gray)
+    if (p.cin == p.cout && !gray) {
+      // byte-wise: flat 16-byte groups from the left margin to the right one
+      const int C = p.cin;
+      const int gb0 = -(int)div_up(px * C, 16);
+      const int ngb = (int)div_up((L.W + px) * C, 16) - gb0;
+      const bool ntf = (int64_t)(n0_rows + n1_rows) * L.W * 2 * C > dev::kNtMinBytes &&
+                       !(std::getenv("STRIPE_NT") && std::atoi(std::getenv("STRIPE_NT")) == 0);
+      const dim3 gridf((unsigned)div_up(ngb, dev::kNT * dev::kFlatU), (unsigned)(y1 - y0));
+      if (ntf) dev::k_pointwise_flat<true><<<gridf, dev::kNT, 0, s>>>(a, ngb, gb0, C);
+      else dev::k_pointwise_flat<false><<<gridf, dev::kNT, 0, s>>>(a, ngb, gb0, C);
+    } else if (p.cin == 3 && p.cout == 1 && gray)
       go(dev::k_pointwise<3, 1, true, true>, dev::k_pointwise<3, 1, true, false>);
     else if (p.cin == 3 && p.cout == 3 && gray)
       go(dev::k_pointwise<3, 3, true, true>, dev::k_pointwise<3, 3, true, false>);
