@@ -626,10 +626,27 @@ void Engine::run_deep(int iterations) {
   if (rows == 0) return;
   const bool up = rank_ > 0, down = rank_ + 1 < part_.active;
   const PassConsts& pc = prt_[0].pc;
+  // the block's exchange flies on the comm stream beside the first iteration's
+  // interior rows [R, rows - R), which read only the rank's own rows; the
+  // boundary rows of that iteration follow once the halo has landed (two
+  // cross-stream waits per block instead of per step)
+  static const bool env_overlap = [] {
+    const char* e = std::getenv("STRIPE_DEEP_OVERLAP");
+    return !e || std::atoi(e) != 0;
+  }();
+  const bool overlap = device() && cfg_.overlap && env_overlap && rows > 2 * R;
+  const int iy0 = up ? R : 0, iy1 = down ? rows - R : rows;  // rows needing no halo
   for (int done = 0; done < iterations;) {
     const int m = std::min(depth_, iterations - done);
     time_halo_ = done + m >= iterations;  // stage events of the last exchange only
-    exchange_halo(origin(buf_[cur_], p.cin), p.cin, m * R, s_compute_);
+    if (overlap) {
+      HIP_CHECK(hipEventRecord(ev_[4], s_compute_));
+      HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_[4], 0));
+      exchange_halo(origin(buf_[cur_], p.cin), p.cin, m * R, s_comm_);
+      HIP_CHECK(hipEventRecord(ev_[5], s_comm_));
+    } else {
+      exchange_halo(origin(buf_[cur_], p.cin), p.cin, m * R, s_compute_);
+    }
     for (int i = 0; i < m; ++i) {
       const int ext = (m - 1 - i) * R;
       const int y0 = up ? -ext : 0, y1 = rows + (down ? ext : 0);
@@ -637,10 +654,23 @@ void Engine::run_deep(int iterations) {
       uint8_t* out = origin(buf_[cur_ ^ 1], p.cout);
       if (device()) {
         PassLaunch L = make_launch(p, in, out, 0);
-        L.nrange = 1;
-        L.ry[0] = y0;
-        L.ry[1] = y1;
         L.ext = ext;
+        if (overlap && i == 0) {
+          L.nrange = 1;
+          L.ry[0] = iy0;
+          L.ry[1] = iy1;
+          launch_pass(p, pc, L, s_compute_);
+          HIP_CHECK(hipStreamWaitEvent(s_compute_, ev_[5], 0));
+          L.nrange = 2;
+          L.ry[0] = y0;
+          L.ry[1] = iy0;
+          L.ry[2] = iy1;
+          L.ry[3] = y1;
+        } else {
+          L.nrange = 1;
+          L.ry[0] = y0;
+          L.ry[1] = y1;
+        }
         launch_pass(p, pc, L, s_compute_);
       } else {
         golden_pass(p, ConstView{in, pitch(p.cin)}, MutView{out, pitch(p.cout)}, cfg_.W, geom(), y0, y1);
