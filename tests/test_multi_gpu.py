@@ -1,0 +1,52 @@
+"""Real multi-GPU runs (one process per GPU over RCCL), skipped on 1-GPU boxes.
+
+bench.py under torchrun on N = 2 (and 4 when present) GPUs: the iterated
+deep-halo schedule and the dist scope must verify against the golden path on
+the stripe seams.  The CPU (gloo) and single-GPU (local ranks) suites cover
+the same partition/halo logic; this checks the RCCL transport itself.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _ngpus() -> int:
+    try:
+        return torch.cuda.device_count()  # does not initialise the GPU
+    except Exception:
+        return 0
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("n", [2, 4])
+@pytest.mark.parametrize("chain,depth", [("gaussian5", 0), ("gaussian5", 1), ("sobel", 0), ("blur:9", 0)])
+def test_torchrun_bench_rccl(n, chain, depth):
+    if _ngpus() < n:
+        pytest.skip(f"needs {n} GPUs")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", str(n), "--steps", "9", "--warmup", "2", "--width", "2048", "--height", "1024",
+           "--chain", chain, "--halo-depth", str(depth), "--dist-steps", "2", "--e2e-steps", "1"]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == n and rec["value"] > 0
+    assert rec["verified_vs_golden"] is True
