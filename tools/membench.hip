@@ -119,6 +119,41 @@ __global__ __launch_bounds__(256) void k_tile2(const uint8_t* in, uint8_t* out, 
   }
 }
 
+
+// tile pattern with NC 16-byte chunks per lane (wave row segment = NC KiB,
+// contiguous), P rows in flight, nt stores
+template <int NC, int P>
+__global__ __launch_bounds__(256) void k_tilew(const uint8_t* in, uint8_t* out, long pitch, int tiles, int rows,
+                                               int band, unsigned bytes) {
+  const int lane = threadIdx.x & 63;
+  const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int xt = w % tiles, bt = w / tiles;
+  const int ys = bt * band;
+  if (ys >= rows) return;
+  const int ye = min(ys + band, rows);
+  const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(in), 0, (int)bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)bytes, 0x00020000);
+  const unsigned x = (unsigned)(xt * 1024 * NC + lane * 16);
+  u32x4 nx[P][NC];
+#pragma unroll
+  for (int i = 0; i < P; ++i)
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+      nx[i][c] = __builtin_amdgcn_raw_buffer_load_b128(rin, (unsigned)((ys + i < ye ? ys + i : ye - 1) * pitch) + x + 1024 * c, 0, 0);
+  for (int y = ys; y < ye; y += P) {
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+      const int yl = y + i + P;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const u32x4 v = nx[i][c];
+        nx[i][c] = __builtin_amdgcn_raw_buffer_load_b128(rin, (unsigned)((yl < ye ? yl : ye - 1) * pitch) + x + 1024 * c, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rout, y + i < ye ? (unsigned)((y + i) * pitch) + x + 1024 * c : 0x80000000u, 0, 2);
+      }
+    }
+  }
+}
+
 struct Timer {
   hipEvent_t a, b;
   Timer() {
@@ -210,6 +245,19 @@ int main(int argc, char** argv) {
   TILE2(4, 0, 0, 8, 2, 0)
   TILE2(4, 4, 0, 16, 2, 2)
   TILE2(4, 4, 0, 32, 2, 2)
+#define TILEW(NC, P, BAND)                                                                               \
+  std::snprintf(nm, sizeof nm, "tilew NC=%d P=%d band=%d nt", NC, P, BAND);                              \
+  run(nm, [&](uint8_t* a, uint8_t* b) {                                                                  \
+    const int nb = (rows + (BAND)-1) / (BAND);                                                           \
+    const int tw = tiles / NC;                                                                           \
+    k_tilew<NC, P><<<(unsigned)((tw * nb + 3) / 4), 256>>>(a, b, pitch, tw, rows, BAND, ub);             \
+  });
+  TILEW(1, 4, 8)
+  TILEW(2, 4, 8)
+  TILEW(2, 2, 8)
+  TILEW(4, 2, 8)
+  TILEW(4, 2, 16)
+  TILEW(2, 4, 16)
   CK(hipMemcpyAsync(y, x, bytes, hipMemcpyDeviceToDevice, 0));
   run("hipMemcpyAsync D2D", [&](uint8_t* a, uint8_t* b) { CK(hipMemcpyAsync(b, a, bytes, hipMemcpyDeviceToDevice, 0)); });
   return 0;
