@@ -69,7 +69,10 @@ __device__ __forceinline__ WaveTask wave_task(const KArgs& a) {
   return t;
 }
 
-enum { PRO_NONE = 0, PRO_LUT = 1, PRO_GRAY = 2 };
+enum { PRO_NONE = 0, PRO_LUT = 1, PRO_GRAY = 2, PRO_GRAYLUT = 3 };
+// PRO_GRAY: arithmetic gray (bt601 fixed point); PRO_GRAYLUT: gray:ref as three
+// per-channel table lookups (see cook_pairs).  Both read 48 RGB bytes per lane.
+constexpr bool is_gray(int pro) { return pro == PRO_GRAY || pro == PRO_GRAYLUT; }
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
@@ -88,13 +91,13 @@ __device__ __forceinline__ uint32_t as_u32(i16x2 x) { return __builtin_bit_cast(
 // the load site forces an s_waitcnt there).
 template <int PRO>
 struct RawChunk {
-  uint32_t d[PRO == PRO_GRAY ? 12 : 4];
+  uint32_t d[is_gray(PRO) ? 12 : 4];
 };
 
 template <int PRO>
 __device__ __forceinline__ void load_raw(__amdgpu_buffer_rsrc_t rin, uint32_t row_off, uint32_t lane_off,
                                          RawChunk<PRO>& r) {
-  if constexpr (PRO == PRO_GRAY) {
+  if constexpr (is_gray(PRO)) {
     const uint32_t off = row_off + lane_off;  // lane_off already scaled by 3
     const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(rin, off, 0, kLoadAux);
     const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(rin, off + 16, 0, kLoadAux);
@@ -108,11 +111,45 @@ __device__ __forceinline__ void load_raw(__amdgpu_buffer_rsrc_t rin, uint32_t ro
   }
 }
 
+// gray:ref (kernel.cu:40-42: per-channel truncated products, summed) as three
+// 256-entry LDS tables per pixel (luts + 768: R, G, B terms, built on the host
+// from the exact multiply-shift constants); the sum (<= 254) and the optional
+// post LUT land straight in the u16 fields the stencil arithmetic uses, so
+// there is no byte packing / unpacking.  ~9 VALU + 6-8 conflict-free LDS reads
+// per pixel pair instead of ~24 VALU for the arithmetic form.
+template <int N>
+__device__ __forceinline__ uint32_t byte_at(const uint32_t (&d)[N], int j) {
+  return (d[j >> 2] >> ((j & 3) * 8)) & 0xFFu;
+}
+
+__device__ __forceinline__ void gray_ref_pairs(const KArgs& a, const uint32_t (&d)[12], const uint8_t* luts,
+                                               uint32_t (&u)[8]) {
+  const uint8_t* tr = luts + 768;
+  const uint8_t* tg = luts + 1024;
+  const uint8_t* tb = luts + 1280;
+#pragma unroll
+  for (int pp = 0; pp < 8; ++pp) {
+    uint32_t g2[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int b0 = 3 * (2 * pp + h);
+      g2[h] = (uint32_t)tr[byte_at(d, b0)] + (uint32_t)tg[byte_at(d, b0 + 1)] + (uint32_t)tb[byte_at(d, b0 + 2)];
+      if (a.has_post) g2[h] = luts[256 + g2[h]];
+    }
+    u[pp] = g2[0] | (g2[1] << 16);
+  }
+}
+
 // Prologue: the 16 output-channel bytes of a raw chunk.
 template <int PRO>
 __device__ __forceinline__ void cook(const KArgs& a, const RawChunk<PRO>& r, const uint8_t* lut_post,
                                      uint32_t (&o)[4]) {
-  if constexpr (PRO == PRO_GRAY) {
+  if constexpr (PRO == PRO_GRAYLUT) {
+    uint32_t u[8];
+    gray_ref_pairs(a, r.d, lut_post - 256, u);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = __builtin_amdgcn_perm(u[2 * q + 1], u[2 * q], 0x06040200u);
+  } else if constexpr (PRO == PRO_GRAY) {
     gray16(a, r.d, o);
     if (a.has_post) lut16(lut_post, o);
   } else {
@@ -131,8 +168,9 @@ __device__ __forceinline__ void load_chunk(const KArgs& a, __amdgpu_buffer_rsrc_
   cook<PRO>(a, r, lut_post, o);
 }
 
+template <int PRO>
 __device__ __forceinline__ void load_luts(const KArgs& a, uint8_t* lds) {
-  for (int i = threadIdx.x; i < 768; i += kNT) lds[i] = a.luts[i];
+  for (int i = threadIdx.x; i < (PRO == PRO_GRAYLUT ? kLutBytes : 768); i += kNT) lds[i] = a.luts[i];
 }
 
 // Legacy skip border (kernel.cu:83 interior-only bounds): bytes of pixels in the
@@ -193,6 +231,19 @@ __device__ __forceinline__ void unpack16(const uint32_t (&r)[4], uint32_t (&p)[8
   for (int d = 0; d < 4; ++d) {
     p[2 * d] = __builtin_amdgcn_perm(0u, r[d], 0x0c010c00u);      // (b0, b1)
     p[2 * d + 1] = __builtin_amdgcn_perm(0u, r[d], 0x0c030c02u);  // (b2, b3)
+  }
+}
+
+// Prologue straight to the unpacked u16-pair form of the stencil arithmetic.
+template <int PRO>
+__device__ __forceinline__ void cook_pairs(const KArgs& a, const RawChunk<PRO>& r, const uint8_t* luts,
+                                           uint32_t (&u)[8]) {
+  if constexpr (PRO == PRO_GRAYLUT) {
+    gray_ref_pairs(a, r.d, luts, u);
+  } else {
+    uint32_t c[4];
+    cook<PRO>(a, r, luts + 256, c);
+    unpack16(c, u);
   }
 }
 
@@ -290,16 +341,16 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : 4)) void k_sep(KArgs a) {
   constexpr int R = F::R, K = F::K;
   constexpr int WLO = (R * C <= 8) ? 8 : 16;  // u16 window start (relative to chunk)
   constexpr int WDW = (2 * WLO + 16) / 2;     // window dwords
-  constexpr int CIN = PRO == PRO_GRAY ? 3 : 1;  // input bytes per output byte
+  constexpr int CIN = is_gray(PRO) ? 3 : 1;  // input bytes per output byte
   using T = SepTraits<F>;
   // per wave: one row of vertical sums, planar (plane h = dwords 4h..4h+3 of a
   // lane's 8) so every ds_write_b128 / ds_read_b128 has a 16-byte lane stride
   // (sobel: planes 2..3 hold the difference row)
   constexpr int NP = F::SOBEL ? 4 : 2;
   __shared__ __attribute__((aligned(16))) uint4 vbuf[kWaves][NP][kW];
-  __shared__ uint8_t luts[768];
+  __shared__ uint8_t luts[PRO == PRO_GRAYLUT ? kLutBytes : 768];
   if (PRO != PRO_NONE || a.has_epi) {
-    load_luts(a, luts);
+    load_luts<PRO>(a, luts);
     __syncthreads();
   }
   const WaveTask t = wave_task(a);
@@ -324,9 +375,10 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : 4)) void k_sep(KArgs a) {
   uint32_t vdummy[8];
 #pragma unroll
   for (int i = 0; i < K - 1; ++i) {  // prime with rows ys-R .. ys+R-1
-    uint32_t r[4], u[8];
-    load_chunk<PRO>(a, rin, in_row_off(a, ys - R + i), lane_in, luts + 256, r);
-    unpack16(r, u);
+    uint32_t u[8];
+    RawChunk<PRO> rr;
+    load_raw<PRO>(rin, in_row_off(a, ys - R + i), lane_in, rr);
+    cook_pairs<PRO>(a, rr, luts, u);
     if constexpr (F::SOBEL) {
       if (i & 1) vpush_sobel<F>(u, sb, sa, vdummy, vdummy);
       else vpush_sobel<F>(u, sa, sb, vdummy, vdummy);
@@ -340,15 +392,14 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : 4)) void k_sep(KArgs a) {
   // (unconditional: no branch around the load)
   // (a gray prologue reads 48 bytes per row: 2 rows give more bytes in flight
   // than 4 plain rows, at 24 fewer registers)
-  constexpr int kPF = PRO == PRO_GRAY ? 2 : 4;
+  constexpr int kPF = is_gray(PRO) ? 2 : 4;
   RawChunk<PRO> nx[kPF];
 #pragma unroll
   for (int i = 0; i < kPF; ++i) load_raw<PRO>(rin, ys + i < ye ? in_row_off(a, ys + i + R) : last_row, lane_in, nx[i]);
 
   auto row_step = [&](int y, const VState<F>& prev, VState<F>& next, RawChunk<PRO>& nb, bool valid) {
-    uint32_t u[8], vv[8], dd[8], c[4];
-    cook<PRO>(a, nb, luts + 256, c);
-    unpack16(c, u);
+    uint32_t u[8], vv[8], dd[8];
+    cook_pairs<PRO>(a, nb, luts, u);
     load_raw<PRO>(rin, y + kPF < ye ? in_row_off(a, y + kPF + R) : last_row, lane_in, nb);
     if constexpr (F::SOBEL) {
       vpush_sobel<F>(u, prev, next, vv, dd);
@@ -512,10 +563,10 @@ __global__ __launch_bounds__(kNT, (F::K >= 5 ? 3 : 4)) void k_direct(KArgs a) {
   constexpr int R = F::R, K = F::K;
   constexpr int NX = (R * C + 1) / 2;  // neighbour dwords per side
   constexpr int NE = 8 + 2 * NX;       // extended row dwords
-  constexpr int CIN = PRO == PRO_GRAY ? 3 : 1;
-  __shared__ uint8_t luts[768];
+  constexpr int CIN = is_gray(PRO) ? 3 : 1;
+  __shared__ uint8_t luts[PRO == PRO_GRAYLUT ? kLutBytes : 768];
   if (PRO != PRO_NONE || a.has_epi) {
-    load_luts(a, luts);
+    load_luts<PRO>(a, luts);
     __syncthreads();
   }
   const WaveTask t = wave_task(a);
@@ -532,9 +583,8 @@ __global__ __launch_bounds__(kNT, (F::K >= 5 ? 3 : 4)) void k_direct(KArgs a) {
 
   uint32_t ring[K][NE];  // slot of input row r: (r - (ys - R)) mod K
   auto push = [&](const RawChunk<PRO>& raw, uint32_t (&slot)[NE]) __attribute__((always_inline)) {
-    uint32_t c[4], u[8];
-    cook<PRO>(a, raw, luts + 256, c);
-    unpack16(c, u);
+    uint32_t u[8];
+    cook_pairs<PRO>(a, raw, luts, u);
     extend_row<NX>(u, slot);
   };
 #pragma unroll
@@ -667,7 +717,8 @@ void launch_filter(const Pass& p, const KArgs& a, int tiles, int n0, int n1, int
     if (lut) launch_one<3, F, PRO_LUT>(skip, nt, a, tiles, n0, n1, band, s);
     else launch_one<3, F, PRO_NONE>(skip, nt, a, tiles, n0, n1, band, s);
   } else {
-    if (gray) launch_one<1, F, PRO_GRAY>(skip, nt, a, tiles, n0, n1, band, s);
+    if (gray && a.gmode == 1) launch_one<1, F, PRO_GRAYLUT>(skip, nt, a, tiles, n0, n1, band, s);
+    else if (gray) launch_one<1, F, PRO_GRAY>(skip, nt, a, tiles, n0, n1, band, s);
     else if (lut) launch_one<1, F, PRO_LUT>(skip, nt, a, tiles, n0, n1, band, s);
     else launch_one<1, F, PRO_NONE>(skip, nt, a, tiles, n0, n1, band, s);
   }

@@ -24,8 +24,11 @@ namespace stripe {
   } while (0)
 
 // Device-resident per-pass constants, built once by the engine.
+// Per-pass LUT block: [pre 256 | post 256 | epi 256 | gray:ref R, G, B terms 3 x 256].
+constexpr int kLutBytes = 1536;
+
 struct PassConsts {
-  uint8_t* luts = nullptr;   // [pre 256 | post 256 | epi 256]
+  uint8_t* luts = nullptr;   // kLutBytes, layout above
   void* conv = nullptr;      // conv pass: packed MFMA operand tables
   size_t conv_bytes = 0;
 };
