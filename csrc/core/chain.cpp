@@ -160,7 +160,7 @@ Plan compile_chain(const std::vector<Op>& ops, int cin, Border default_border, b
       p.sep_v = op.sep_v;
       p.cin = p.cmid = p.cout = c;
       p.desc = "conv" + std::to_string(op.K) + "x" + std::to_string(op.K) +
-               (p.sep_h.empty() ? "(mfma) " : "(mfma-separable) ") +
+               (p.sep_h.empty() ? (op.K <= 5 || (op.K == 7 && c == 1) ? "(direct) " : "(mfma) ") : "(mfma-separable) ") +
                std::to_string(c) + "ch border=" + border_name(p.border);
     } else {
       const StencilInfo& si = stencil_info(op.sid);

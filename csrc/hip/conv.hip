@@ -127,8 +127,24 @@ void prepare_conv_consts(const Pass& p, PassConsts* pc, hipStream_t s) {
   HIP_CHECK(hipStreamSynchronize(s));
 }
 
+void launch_conv_mfma(const Pass& p, const PassConsts& pc, const PassLaunch& L, hipStream_t s);
+
 void launch_conv(const Pass& p, const PassConsts& pc, const PassLaunch& L, hipStream_t s) {
   if (sep_supported(p)) return launch_blur_sep(p, pc, L, s);
+  if (conv_small_supported(p)) {
+    launch_conv_small(p, L, s);
+  } else {
+    launch_conv_mfma(p, pc, L, s);
+  }
+  // output margins for the next consumer
+  if (p.out_margin_px > 0)
+    for (int r = 0; r < L.nrange; ++r)
+      launch_fill_margins(L.out, L.out_pitch, L.W, p.cmid, L.ry[2 * r], L.ry[2 * r + 1], p.out_margin_px,
+                          p.out_margin_border, s);
+}
+
+// Banded-Toeplitz MFMA convolution for windows beyond the direct kernel's reach.
+void launch_conv_mfma(const Pass& p, const PassConsts& pc, const PassLaunch& L, hipStream_t s) {
   STRIPE_CHECK(pc.conv != nullptr, "conv pass constants not prepared");
   dev::ConvArgs ca{};
   dev::KArgs& a = ca.a;
@@ -157,11 +173,6 @@ void launch_conv(const Pass& p, const PassConsts& pc, const PassLaunch& L, hipSt
     else dev::k_conv_mfma<1><<<grid, 256, lds, s>>>(ca);
     HIP_CHECK(hipGetLastError());
   }
-  // output margins for the next consumer
-  if (p.out_margin_px > 0)
-    for (int r = 0; r < L.nrange; ++r)
-      launch_fill_margins(L.out, L.out_pitch, L.W, p.cmid, L.ry[2 * r], L.ry[2 * r + 1], p.out_margin_px,
-                          p.out_margin_border, s);
 }
 
 }  // namespace stripe

@@ -76,6 +76,10 @@ void launch_synth(uint8_t* origin, int64_t pitch, int W, int C, int row0, int ro
 // Build the device constant block of a conv pass (MFMA operand tables).
 void prepare_conv_consts(const Pass& p, PassConsts* pc, hipStream_t s);
 
+// Small general conv (K <= 7) on the VALU (csrc/hip/stencil.hip k_conv_small).
+bool conv_small_supported(const Pass& p);
+void launch_conv_small(const Pass& p, const PassLaunch& L, hipStream_t s);
+
 // Separable (rank-one) conv on MFMA (csrc/hip/blur_sep.hip).
 bool sep_supported(const Pass& p);
 void prepare_sep_consts(const Pass& p, PassConsts* pc, hipStream_t s);
