@@ -7,8 +7,9 @@ void launch_pass(const Pass& p, const PassConsts& pc, const PassLaunch& L, hipSt
   // host-side shape checks before any kernel touches memory
   STRIPE_CHECK(L.in && L.out && L.W >= 1 && L.rows >= 0, "bad pass launch");
   STRIPE_CHECK(L.nrange == 1 || L.nrange == 2, "nrange must be 1 or 2");
-  STRIPE_CHECK(L.ext >= 0 && (L.ext == 0 || p.kind == PassKind::Separable || p.kind == PassKind::Direct),
-               "halo-row outputs (ext) are for stencil passes only");
+  STRIPE_CHECK(L.ext >= 0 && (L.ext == 0 || p.kind == PassKind::Separable || p.kind == PassKind::Direct ||
+                               p.kind == PassKind::Pointwise),
+               "halo-row outputs (ext) are for stencil and pointwise passes only");
   for (int r = 0; r < L.nrange; ++r)
     STRIPE_CHECK(-L.ext <= L.ry[2 * r] && L.ry[2 * r] <= L.ry[2 * r + 1] && L.ry[2 * r + 1] <= L.rows + L.ext,
                  "row range [" << L.ry[2 * r] << "," << L.ry[2 * r + 1] << ") outside stripe of " << L.rows

@@ -136,7 +136,7 @@ class Engine {
   void rewind();
   // hipGraph replays so far (tests / reporting).
   int graph_launches() const { return graph_launches_; }
-  // Iterations per halo exchange of iterated runs (1: every iteration).
+  // Iterations per chain-level halo exchange (0: one exchange per pass and iteration).
   int halo_depth() const { return depth_; }
   // Tuned band heights per pass (after autotune), for reporting.
   std::vector<int> bands() const;
@@ -180,9 +180,10 @@ class Engine {
   bool time_halo_ = true;  // record the halo stage events (last iteration of a run only)
   void run_pass(const Pass& p, const uint8_t* in, uint8_t* out);
   bool pipelined_ok() const;
+  int chain_reach() const;  // sum of the chain's radii if every pass can extend its rows, else 0
   int choose_depth() const;
   void run_deep(int iterations);
-  int depth_ = 1;                  // iterations per halo exchange (deep halo)
+  int depth_ = 0;                  // iterations per chain-level exchange (deep halo); 0: per-pass exchange
   void run_pipelined(int iterations);
   hipStream_t s_edge_ = nullptr;   // rim + boundary rows of the pipelined halo schedule
   hipEvent_t pev_[7] = {};         // core[2], rim[2], boundary, exchange, start

@@ -100,7 +100,7 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
   part_ = plan_rows(cfg_.H, world_, std::max(1, plan_.max_radius), cfg_.legacy_partition);
   halo_ = plan_.max_radius;
   depth_ = choose_depth();
-  if (depth_ > 1) halo_ = std::max(halo_, depth_ * plan_.passes[0].R);
+  if (depth_ >= 1) halo_ = std::max(halo_, depth_ * chain_reach());
   const Stripe& st = stripe();
   rows_alloc_ = st.rows + 2 * halo_;
   const int64_t pmax = padded_pitch(cfg_.W, plan_.max_channels);
@@ -591,95 +591,109 @@ void Engine::run_pipelined(int iterations) {
 }
 
 // ---------------------------------------------------------------------------
-// Deep halo (communication-avoiding iteration) for iterated single-pass chains
-// over > 1 ranks.  A block of m <= k iterations starts with ONE exchange of
-// m*R rows per side; iteration i of the block then computes the rank's own
-// rows plus (m-1-i)*R rows of each neighbour's stripe (recomputed redundantly,
-// bit-identical to what the neighbour computes: same kernel, same global row
-// grid), so iteration i+1 finds its R-row halo already local.  Per iteration
-// the wire carries the same R rows on average, but the exchange latency, the
-// cross-stream waits and the interior/boundary launch split are paid once per
-// block instead of once per iteration; the price is (m-1)*R/2 extra rows per
-// interior side and iteration on average (< 1 % of a 2048-row stripe at the
-// default depth).  Stencil kernels address rows by global index
-// (in_row_off), so an output range reaching into the halo rows is ordinary.
+// Chain-level ("deep") halo for multi-rank runs.  The chain's stencil radii
+// sum to S; a block of m <= k iterations starts with ONE exchange of m*S rows
+// of the chain input per side, and every pass then computes the rank's own
+// rows plus the shrinking band of neighbour rows the rest of the block still
+// needs ((m-1-i)*S + the radii of the passes after it), recomputed
+// redundantly and bit-identically to the neighbour (same kernels, same global
+// row grid).  Compared with one exchange per pass and iteration, the wire
+// carries the same rows on average, but the exchange latency, the cross-stream
+// waits and the interior/boundary launch split are paid once per block; the
+// price is (m-1)*S/2 + O(S) extra rows per interior side and pass (< 1 % of a
+// 2048-row stripe at the default depth).  Multi-pass chains (e.g.
+// gaussian5,sobel) exchange once per chain instead of once per pass even at
+// m = 1.  Stencil and pointwise kernels address rows by global index, so an
+// output range reaching into the halo rows is ordinary; the MFMA blur/conv
+// passes (32-row group grid) keep the per-pass exchange.
 // ---------------------------------------------------------------------------
+int Engine::chain_reach() const {
+  int s = 0;
+  for (const Pass& p : plan_.passes) {
+    if (p.kind != PassKind::Pointwise && p.kind != PassKind::Separable && p.kind != PassKind::Direct) return 0;
+    s += p.R;
+  }
+  return s;
+}
+
 int Engine::choose_depth() const {
-  if (!cfg_.halo || part_.active <= 1 || plan_.passes.size() != 1 || plan_.cin != plan_.cout) return 1;
-  // integer stencils only: the MFMA blur computes whole 32-row groups anchored
-  // to the global row grid, so its halo-row outputs would cost a group per side
-  const PassKind kind = plan_.passes[0].kind;
-  if (kind != PassKind::Separable && kind != PassKind::Direct) return 1;
-  const int R = plan_.passes[0].R;
-  if (R <= 0) return 1;
+  if (!cfg_.halo || part_.active <= 1) return 0;
+  if (const char* e = std::getenv("STRIPE_DEEP"); e && std::atoi(e) == 0) return 0;  // A/B: per-pass exchange
+  const int S = chain_reach();
+  if (S <= 0) return 0;
   int minrows = std::numeric_limits<int>::max();
   for (int r = 0; r < part_.active; ++r) minrows = std::min(minrows, part_.of(r).rows);
   int k = cfg_.halo_depth;
   if (k <= 0) {
     if (const char* e = std::getenv("STRIPE_HALO_DEPTH")) k = std::atoi(e);
   }
-  if (k <= 0) k = std::min(8, 1 + (minrows / 100) / R);  // redundant rows <= ~1 % of the stripe
-  // every neighbour must own the k*R rows it sends (and keep its own interior)
-  k = std::min(k, minrows / (2 * R));
-  return std::max(1, k);
+  if (plan_.cin != plan_.cout) k = 1;                          // not iterable: one chain per run
+  if (k <= 0) k = std::min(8, 1 + (minrows / 100) / S);       // redundant rows <= ~1 % of the stripe
+  // every neighbour must own the k*S rows it sends (and keep its own interior)
+  k = std::min(k, minrows / (2 * S));
+  return k >= 1 ? k : 0;
 }
 
 void Engine::run_deep(int iterations) {
-  const Pass& p = plan_.passes[0];
-  const int R = p.R, rows = stripe().rows;
+  const int S = chain_reach(), rows = stripe().rows;
   if (rows == 0) return;
   const bool up = rank_ > 0, down = rank_ + 1 < part_.active;
-  const PassConsts& pc = prt_[0].pc;
-  // the block's exchange flies on the comm stream beside the first iteration's
-  // interior rows [R, rows - R), which read only the rank's own rows; the
-  // boundary rows of that iteration follow once the halo has landed (two
-  // cross-stream waits per block instead of per step)
+  const Pass& p0 = plan_.passes[0];
+  const int R0 = p0.R;
+  // the block's exchange flies on the comm stream beside the first pass's
+  // interior rows [R0, rows - R0), which read only the rank's own rows; its
+  // boundary rows follow once the halo has landed (two cross-stream waits per
+  // block instead of per pass and step)
   static const bool env_overlap = [] {
     const char* e = std::getenv("STRIPE_DEEP_OVERLAP");
     return !e || std::atoi(e) != 0;
   }();
-  const bool overlap = device() && cfg_.overlap && env_overlap && rows > 2 * R;
-  const int iy0 = up ? R : 0, iy1 = down ? rows - R : rows;  // rows needing no halo
+  const bool overlap = device() && cfg_.overlap && env_overlap && rows > 2 * R0;
+  const int iy0 = up ? R0 : 0, iy1 = down ? rows - R0 : rows;  // rows needing no halo
   for (int done = 0; done < iterations;) {
     const int m = std::min(depth_, iterations - done);
     time_halo_ = done + m >= iterations;  // stage events of the last exchange only
     if (overlap) {
       HIP_CHECK(hipEventRecord(ev_[4], s_compute_));
       HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_[4], 0));
-      exchange_halo(origin(buf_[cur_], p.cin), p.cin, m * R, s_comm_);
+      exchange_halo(origin(buf_[cur_], p0.cin), p0.cin, m * S, s_comm_);
       HIP_CHECK(hipEventRecord(ev_[5], s_comm_));
     } else {
-      exchange_halo(origin(buf_[cur_], p.cin), p.cin, m * R, s_compute_);
+      exchange_halo(origin(buf_[cur_], p0.cin), p0.cin, m * S, s_compute_);
     }
     for (int i = 0; i < m; ++i) {
-      const int ext = (m - 1 - i) * R;
-      const int y0 = up ? -ext : 0, y1 = rows + (down ? ext : 0);
-      uint8_t* in = origin(buf_[cur_], p.cin);
-      uint8_t* out = origin(buf_[cur_ ^ 1], p.cout);
-      if (device()) {
-        PassLaunch L = make_launch(p, in, out, 0);
-        L.ext = ext;
-        if (overlap && i == 0) {
-          L.nrange = 1;
-          L.ry[0] = iy0;
-          L.ry[1] = iy1;
-          launch_pass(p, pc, L, s_compute_);
-          HIP_CHECK(hipStreamWaitEvent(s_compute_, ev_[5], 0));
-          L.nrange = 2;
-          L.ry[0] = y0;
-          L.ry[1] = iy0;
-          L.ry[2] = iy1;
-          L.ry[3] = y1;
+      int reach = (m - i) * S;  // halo rows valid in the current input
+      for (size_t k = 0; k < plan_.passes.size(); ++k) {
+        const Pass& p = plan_.passes[k];
+        reach -= p.R;  // halo rows this pass's output must cover
+        const int y0 = up ? -reach : 0, y1 = rows + (down ? reach : 0);
+        uint8_t* in = origin(buf_[cur_], p.cin);
+        uint8_t* out = origin(buf_[cur_ ^ 1], p.cout);
+        if (device()) {
+          PassLaunch L = make_launch(p, in, out, (int)k);
+          L.ext = reach;
+          if (overlap && i == 0 && k == 0) {
+            L.nrange = 1;
+            L.ry[0] = iy0;
+            L.ry[1] = iy1;
+            launch_pass(p, prt_[k].pc, L, s_compute_);
+            HIP_CHECK(hipStreamWaitEvent(s_compute_, ev_[5], 0));
+            L.nrange = 2;
+            L.ry[0] = y0;
+            L.ry[1] = iy0;
+            L.ry[2] = iy1;
+            L.ry[3] = y1;
+          } else {
+            L.nrange = 1;
+            L.ry[0] = y0;
+            L.ry[1] = y1;
+          }
+          launch_pass(p, prt_[k].pc, L, s_compute_);
         } else {
-          L.nrange = 1;
-          L.ry[0] = y0;
-          L.ry[1] = y1;
+          golden_pass(p, ConstView{in, pitch(p.cin)}, MutView{out, pitch(p.cout)}, cfg_.W, geom(), y0, y1);
         }
-        launch_pass(p, pc, L, s_compute_);
-      } else {
-        golden_pass(p, ConstView{in, pitch(p.cin)}, MutView{out, pitch(p.cout)}, cfg_.W, geom(), y0, y1);
+        cur_ ^= 1;
       }
-      cur_ ^= 1;
     }
     done += m;
   }
@@ -761,7 +775,7 @@ void Engine::run(int iterations) {
     }
   };
   const int cycle = plan_.passes.size() % 2 == 0 ? 1 : 2;
-  if (depth_ > 1 && iterations > 1 && cur_c_ == plan_.cin) {
+  if (depth_ >= 1 && cur_c_ == plan_.cin && ((depth_ > 1 && iterations > 1) || plan_.passes.size() > 1)) {
     run_deep(iterations);
   } else if (cfg_.pipeline && cfg_.overlap && pipelined_ok() && cur_c_ == plan_.cin) {
     run_pipelined(iterations);

@@ -37,15 +37,15 @@ def test_depth_reported_and_clamped(C):
 
     # 3 ranks over 30 rows: 10-row stripes hold at most 10 / (2*R) = 2 exchanges' worth at R=2
     cfg = m.Pipeline("gaussian5", halo_depth=8).config(40, 30, 3, "host")
-    assert C.Engine(cfg).halo_depth == 1  # one rank (no comm): no exchange to avoid
+    assert C.Engine(cfg).halo_depth == 0  # one rank (no comm): no chain-level exchange
     out = C.run_local_group(cfg, 3, m.utils.synthetic_image(2, 40, 30, 3), 6)
     assert (out == _golden_iter(C, m.utils.synthetic_image(2, 40, 30, 3), "gaussian5", 6)).all()
 
 
-@pytest.mark.parametrize("chain", ["gaussian5,sobel", "gray,emboss3", "blur:9"])
+@pytest.mark.parametrize("chain", ["gray,emboss3", "blur:9"])
 def test_other_chains_keep_per_pass_exchange(C, chain):
-    """Multi-pass chains, channel-changing chains and MFMA passes keep the
-    per-pass exchange (depth 1) and stay exact."""
+    """Channel-changing single passes and MFMA passes keep the per-pass
+    exchange and stay exact."""
     import mpi_cuda_imagemanipulation_amd as m
 
     img = m.utils.synthetic_image(9, 47, 60, 3)
@@ -54,3 +54,23 @@ def test_other_chains_keep_per_pass_exchange(C, chain):
     ref = C.golden_apply(img, chain, "reflect101", True)
     tol = 1 if chain.startswith("blur") else 0
     assert np.abs(out.astype(int) - ref.astype(int)).max() <= tol
+
+
+@pytest.mark.parametrize("chain", ["gaussian5,sobel", "gaussian3,invert,emboss3", "gray,gaussian5,expand,box3",
+                                   "sobel,gaussian7", "invert,gaussian5,brightness:9,sharpen"])
+@pytest.mark.parametrize("ranks,depth", [(2, 0), (3, 2), (4, 3)])
+@pytest.mark.parametrize("iters", [1, 3])
+def test_multipass_chain_level_exchange(C, chain, ranks, depth, iters):
+    """Multi-pass chains exchange the summed radius once per chain (and per
+    block of `depth` iterations); every pass, pointwise ones included,
+    extends its rows into the halo.  Must equal the iterated golden chain."""
+    import mpi_cuda_imagemanipulation_amd as m
+
+    W, H = 41, 96
+    img = m.utils.synthetic_image(17, W, H, 3)
+    info = C.plan_info(chain, 3)
+    if info["cin"] != info["cout"] and iters > 1:
+        pytest.skip("chain changes the channel count: not iterable")
+    cfg = m.Pipeline(chain, halo_depth=depth).config(W, H, 3, "host")
+    out = C.run_local_group(cfg, ranks, img, iters)
+    assert (out == _golden_iter(C, img, chain, iters)).all()

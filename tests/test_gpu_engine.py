@@ -170,3 +170,24 @@ def test_deep_halo_schedule(m, chain, ranks, H, depth, iters):
         res.append(C.run_local_group(pipe.config(W, H, 3, "device", device=0), nr, img, iters))
     assert (res[0] == res[1]).all()
     assert (res[0] == res[2]).all()
+
+
+@pytest.mark.parametrize("chain", ["gaussian5,sobel", "gaussian3,invert,emboss3", "gray,gaussian5,expand,box3",
+                                   "invert,gaussian5,brightness:9,sharpen"])
+@pytest.mark.parametrize("ranks,depth", [(2, 0), (4, 2), (8, 3)])
+@pytest.mark.parametrize("iters", [1, 4])
+def test_multipass_chain_level_exchange_gpu(m, chain, ranks, depth, iters):
+    """Multi-pass chains on the GPU: one exchange of the summed radius per
+    chain (per block of `depth` iterations), every pass (pointwise ones too)
+    writing rows inside the halo; equals the 1-rank result bit-for-bit."""
+    C = m._C
+    W, H = 203, 211
+    info = C.plan_info(chain, 3)
+    if info["cin"] != info["cout"] and iters > 1:
+        pytest.skip("chain changes the channel count: not iterable")
+    img = m.utils.synthetic_image(19, W, H, 3)
+    res = []
+    for nr in (ranks, 1):
+        pipe = m.Pipeline(chain, halo_depth=depth)
+        res.append(C.run_local_group(pipe.config(W, H, 3, "device", device=0), nr, img, iters))
+    assert (res[0] == res[1]).all()
