@@ -12,4 +12,5 @@ run c4_gauss5_16k_rgb --steps 200 --warmup 20 --e2e-steps 3 --dist-steps 5
 run c4_gauss5_16k_rgb_share8 --height 2048 --steps 400 --warmup 40 --e2e-steps 0 --dist-steps 0
 run c5_blur31_16k_rgb --chain blur:31 --steps 20 --warmup 3 --e2e-steps 2 --dist-steps 2
 run c5_blur31_16k_rgb_share8 --chain blur:31 --height 2048 --steps 100 --warmup 10 --e2e-steps 0 --dist-steps 0
-run c4_ref_chain_16k_rgb --chain "gray:ref,contrast:3.5,emboss3" --steps 1 --warmup 1 --e2e-steps 2 --dist-steps 2
+run c4_ref_chain_16k_rgb --chain "gray:ref,contrast:3.5,emboss3" --steps 50 --warmup 5 --e2e-steps 2 --dist-steps 2
+run c2_conv3_4096_rgb --width 4096 --height 4096 --chain "conv:3:1;2;1;2;4;2;1;2;1" --steps 200 --warmup 20 --e2e-steps 0 --dist-steps 0
