@@ -1,13 +1,16 @@
-// Large-kernel float convolution pass (blur:K, conv:K:...).
+// Large-kernel float convolution pass (conv:K:..., K up to 33, not rank one).
 //
-// Implicit im2col -> GEMM on MFMA.  For one kernel row ky the output tile
-//   out[y0:y0+16, x0:x0+32] += In[y0+ky-R : +16, x0-R : x0-R+64] . T_ky[64 x 32]
-// is a real GEMM (M = 16 output rows, N = 32 output pixels, K = 64 input pixels),
-// where T_ky is the banded Toeplitz matrix of weight row ky (T[k][n] = w[ky][k-n]).
-// Channels are de-interleaved into planes in LDS so the band only couples
-// pixels of one channel.  u8 inputs are exact in f16; each weight is split into
-// hi + lo f16 parts (two MFMAs) so the f32 accumulation sees ~2^-22 relative
-// weight error: results match the f64 golden to within 1 LSB (ties only).
+// Implicit im2col -> GEMM on MFMA.  For one kernel row ky and one 16-pixel
+// n-tile the output tile
+//   out[y0:y0+16, x0:x0+16] += In[y0+ky-R : +16, x0-R : x0-R+64] . T_ky[64 x 16]
+// is a real GEMM (M = 16 output rows, N = 16 output pixels, K = 64 window
+// pixels), where T_ky is the banded Toeplitz matrix of weight row ky
+// (T[k][n] = w[ky][k-n]), the same for every n-tile.  Channels are
+// de-interleaved into f16 planes in LDS so the band only couples pixels of one
+// channel.  u8 inputs are exact in f16; each weight is split into hi + lo f16
+// parts (two MFMAs) so the f32 accumulation sees ~2^-22 relative weight error:
+// results match the f64 golden to within 1 LSB (ties only).  Windows up to
+// 5x5 (7x7 gray) take the VALU direct kernel instead (stencil.hip).
 #include "dev_common.h"
 #include "stripe/kernels.h"
 
@@ -21,78 +24,96 @@ typedef float float4v __attribute__((ext_vector_type(4)));
 
 struct ConvArgs {
   KArgs a;
-  const _Float16* tw;  // Toeplitz B fragments: [K][hilo 2][ntile 2][kstep 2][lane 64][8]
+  const _Float16* tw;  // Toeplitz B fragments: [K][hilo 2][kstep 2][lane 64][8]
   int K, R;
 };
 
-constexpr int kCTM = 16;          // output rows per MFMA tile (M)
-constexpr int kCTN = 32;          // output pixels per tile (N = 2 x 16)
-constexpr int kCTK = 64;          // input pixels per tile window (K = 2 x 32)
-constexpr int kCTKP = 72;         // LDS row stride (halves): 144 B rows spread the banks
+constexpr int kCTN = 64;          // output pixels per workgroup (4 waves x 16)
+constexpr int kCTK = 64;          // Toeplitz window per 16-pixel n-tile (2 k-steps x 32)
+constexpr int kCWin = 48 + kCTK;  // staged pixels per row: every wave's full 64-pixel window
+                                  // (the zero-weight tail is multiplied too: it must hold
+                                  // finite values, not stale LDS that may read as NaN)
+constexpr int kCTKP = kCWin + 8;  // LDS row stride (halves): 240 B rows spread the banks
 constexpr int kConvWaves = 4;     // waves per workgroup
-constexpr int kConvRowsPerWave = 16;
-constexpr int kConvRowsPerBlock = kConvWaves * kConvRowsPerWave;  // 64 output rows
+constexpr int kConvMT = 3;        // 16-row m-tiles per wave (each B fragment feeds 3 MFMAs;
+                                  // 3 planes x (48 + 32) rows x 240 B stays under 64 KiB)
+constexpr int kConvRowsPerBlock = 16 * kConvMT;  // 48 output rows
 
-// One workgroup: 64 output rows x 32 output pixels x all channels.
-// LDS: input plane window [(64 + K - 1) rows][64 px] f16 per channel.
+// One workgroup: 48 output rows x 64 output pixels x all channels.  The input
+// window [(48 + K - 1) rows][112 px] is staged once for every channel
+// plane (dword loads of the interleaved row, de-interleaved into f16 planes);
+// wave w owns output pixels [16 w, 16 w + 16) of every row, so each Toeplitz B
+// fragment it streams from L2 feeds three MFMAs (one per 16-row m-tile).
 template <int C>
 __global__ __launch_bounds__(256) void k_conv_mfma(ConvArgs ca) {
   const KArgs& a = ca.a;
   const int K = ca.K, R = ca.R;
-  extern __shared__ __attribute__((aligned(16))) _Float16 plane[];  // [rows_in][kCTKP]
+  extern __shared__ __attribute__((aligned(16))) _Float16 plane[];  // [C][rows_in][kCTKP]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int x0 = blockIdx.x * kCTN;                     // first output pixel
+  const int x0 = blockIdx.x * kCTN;                       // first output pixel
   const int yb = a.ry0 + blockIdx.y * kConvRowsPerBlock;  // first output row of block
   if (yb >= a.ry1) return;
   const int rows_in = kConvRowsPerBlock + K - 1;
+  const int win = kCWin;  // staged pixels per row
+  const int plane_sz = rows_in * kCTKP;
 
-  for (int c = 0; c < C; ++c) {
-    // stage input plane: rows yb-R .. yb+63+R, pixels x0-R .. x0-R+63 (margins hold borders)
-    __syncthreads();
-    for (int i = tid; i < rows_in * kCTK; i += 256) {
-      const int r = i / kCTK, px = i % kCTK;
+  // ---- stage: pixels [x0 - R, x0 - R + kCWin) of rows yb - R .. (dword loads) ----
+  {
+    const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);
+    const int b0 = (x0 - R) * C;                // first window byte (margins hold the x-border)
+    const int b0a = b0 & ~3;                    // dword-aligned start
+    const int nd = (b0 + win * C - b0a + 3) / 4;  // dwords per row
+    for (int i = tid; i < rows_in * nd; i += 256) {
+      const int r = i / nd, q = i - r * nd;
       // rows past the range's last needed input row (ry1 - 1 + R) feed only
       // outputs that are not stored; clamp so no read leaves the stripe + halo
-      const uint8_t* row = in_row(a, min(yb - R + r, a.ry1 - 1 + R));
-      int x = x0 - R + px;
-      // pixels beyond the right margin are never used by valid outputs; clamp reads
-      if (x > a.W - 1 + R) x = a.W - 1 + R;
-      plane[r * kCTKP + px] = (_Float16)(float)row[(int64_t)x * C + c];
+      const int y = min(yb - R + r, a.ry1 - 1 + R);
+      // bytes past the allocation read as 0 (range check); they feed only x >= W
+      const uint32_t d = __builtin_amdgcn_raw_buffer_load_b32(rin, in_row_off(a, y) + (uint32_t)(b0a + 4 * q), 0, 0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int bi = b0a + 4 * q + e - b0;  // byte index within the window
+        if (bi >= 0 && bi < win * C) {
+          const int px = bi / C, c = bi - px * C;
+          plane[c * plane_sz + r * kCTKP + px] = (_Float16)(float)((d >> (8 * e)) & 0xFFu);
+        }
+      }
     }
-    __syncthreads();
-    float4v acc[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
-    const int mrow = lane & 15;        // A row (output row within wave tile)
-    const int kq = (lane >> 4) * 8;    // A k offset within a 32-step
+  }
+  __syncthreads();
+
+  const int mrow = lane & 15;      // A row (output row within an m-tile)
+  const int kq = (lane >> 4) * 8;  // A k offset within a 32-step
+  for (int c = 0; c < C; ++c) {
+    const _Float16* pl = plane + c * plane_sz + 16 * wave;  // n-tile window start
+    float4v acc[kConvMT];
+#pragma unroll
+    for (int mt = 0; mt < kConvMT; ++mt) acc[mt] = float4v{0.f, 0.f, 0.f, 0.f};
     for (int ky = 0; ky < K; ++ky) {
-      const _Float16* arow = plane + (wave * kConvRowsPerWave + mrow + ky) * kCTKP;
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const half8 afrag = *reinterpret_cast<const half8*>(arow + ks * 32 + kq);
+        half8 bfrag[2];
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {
+        for (int hl = 0; hl < 2; ++hl)
+          bfrag[hl] = *reinterpret_cast<const half8*>(ca.tw + (((size_t)ky * 2 + hl) * 2 + ks) * 512 + lane * 8);
 #pragma unroll
-          for (int hl = 0; hl < 2; ++hl) {
-            const half8 bfrag = *reinterpret_cast<const half8*>(
-                ca.tw + ((((size_t)ky * 2 + hl) * 2 + nt) * 2 + ks) * 512 + lane * 8);
-            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(afrag, bfrag, acc[nt], 0, 0, 0);
-          }
+        for (int mt = 0; mt < kConvMT; ++mt) {
+          const half8 afrag = *reinterpret_cast<const half8*>(pl + (16 * mt + mrow + ky) * kCTKP + ks * 32 + kq);
+          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(afrag, bfrag[0], acc[mt], 0, 0, 0);
+          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(afrag, bfrag[1], acc[mt], 0, 0, 0);
         }
       }
     }
     // C/D layout: col = lane & 15, row = (lane >> 4) * 4 + reg
+    const int x = x0 + 16 * wave + (lane & 15);
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
+    for (int mt = 0; mt < kConvMT; ++mt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int y = yb + wave * kConvRowsPerWave + (lane >> 4) * 4 + r;
-        const int x = x0 + nt * 16 + (lane & 15);
-        if (y < a.ry1 && x < a.W) {
-          float v = rintf(acc[nt][r]);
-          v = fminf(fmaxf(v, 0.f), 255.f);
-          a.out[(int64_t)y * a.out_pitch + (int64_t)x * C + c] = (uint8_t)v;
-        }
+        const int y = yb + 16 * mt + (lane >> 4) * 4 + r;
+        if (y < a.ry1 && x < a.W)  // v_cvt_pk_u8_f32: round half even + saturate (the golden's nearbyint)
+          a.out[(int64_t)y * a.out_pitch + (int64_t)x * C + c] = (uint8_t)__builtin_amdgcn_cvt_pk_u8_f32(acc[mt][r], 0, 0u);
       }
-    }
   }
 }
 
@@ -103,24 +124,24 @@ __global__ __launch_bounds__(256) void k_conv_mfma(ConvArgs ca) {
 void prepare_conv_consts(const Pass& p, PassConsts* pc, hipStream_t s) {
   if (sep_supported(p)) return prepare_sep_consts(p, pc, s);
   const int K = p.K;
-  STRIPE_CHECK(K - 1 + dev::kCTN <= dev::kCTK, "conv K=" << K << " exceeds the 64-pixel window");
-  std::vector<_Float16> host((size_t)K * 2 * 2 * 2 * 512);
+  STRIPE_CHECK(K - 1 + 16 <= dev::kCTK && K <= 33,
+               "conv K=" << K << " exceeds the 64-pixel Toeplitz window");
+  std::vector<_Float16> host((size_t)K * 2 * 2 * 512);
   for (int ky = 0; ky < K; ++ky)
     for (int hl = 0; hl < 2; ++hl)
-      for (int nt = 0; nt < 2; ++nt)
-        for (int ks = 0; ks < 2; ++ks)
-          for (int l = 0; l < 64; ++l)
-            for (int j = 0; j < 8; ++j) {
-              const int k = ks * 32 + 8 * (l >> 4) + j;
-              const int n = nt * 16 + (l & 15);
-              const int d = k - n;
-              float w = 0.f;
-              if (d >= 0 && d < K) w = p.conv_w[(size_t)ky * K + d];
-              const _Float16 whi = (_Float16)w;
-              const float rem = w - (float)whi;
-              const _Float16 v = hl == 0 ? whi : (_Float16)rem;
-              host[(((((size_t)ky * 2 + hl) * 2 + nt) * 2 + ks) * 64 + l) * 8 + j] = v;
-            }
+      for (int ks = 0; ks < 2; ++ks)
+        for (int l = 0; l < 64; ++l)
+          for (int j = 0; j < 8; ++j) {
+            const int k = ks * 32 + 8 * (l >> 4) + j;  // window pixel
+            const int n = l & 15;                      // output pixel of the n-tile
+            const int d = k - n;
+            float w = 0.f;
+            if (d >= 0 && d < K) w = p.conv_w[(size_t)ky * K + d];
+            const _Float16 whi = (_Float16)w;
+            const float rem = w - (float)whi;
+            const _Float16 v = hl == 0 ? whi : (_Float16)rem;
+            host[((((size_t)ky * 2 + hl) * 2 + ks) * 64 + l) * 8 + j] = v;
+          }
   pc->conv_bytes = host.size() * sizeof(_Float16);
   HIP_CHECK(hipMalloc(&pc->conv, pc->conv_bytes));
   HIP_CHECK(hipMemcpyAsync(pc->conv, host.data(), pc->conv_bytes, hipMemcpyHostToDevice, s));
@@ -162,7 +183,12 @@ void launch_conv_mfma(const Pass& p, const PassConsts& pc, const PassLaunch& L, 
   ca.tw = reinterpret_cast<const _Float16*>(pc.conv);
   ca.K = p.K;
   ca.R = p.R;
-  const size_t lds = (size_t)(dev::kConvRowsPerBlock + p.K - 1) * dev::kCTKP * sizeof(_Float16);
+  const size_t lds = (size_t)p.cmid * (dev::kConvRowsPerBlock + p.K - 1) * dev::kCTKP * sizeof(_Float16);
+  STRIPE_CHECK(L.in_base && L.in_bytes > 0 && L.in_bytes < (int64_t)dev::kOOB, "conv launch needs the allocation view");
+  a.in_base = L.in_base;
+  a.in_bytes = (uint32_t)L.in_bytes;
+  a.in_org = (uint32_t)L.in_org;
+  a.in_zero = (uint32_t)L.in_zero;
   for (int r = 0; r < L.nrange; ++r) {
     const int y0 = L.ry[2 * r], y1 = L.ry[2 * r + 1];
     if (y1 <= y0) continue;
