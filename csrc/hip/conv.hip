@@ -55,28 +55,43 @@ __global__ __launch_bounds__(256) void k_conv_mfma(ConvArgs ca) {
   if (yb >= a.ry1) return;
   const int rows_in = kConvRowsPerBlock + K - 1;
   const int win = kCWin;  // staged pixels per row
-  const int plane_sz = rows_in * kCTKP;
+  // plane stride padded by 12 dwords so the three planes' writes of one pixel
+  // land in different LDS banks
+  const int plane_sz = rows_in * kCTKP + 24;
 
   // ---- stage: pixels [x0 - R, x0 - R + kCWin) of rows yb - R .. (dword loads) ----
+  // A lane loads dwords q = lane and lane + 64 of every row; which plane slot
+  // each of their bytes lands in is the same for every row, so it is computed
+  // once, and each wave walks its own rows with a wave-uniform (scalar) row
+  // offset: ~10 VALU per staged dword.
   {
     const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);
     const int b0 = (x0 - R) * C;                // first window byte (margins hold the x-border)
     const int b0a = b0 & ~3;                    // dword-aligned start
-    const int nd = (b0 + win * C - b0a + 3) / 4;  // dwords per row
-    for (int i = tid; i < rows_in * nd; i += 256) {
-      const int r = i / nd, q = i - r * nd;
+    const int lead = b0 - b0a;
+    const int nd = (lead + win * C + 3) / 4;    // dwords per row (<= 84 for C = 3)
+    int dst[2][4];
+#pragma unroll
+    for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int q = lane + 64 * qi;
+        const int bi = 4 * q + e - lead;  // byte index within the window
+        dst[qi][e] = (q < nd && bi >= 0 && bi < win * C) ? (bi % C) * plane_sz + bi / C : -1;
+      }
+    for (int r = wave; r < rows_in; r += kConvWaves) {
       // rows past the range's last needed input row (ry1 - 1 + R) feed only
       // outputs that are not stored; clamp so no read leaves the stripe + halo
       const int y = min(yb - R + r, a.ry1 - 1 + R);
-      // bytes past the allocation read as 0 (range check); they feed only x >= W
-      const uint32_t d = __builtin_amdgcn_raw_buffer_load_b32(rin, in_row_off(a, y) + (uint32_t)(b0a + 4 * q), 0, 0);
+      const uint32_t roff = in_row_off(a, y) + (uint32_t)b0a;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int bi = b0a + 4 * q + e - b0;  // byte index within the window
-        if (bi >= 0 && bi < win * C) {
-          const int px = bi / C, c = bi - px * C;
-          plane[c * plane_sz + r * kCTKP + px] = (_Float16)(float)((d >> (8 * e)) & 0xFFu);
-        }
+      for (int qi = 0; qi < 2; ++qi) {
+        const int q = lane + 64 * qi;
+        // bytes past the allocation read as 0 (range check); they feed only x >= W
+        const uint32_t d = __builtin_amdgcn_raw_buffer_load_b32(rin, roff + 4u * (uint32_t)q, 0, 0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (dst[qi][e] >= 0) plane[dst[qi][e] + r * kCTKP] = (_Float16)(float)((d >> (8 * e)) & 0xFFu);
       }
     }
   }
@@ -183,7 +198,7 @@ void launch_conv_mfma(const Pass& p, const PassConsts& pc, const PassLaunch& L, 
   ca.tw = reinterpret_cast<const _Float16*>(pc.conv);
   ca.K = p.K;
   ca.R = p.R;
-  const size_t lds = (size_t)p.cmid * (dev::kConvRowsPerBlock + p.K - 1) * dev::kCTKP * sizeof(_Float16);
+  const size_t lds = (size_t)p.cmid * ((dev::kConvRowsPerBlock + p.K - 1) * dev::kCTKP + 24) * sizeof(_Float16);
   STRIPE_CHECK(L.in_base && L.in_bytes > 0 && L.in_bytes < (int64_t)dev::kOOB, "conv launch needs the allocation view");
   a.in_base = L.in_base;
   a.in_bytes = (uint32_t)L.in_bytes;

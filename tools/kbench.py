@@ -31,7 +31,7 @@ def main():
     from mpi_cuda_imagemanipulation_amd.models import Pipeline
 
     W, H, Cc = (int(v) for v in a.shape.split("x"))
-    for chain, band in [(c, int(b)) for c in (a.chains.split("|") if "|" in a.chains else a.chains.split(";")) for b in a.bands.split(",")]:
+    for chain, band in [(c, int(b)) for c in (a.chains.split("|") if "|" in a.chains else a.chains.split(";")) if c for b in a.bands.split(",")]:
         pipe = Pipeline(chain, fuse=not a.no_fuse)
         cfg = pipe.config(W, H, Cc, "device", device=0)
         cfg.band = band
