@@ -1,4 +1,7 @@
 // CPU golden implementation of compiled passes (the bit-exact oracle).
+// It specifies every GPU kernel (the reference's grayscale/contrast/emboss,
+// kernel.cu:31-94, race-free) and is the engine of the
+// ref-cpu preset / host backend (the reference's OpenCV chain, kern.cpp:58-77).
 #include "stripe/golden.h"
 
 #include <cmath>

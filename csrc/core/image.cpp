@@ -1,4 +1,7 @@
 // PNM (PGM/PPM) codec, synthetic frames, image comparison.
+// Replaces the reference's cv::imread / cv::imwrite of a hard-coded path
+// (kernel.cu:108-123,236; kern.cpp:31-43,92): lossless, atomic-rename writes,
+// validated headers; other formats go through the Python front end (Pillow).
 #include "stripe/image.h"
 
 #include <cmath>

@@ -10,7 +10,9 @@
 // channel.  u8 inputs are exact in f16; each weight is split into hi + lo f16
 // parts (two MFMAs) so the f32 accumulation sees ~2^-22 relative weight error:
 // results match the f64 golden to within 1 LSB (ties only).  Windows up to
-// 5x5 (7x7 gray) take the VALU direct kernel instead (stencil.hip).
+// 5x5 (7x7 gray) take the VALU direct kernel instead (stencil.hip).  The
+// reference has no large-window convolution (its only stencil is the 3x3/5x5
+// emboss, kernel.cu:64-94); this is SURVEY config 5's im2col -> MFMA path.
 #include "dev_common.h"
 #include "stripe/kernels.h"
 

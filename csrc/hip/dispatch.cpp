@@ -1,4 +1,6 @@
 // Pass dispatch: one entry point for every compiled pass kind.
+// Every launch is shape-checked before it runs and error-checked after (the
+// reference launches three kernels with no checks, kernel.cu:192-195).
 #include "stripe/kernels.h"
 
 namespace stripe {

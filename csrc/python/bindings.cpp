@@ -1,4 +1,6 @@
 // Python bindings (pybind11): the native core exposed to the Python package.
+// (The reference has no Python API; this is the torch-facing front end of the
+// same engine the C++ CLI drives)
 //
 // Device buffers cross the boundary as integer pointers (torch tensor
 // data_ptr()) plus a stream handle (torch.cuda.current_stream().cuda_stream),

@@ -1,4 +1,8 @@
 // roctx ranges, fault injection and the collective wait bound (see trace.h).
+// The reference's only instrumentation is a chrono window printed on rank 0
+// (kernel.cu:190,226-232) and its error paths return without MPI_Abort
+// (kernel.cu:111-114); here stages carry roctx ranges and failures abort
+// the whole group.
 #include "stripe/trace.h"
 
 #include <rocprofiler-sdk-roctx/roctx.h>
