@@ -1,8 +1,9 @@
 // In-process communication groups (local = device copies, host = memcpy) and the
 // callback backend.  `local` is the 1-GPU stand-in for N ranks (the reference
 // runs every MPI rank on GPU 0, kernel.cu:147; SURVEY §4 'distributed (fake)').
-// Semantics match a grouped ncclSend/ncclRecv: sends are posted immediately, group_end() completes this rank's receives, then waits for
-// its sends to be consumed (so the sender may reuse its buffer afterwards).
+// Semantics match a grouped ncclSend/ncclRecv: sends are posted immediately,
+// group_end() completes this rank's receives, then waits for its sends to be
+// consumed (so the sender may reuse its buffer afterwards).
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
