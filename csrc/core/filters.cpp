@@ -38,6 +38,7 @@ StencilInfo make_info(StencilId id, const char* name) {
   s.K = F::K;
   s.separable = F::SEP;
   s.sobel = F::SOBEL;
+  if constexpr (F::SOBEL) s.l2 = F::L2;
   s.div = F::DIV;
   for (int dy = 0; dy < F::K; ++dy)
     for (int dx = 0; dx < F::K; ++dx) s.w.push_back(F::w(dy, dx));
@@ -64,6 +65,7 @@ const std::vector<StencilInfo>& table() {
     v[(int)StencilId::Sharpen] = make_info<sdef::Sharpen>(StencilId::Sharpen, "sharpen");
     v[(int)StencilId::Laplace] = make_info<sdef::Laplace>(StencilId::Laplace, "laplace");
     v[(int)StencilId::Sobel] = make_info<sdef::Sobel>(StencilId::Sobel, "sobel");
+    v[(int)StencilId::SobelL2] = make_info<sdef::SobelL2>(StencilId::SobelL2, "sobel_l2");
     return v;
   }();
   return t;
@@ -114,7 +116,8 @@ bool stencil_from_name(const std::string& name, StencilId* out) {
       {"box3", StencilId::Box3},         {"box5", StencilId::Box5},
       {"sharpen", StencilId::Sharpen},   {"laplace", StencilId::Laplace},
       {"laplacian", StencilId::Laplace}, {"sobel", StencilId::Sobel},
-      {"edge", StencilId::Sobel},
+      {"edge", StencilId::Sobel},        {"sobel_l2", StencilId::SobelL2},
+      {"magnitude", StencilId::SobelL2},
   };
   auto it = alias.find(name);
   if (it == alias.end()) return false;
@@ -267,7 +270,7 @@ std::vector<Op> parse_chain(const std::string& spec_in) {
     } else {
       fail("unknown filter '" + name +
            "' (gray[:ref|bt601], contrast:F[:cv], invert, brightness:D, threshold:T, expand, "
-           "emboss3, emboss5, gaussian3/5/7, box3/5, sharpen, laplace, sobel, blur:K[:sigma], conv:K:w.., sepconv:K:h..:v..)");
+           "emboss3, emboss5, gaussian3/5/7, box3/5, sharpen, laplace, sobel, sobel_l2, blur:K[:sigma], conv:K:w.., sepconv:K:h..:v..)");
     }
     if (op.has_border) op.text += std::string("@") + border_name(op.border);
     ops.push_back(op);

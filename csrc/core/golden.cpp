@@ -75,6 +75,14 @@ RowCache build_cache(const Pass& p, ConstView in, int W, RowGeom g, int y_lo, in
 
 }  // namespace
 
+// round(sqrt(n)) for n >= 0, exactly: sqrt of an integer is never k + 1/2.
+static int isqrt_round(int n) {
+  int k = (int)std::sqrt((double)n);
+  while (k * k > n) --k;
+  while ((k + 1) * (k + 1) <= n) ++k;
+  return n > k * k + k ? k + 1 : k;
+}
+
 void golden_pass(const Pass& p, ConstView in, MutView out, int W, RowGeom g, int y0, int y1) {
   if (y1 <= y0) return;
   if (p.kind == PassKind::Pointwise) {
@@ -134,7 +142,8 @@ void golden_pass(const Pass& p, ConstView in, MutView out, int W, RowGeom g, int
               if (si.sobel) s2 += wy[(size_t)dy * K + dx] * pv;
             }
           }
-          if (si.sobel) v = std::abs(s) + std::abs(s2);
+          if (si.sobel && si.l2) v = isqrt_round(s * s + s2 * s2);
+          else if (si.sobel) v = std::abs(s) + std::abs(s2);
           else if (si.div > 1) v = (s + si.div / 2) / si.div;  // s >= 0 for smoothing filters
           else v = s;
           v = sat(v);

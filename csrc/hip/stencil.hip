@@ -448,8 +448,26 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : 4)) void k_sep(KArgs a) {
         const i16x2 gx = as_i16x2(pair_at(w, WLO + 2 * pp + C)) - as_i16x2(pair_at(w, WLO + 2 * pp - C));
         const i16x2 gy = as_i16x2(pair_at(wd, WLO + 2 * pp - C)) + as_i16x2(pair_at(wd, WLO + 2 * pp + C)) +
                          (as_i16x2(pair_at(wd, WLO + 2 * pp)) << (short)1);
-        const i16x2 m = __builtin_elementwise_max(gx, -gx) + __builtin_elementwise_max(gy, -gy);
-        h[pp] = as_u32(__builtin_elementwise_min(m, (i16x2)(short)255));
+        if constexpr (F::L2) {
+          // round(sqrt(gx^2 + gy^2)) exactly: f32 sqrt lands within one of
+          // isqrt(n) (n < 2^21), two integer corrections make it exact, and the
+          // rounding is k + (n > k^2 + k) (sqrt(n) is never a half-integer)
+          uint32_t hv[2];
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int xg = gx[e], yg = gy[e];
+            const int n = xg * xg + yg * yg;
+            int k = (int)__builtin_sqrtf((float)n);
+            k -= k * k > n ? 1 : 0;
+            k += (k + 1) * (k + 1) <= n ? 1 : 0;
+            k += n > k * k + k ? 1 : 0;
+            hv[e] = (uint32_t)min(k, 255);
+          }
+          h[pp] = hv[0] | (hv[1] << 16);
+        } else {
+          const i16x2 m = __builtin_elementwise_max(gx, -gx) + __builtin_elementwise_max(gy, -gy);
+          h[pp] = as_u32(__builtin_elementwise_min(m, (i16x2)(short)255));
+        }
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) o[q] = __builtin_amdgcn_perm(h[2 * q + 1], h[2 * q], 0x06040200u);
@@ -893,6 +911,7 @@ void launch_stencil(const Pass& p, const PassConsts& pc, const PassLaunch& L, hi
     case StencilId::Sharpen: dev::launch_filter<Sharpen>(p, a, tiles, n0, n1, band, nt, s); break;
     case StencilId::Laplace: dev::launch_filter<Laplace>(p, a, tiles, n0, n1, band, nt, s); break;
     case StencilId::Sobel: dev::launch_filter<Sobel>(p, a, tiles, n0, n1, band, nt, s); break;
+    case StencilId::SobelL2: dev::launch_filter<SobelL2>(p, a, tiles, n0, n1, band, nt, s); break;
     case StencilId::Gaussian3: dev::launch_filter<Gaussian3>(p, a, tiles, n0, n1, band, nt, s); break;
     case StencilId::Gaussian5: dev::launch_filter<Gaussian5>(p, a, tiles, n0, n1, band, nt, s); break;
     case StencilId::Gaussian7: dev::launch_filter<Gaussian7>(p, a, tiles, n0, n1, band, nt, s); break;

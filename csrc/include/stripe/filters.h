@@ -44,6 +44,7 @@ enum class StencilId : int {
   Sharpen,
   Laplace,
   Sobel,
+  SobelL2,
   kCount
 };
 
@@ -52,7 +53,8 @@ struct StencilInfo {
   const char* name;
   int K;                 // window size (odd)
   bool separable;        // weights = w1 (x) w1
-  bool sobel;            // sat(|Gx|+|Gy|)
+  bool sobel;            // sat(|Gx|+|Gy|), or with l2: sat(round(sqrt(Gx^2 + Gy^2)))
+  bool l2 = false;
   int div;               // out = sat(floor((sum + div/2) / div)) (div==1: sat(sum))
   std::vector<int> w;    // K*K row-major [dy][dx] (correlation, like filter2D)
   std::vector<int> w1;   // separable 1-D taps

@@ -76,6 +76,14 @@ struct Sobel {
     return d[dy] * s[dx];
   }
   STRIPE_HD static constexpr int w(int dy, int dx) { return wx(dy, dx); }
+  static constexpr bool L2 = false;
+};
+
+// Sobel gradient magnitude: out = sat(round(sqrt(Gx^2 + Gy^2))), the L2 form of
+// SURVEY §2.7's "sobel (|Gx|+|Gy| or L2)".  sqrt of an integer is never a
+// half-integer, so the rounding is exact: round = k + (n > k^2 + k), k = isqrt(n).
+struct SobelL2 : Sobel {
+  static constexpr bool L2 = true;
 };
 
 // Separable integer smoothing filters: out = (sum + DIV/2) / DIV, sum >= 0.

@@ -39,6 +39,7 @@ FILTERS = {
     "sharpen": "[[0,-1,0],[-1,5,-1],[0,-1,0]]",
     "laplace": "[[0,1,0],[1,-4,1],[0,1,0]]",
     "sobel": "sat(|Gx| + |Gy|)",
+    "sobel_l2 / magnitude": "sat(round(sqrt(Gx^2 + Gy^2))), exact integer rounding",
     "blur:K[:sigma]": "KxK float Gaussian (MFMA implicit-GEMM path), K <= 33",
     "conv:K:w0;w1;...": "generic KxK float correlation (MFMA path)",
     "sepconv:K:h..:v..": "rank-one KxK float correlation v (x) h (separable MFMA path)",

@@ -80,10 +80,13 @@ def stencil(img, name, border="reflect101"):
     b = "reflect101" if skip else border
 
     def one(ch):
-        if name == "sobel":
+        if name in ("sobel", "sobel_l2"):
             gx = _correlate(ch, SOBEL_X, b)
             gy = _correlate(ch, SOBEL_X.T, b)
-            out = np.clip(np.abs(gx) + np.abs(gy), 0, 255)
+            if name == "sobel":
+                out = np.clip(np.abs(gx) + np.abs(gy), 0, 255)
+            else:  # double sqrt is correctly rounded and never lands on a half-integer
+                out = np.clip(np.rint(np.sqrt((gx.astype(np.int64) ** 2 + gy.astype(np.int64) ** 2).astype(np.float64))), 0, 255)
             R = 1
         else:
             w, div = STENCILS[name]

@@ -72,12 +72,12 @@ def test_invert_brightness_threshold(rng):
     assert (ops.apply(x, "threshold:100") == np.where(x >= 100, 255, 0)).all()
 
 
-@pytest.mark.parametrize("name", sorted(np_ref.STENCILS) + ["sobel"])
+@pytest.mark.parametrize("name", sorted(np_ref.STENCILS) + ["sobel", "sobel_l2"])
 @pytest.mark.parametrize("border", ["reflect101", "replicate", "constant", "skip"])
 @pytest.mark.parametrize("shape", SHAPES)
 def test_stencils(rng, name, border, shape):
     h, w = shape
-    R = 1 if name == "sobel" else np_ref.STENCILS[name][0].shape[0] // 2
+    R = 1 if name.startswith("sobel") else np_ref.STENCILS[name][0].shape[0] // 2
     if border == "reflect101" and (h < 2 or w < 2):
         pytest.skip("numpy reflect needs >= 2 samples")
     if border == "reflect101" and (h <= R or w <= R):

@@ -26,7 +26,7 @@ def _run(m, img, chain, border="reflect101"):
 
 SHAPES = [(1, 1), (3, 2), (17, 15), (64, 65), (37, 1365), (130, 4100), (9, 5000)]
 STENCILS = ["gaussian3", "gaussian5", "gaussian7", "box3", "box5", "emboss3", "emboss5", "sharpen", "laplace",
-            "sobel"]
+            "sobel", "sobel_l2"]
 
 
 @pytest.mark.parametrize("name", STENCILS)
@@ -43,7 +43,7 @@ def test_stencil_exact(m, rng, name, shape, C):
         assert bad.size == 0, f"{name} {border} {img.shape}: {len(bad)} mismatches, first {bad[:5].tolist()}"
 
 
-@pytest.mark.parametrize("name", ["emboss3", "emboss5", "gaussian5", "sobel"])
+@pytest.mark.parametrize("name", ["emboss3", "emboss5", "gaussian5", "sobel", "sobel_l2"])
 def test_skip_border(m, rng, name):
     img = rng.integers(0, 256, size=(45, 77), dtype=np.uint8)
     got = _run(m, img, f"{name}@skip")
