@@ -96,6 +96,23 @@ __device__ __forceinline__ uint32_t in_row_off(const KArgs& a, int y) {
   return a.in_org + (uint32_t)((int64_t)(g - a.row0) * a.in_pitch);
 }
 
+// True when input rows [y0, y1] of this wave's band need no border remap: the
+// hot loop then computes row offsets without the remap's scalar branch tree
+// (three scalar branches and the remap per row otherwise).
+__device__ __forceinline__ bool rows_inside(const KArgs& a, int y0, int y1) {
+  return a.row0 + y0 >= 0 && a.row0 + y1 < a.Hg;
+}
+
+// Offset of the input row feeding step y + ahead of a band ending at ye (rows
+// past the band re-read its last input row).  `inner` (wave-uniform): the
+// band's rows need no border remap (rows_inside) -> straight-line scalar math,
+// no branch tree; the remap stays for the edge bands.
+__device__ __forceinline__ uint32_t ahead_row_off(const KArgs& a, bool inner, int y, int ahead, int ye, int R,
+                                                  uint32_t last_row) {
+  if (inner) return a.in_org + (uint32_t)(min(y + ahead, ye - 1) + R) * (uint32_t)a.in_pitch;
+  return y + ahead < ye ? in_row_off(a, y + ahead + R) : last_row;
+}
+
 // Bijective XCD-aware remap of the workgroup index: the hardware hands
 // consecutive workgroups to the XCDs round-robin (blockIdx % 8 shares an L2),
 // so logical workgroup ranges are made contiguous per XCD: vertically /

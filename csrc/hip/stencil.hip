@@ -397,10 +397,11 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : 4)) void k_sep(KArgs a) {
 #pragma unroll
   for (int i = 0; i < kPF; ++i) load_raw<PRO>(rin, ys + i < ye ? in_row_off(a, ys + i + R) : last_row, lane_in, nx[i]);
 
+  const bool inner = rows_inside(a, ys - R, ye - 1 + R);
   auto row_step = [&](int y, const VState<F>& prev, VState<F>& next, RawChunk<PRO>& nb, bool valid) {
     uint32_t u[8], vv[8], dd[8];
     cook_pairs<PRO>(a, nb, luts, u);
-    load_raw<PRO>(rin, y + kPF < ye ? in_row_off(a, y + kPF + R) : last_row, lane_in, nb);
+    load_raw<PRO>(rin, ahead_row_off(a, inner, y, kPF, ye, R, last_row), lane_in, nb);
     if constexpr (F::SOBEL) {
       vpush_sobel<F>(u, prev, next, vv, dd);
       vb[2][lane] = make_uint4(dd[0], dd[1], dd[2], dd[3]);
@@ -615,12 +616,13 @@ __global__ __launch_bounds__(kNT, (F::K >= 5 ? 3 : 4)) void k_direct(KArgs a) {
 #pragma unroll
   for (int o = 0; o < K; ++o) load_raw<PRO>(rin, ys + o < ye ? in_row_off(a, ys + o + R) : last_row, lane_in, nx[o]);
 
+  const bool inner = rows_inside(a, ys - R, ye - 1 + R);
   for (int y = ys; y < ye; y += K) {
 #pragma unroll
     for (int o = 0; o < K; ++o) {
       const int yy = y + o;
       push(nx[o], ring[(o + K - 1) % K]);
-      load_raw<PRO>(rin, yy + K < ye ? in_row_off(a, yy + K + R) : last_row, lane_in, nx[o]);
+      load_raw<PRO>(rin, ahead_row_off(a, inner, yy, K, ye, R, last_row), lane_in, nx[o]);
       uint32_t h[8];
 #pragma unroll
       for (int pp = 0; pp < 8; ++pp) {
