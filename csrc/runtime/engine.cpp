@@ -721,19 +721,23 @@ void Engine::autotune_bands() {
     int best_band = 0;
     for (int b : cand) {
       prt_[i].band = b;
-      // median of 7 timed launches after one warmup: single launches of a
-      // 40-300 us kernel jitter by a few percent, about the gap between bands
+      // median over 5 timed bursts (after one warmup burst) of kBurst
+      // back-to-back launches: the steady state of an iterated run, where one
+      // launch's tail overlaps the next one's ramp (isolated launches favour
+      // taller bands by ~5 % on 20-90 us kernels); bursts of a 40-300 us kernel
+      // still jitter by a few percent, about the gap between bands
+      constexpr int kBurst = 4;
+      PassLaunch L = make_launch(p, origin(buf_[cur_], p.cin), origin(buf_[cur_ ^ 1], p.cout), (int)i);
+      L.band = b;
+      L.ry[0] = 0;
+      L.ry[1] = L.rows;
       std::vector<float> t;
-      for (int rep = 0; rep < 8; ++rep) {
-        PassLaunch L = make_launch(p, origin(buf_[cur_], p.cin), origin(buf_[cur_ ^ 1], p.cout), (int)i);
-        L.band = b;
-        L.ry[0] = 0;
-        L.ry[1] = L.rows;
+      for (int rep = 0; rep < 6; ++rep) {
         HIP_CHECK(hipEventRecord(e0, s_compute_));
-        launch_pass(p, prt_[i].pc, L, s_compute_);
+        for (int k = 0; k < kBurst; ++k) launch_pass(p, prt_[i].pc, L, s_compute_);
         HIP_CHECK(hipEventRecord(e1, s_compute_));
         HIP_CHECK(hipEventSynchronize(e1));
-        if (rep > 0) t.push_back(elapsed(e0, e1));
+        if (rep > 0) t.push_back(elapsed(e0, e1) / kBurst);
       }
       std::nth_element(t.begin(), t.begin() + t.size() / 2, t.end());
       const float med = t[t.size() / 2];

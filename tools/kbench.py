@@ -21,7 +21,7 @@ def main():
     ap.add_argument("--shape", default="16384x16384x3")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--bands", default="0", help="comma list of stencil band heights (0 = auto)")
+    ap.add_argument("--bands", default="0", help="comma list of stencil band heights (0 = static heuristic, -1 = engine autotune)")
     ap.add_argument("--no-fuse", action="store_true")
     ap.add_argument("--graphs", action="store_true", help="replay iterations from a captured hipGraph")
     a = ap.parse_args()
@@ -34,7 +34,8 @@ def main():
     for chain, band in [(c, int(b)) for c in (a.chains.split("|") if "|" in a.chains else a.chains.split(";")) if c for b in a.bands.split(",")]:
         pipe = Pipeline(chain, fuse=not a.no_fuse)
         cfg = pipe.config(W, H, Cc, "device", device=0)
-        cfg.band = band
+        cfg.band = max(band, 0)
+        cfg.autotune = band < 0
         cfg.graphs = a.graphs
         e = C.Engine(cfg)
         info = C.plan_info(chain, Cc)
@@ -55,7 +56,8 @@ def main():
         byts = sum(W * H * (p["cin"] + p["cout"]) for p in info["passes"])
         print(json.dumps({"chain": chain, "band": band, "shape": a.shape, "ms": round(ms, 4),
                           "mpx_s": round(W * H / ms / 1e3, 1), "GBps": round(byts / ms / 1e6, 1),
-                          "passes": len(info["passes"]), "graphs": e.graph_launches > 0}), flush=True)
+                          "passes": len(info["passes"]), "graphs": e.graph_launches > 0,
+                          "bands": e.bands}), flush=True)
         del e
 
 
