@@ -191,3 +191,24 @@ def test_multipass_chain_level_exchange_gpu(m, chain, ranks, depth, iters):
         pipe = m.Pipeline(chain, halo_depth=depth)
         res.append(C.run_local_group(pipe.config(W, H, 3, "device", device=0), nr, img, iters))
     assert (res[0] == res[1]).all()
+
+
+@pytest.mark.parametrize("chain", ["gaussian5", "sobel,emboss3", "gray:ref,contrast:3.5,emboss3"])
+def test_autotune_bands_keep_output_exact(m, chain):
+    """The band autotuner (engine.cpp autotune_bands: bursts of back-to-back
+    launches into the scratch buffer) picks a band per stencil pass from its
+    candidate set and leaves the run's result bit-exact vs the golden path."""
+    C = m._C
+    img = m.utils.synthetic_image(5, 640, 200, 3)
+    cfg = m.Pipeline(chain).config(640, 200, 3, "device", device=0, autotune=True)
+    e = C.Engine(cfg)
+    e.load_packed(np.ascontiguousarray(img))
+    e.run(1)
+    e.synchronize()
+    bands = e.bands
+    assert len(bands) == len(C.plan_info(chain, 3)["passes"])
+    assert all(b in (0, 8, 12, 16, 24, 32) for b in bands), bands
+    assert any(b > 0 for b in bands)
+    got = e.store_packed()
+    ref = C.golden_apply(img, chain, "reflect101", True)
+    assert (got == ref).all()
