@@ -219,10 +219,19 @@ Plan compile_chain(const std::vector<Op>& ops, int cin, Border default_border, b
   plan.in_margin_px = next_r;
   plan.in_margin_border = next_b;
   // a chain that maps C -> C can be iterated (ping-pong): the last pass then
-  // feeds the first one, so it must maintain the first pass's input margins
-  if (plan.cout == plan.cin && plan.passes.back().out_margin_px < plan.in_margin_px) {
-    plan.passes.back().out_margin_px = plan.in_margin_px;
-    plan.passes.back().out_margin_border = plan.in_margin_border;
+  // feeds the first one, so it must maintain the first pass's input margins.
+  // A pointwise pass maps its input margins byte by byte, so the contract
+  // walks back through the trailing pointwise passes to the last stencil/conv
+  // pass, which recomputes its output margins from its own pixels.
+  if (plan.cout == plan.cin && plan.in_margin_px > 0) {
+    for (int i = (int)plan.passes.size() - 1; i >= 0; --i) {
+      Pass& p = plan.passes[i];
+      if (p.out_margin_px < plan.in_margin_px) {
+        p.out_margin_px = plan.in_margin_px;
+        p.out_margin_border = plan.in_margin_border;
+      }
+      if (p.kind != PassKind::Pointwise) break;
+    }
   }
   plan.max_radius = 0;
   plan.max_channels = cin;

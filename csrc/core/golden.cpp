@@ -126,6 +126,10 @@ void golden_pass(const Pass& p, ConstView in, MutView out, int W, RowGeom g, int
     uint8_t* dst = out.origin + (int64_t)y * out.pitch;
     const int gy = g.row0 + y;
     for (int x = 0; x < W; ++x) {
+      // @skip: the reference processes o < x <= W-o, o < y <= H-o (kernel.cu:83).
+      // Deliberate deviation at x = W-o and y = H-o: there the reference's window
+      // reads column W (wrapping into the next row) or row H (past the buffer),
+      // so those pixels keep their input value here, like the rest of the frame.
       const bool skip = p.border == Border::Skip &&
                         (x <= R || gy <= R || x >= W - R || gy >= g.Hg - R);
       for (int c = 0; c < C; ++c) {

@@ -185,6 +185,7 @@ class Engine {
   void run_deep(int iterations);
   int depth_ = 0;                  // iterations per chain-level exchange (deep halo); 0: per-pass exchange
   void run_pipelined(int iterations);
+  void join_d2h();
   hipStream_t s_edge_ = nullptr;   // rim + boundary rows of the pipelined halo schedule
   hipEvent_t pev_[7] = {};         // core[2], rim[2], boundary, exchange, start
   void copy2d(void* dst, int64_t dpitch, const void* src, int64_t spitch, int64_t width, int64_t rows,

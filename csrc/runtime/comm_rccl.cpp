@@ -2,8 +2,10 @@
 // kernel.cu:137,223 and provides the halo exchange the reference lacks, Q6).
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <chrono>
 #include <cstring>
+#include <mutex>
 #include <thread>
 
 #include "stripe/comm.h"
@@ -32,10 +34,7 @@ class RcclComm final : public Comm {
     HIP_CHECK(hipMalloc(&bar_buf_, sizeof(int)));
   }
   ~RcclComm() override {
-    if (comm_) {
-      if (aborted_) ncclCommAbort(comm_);
-      else ncclCommDestroy(comm_);
-    }
+    if (comm_) ncclCommDestroy(comm_);  // an aborted communicator is already gone
     if (bar_buf_) (void)hipFree(bar_buf_);
     if (bar_stream_) (void)hipStreamDestroy(bar_stream_);
     (void)hipGetLastError();
@@ -45,21 +44,37 @@ class RcclComm final : public Comm {
   const char* backend() const override { return "rccl"; }
   bool device_buffers() const override { return true; }
   void group_start() override { NCCL_CHECK(ncclGroupStart()); }
+  // enqueue calls hold the lock, so a concurrent abort() never frees the
+  // communicator under them (group_end may block on peers: it does not)
   void send(const void* buf, size_t bytes, int peer, hipStream_t s) override {
-    STRIPE_CHECK(comm_ != nullptr, "RCCL communicator was aborted");
-    NCCL_CHECK(ncclSend(buf, bytes, ncclUint8, peer, comm_, s));
+    std::lock_guard<std::mutex> lk(mu_);
+    NCCL_CHECK(ncclSend(buf, bytes, ncclUint8, peer, live_locked(), s));
   }
   void recv(void* buf, size_t bytes, int peer, hipStream_t s) override {
-    STRIPE_CHECK(comm_ != nullptr, "RCCL communicator was aborted");
-    NCCL_CHECK(ncclRecv(buf, bytes, ncclUint8, peer, comm_, s));
+    std::lock_guard<std::mutex> lk(mu_);
+    NCCL_CHECK(ncclRecv(buf, bytes, ncclUint8, peer, live_locked(), s));
   }
   void group_end() override { NCCL_CHECK(ncclGroupEnd()); }
   void barrier() override {
-    STRIPE_CHECK(comm_ != nullptr, "RCCL communicator was aborted");
-    NCCL_CHECK(ncclAllReduce(bar_buf_, bar_buf_, 1, ncclInt32, ncclSum, comm_, bar_stream_));
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      NCCL_CHECK(ncclAllReduce(bar_buf_, bar_buf_, 1, ncclInt32, ncclSum, live_locked(), bar_stream_));
+    }
     wait(bar_stream_);
   }
-  void abort(const std::string&) override { aborted_ = true; }
+  // Collective abort (Q9), callable from any thread: ncclCommAbort stops this
+  // rank's queued RCCL kernels and proxy, and a wait() blocked in another
+  // thread (run_group aborts every rank of an in-process group when one
+  // fails) sees the flag and raises at once instead of running into
+  // STRIPE_COMM_TIMEOUT_S.  A second abort is a no-op.
+  void abort(const std::string& why) override {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (aborted_.load()) return;
+    why_ = why;
+    aborted_.store(true);
+    if (comm_) ncclCommAbort(comm_);
+    comm_ = nullptr;
+  }
 
   // Bounded wait: poll the stream and the communicator's asynchronous error
   // state; a peer that died or a transport error aborts the communicator and
@@ -69,35 +84,52 @@ class RcclComm final : public Comm {
     const auto t0 = std::chrono::steady_clock::now();
     const double limit = comm_timeout_s();
     for (int it = 0;; ++it) {
+      check_aborted();
       const hipError_t e = hipStreamQuery(s);
-      if (e == hipSuccess) return;
+      if (e == hipSuccess) {
+        check_aborted();  // kernels stopped by an abort also complete the stream
+        return;
+      }
       if (e != hipErrorNotReady) HIP_CHECK(e);
       (void)hipGetLastError();  // NotReady is not an error; keep the sticky state clean
-      if (comm_) {
+      {
+        std::lock_guard<std::mutex> lk(mu_);
         ncclResult_t ar = ncclSuccess;
-        ncclCommGetAsyncError(comm_, &ar);
+        if (comm_) ncclCommGetAsyncError(comm_, &ar);
         if (ar != ncclSuccess && ar != ncclInProgress) {
+          why_ = std::string("RCCL asynchronous error on rank ") + std::to_string(rank_) + ": " +
+                 ncclGetErrorString(ar);
+          aborted_.store(true);
           ncclCommAbort(comm_);
           comm_ = nullptr;
-          fail(std::string("RCCL asynchronous error on rank ") + std::to_string(rank_) + ": " +
-               ncclGetErrorString(ar) + " (communicator aborted)");
         }
       }
       const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       if (el > limit) {
-        if (comm_) ncclCommAbort(comm_);
-        comm_ = nullptr;
-        fail("rank " + std::to_string(rank_) + ": collective did not complete within " + std::to_string(limit) +
-             " s (STRIPE_COMM_TIMEOUT_S); communicator aborted");
+        abort("rank " + std::to_string(rank_) + ": collective did not complete within " + std::to_string(limit) +
+              " s (STRIPE_COMM_TIMEOUT_S)");
+        check_aborted();
       }
       if (it > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
   }
 
  private:
+  ncclComm_t live_locked() {  // caller holds mu_
+    if (aborted_.load()) fail("RCCL communicator of rank " + std::to_string(rank_) + " was aborted: " + why_);
+    return comm_;
+  }
+  void check_aborted() {
+    if (!aborted_.load()) return;
+    std::lock_guard<std::mutex> lk(mu_);
+    live_locked();
+  }
+
   ncclComm_t comm_ = nullptr;
   int rank_, world_, dev_;
-  bool aborted_ = false;
+  std::mutex mu_;                    // guards comm_ / why_ against a concurrent abort()
+  std::atomic<bool> aborted_{false};
+  std::string why_;
   hipStream_t bar_stream_ = nullptr;
   int* bar_buf_ = nullptr;
 };

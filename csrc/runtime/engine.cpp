@@ -176,6 +176,16 @@ Engine::~Engine() {
 
 void Engine::use_external_stream(hipStream_t s) {
   STRIPE_CHECK(device(), "external streams need the device backend");
+  if (s == s_compute_) return;
+  // Work already queued on the previous stream (this engine's run/store, whose
+  // ping-pong buffers the next call overwrites) must precede everything queued
+  // on the new one: an event on the old stream, waited on by the new stream.
+  // Every side stream (comm, edge, e2e) joins the compute stream at the end of
+  // each call, so the compute stream's tail covers them too.
+  if (s_compute_) {
+    HIP_CHECK(hipEventRecord(ev_[0], s_compute_));
+    HIP_CHECK(hipStreamWaitEvent(s, ev_[0], 0));
+  }
   if (own_compute_ && s_compute_) {
     HIP_CHECK(hipStreamSynchronize(s_compute_));
     HIP_CHECK(hipStreamDestroy(s_compute_));
@@ -201,7 +211,10 @@ const uint8_t* Engine::output_origin() const {
 
 RowGeom Engine::geom() const {
   const Stripe& st = stripe();
-  if (cfg_.halo) return RowGeom{st.row0, cfg_.H};
+  // a legacy split (Q7) processes only the covered rows H/N*N: with halo
+  // exchange those rows form the frame, so the last rank's bottom rows take the
+  // border rather than halo rows no neighbour fills
+  if (cfg_.halo) return RowGeom{st.row0, part_.legacy ? part_.covered_rows() : cfg_.H};
   return RowGeom{0, st.rows};  // legacy: each stripe is an image of its own
 }
 
@@ -943,6 +956,7 @@ void Engine::run_e2e(int chunks) {
     download(origin(buf_[out_buf_], cout), 0, rows);
     stage_end(Stage::D2H, s_d2h_);
     stage_end(Stage::E2E, s_d2h_);
+    join_d2h();
     return;
   }
   const Pass& p = plan_.passes[0];
@@ -1002,8 +1016,16 @@ void Engine::run_e2e(int chunks) {
   stage_end(Stage::Compute, s_compute_);
   stage_end(Stage::D2H, s_d2h_);
   stage_end(Stage::E2E, s_d2h_);
+  join_d2h();
   out_buf_ = 1;
   out_c_ = cout;
+}
+
+// Later work on the compute stream (and a stream switch) orders behind this
+// step's downloads: the compute stream's tail then covers every side stream.
+void Engine::join_d2h() {
+  HIP_CHECK(hipEventRecord(ev_[1], s_d2h_));
+  HIP_CHECK(hipStreamWaitEvent(s_compute_, ev_[1], 0));
 }
 
 void Engine::store_packed(void* dst, bool dst_device) {
@@ -1162,7 +1184,9 @@ Image run_group(const EngineConfig& cfg, const std::vector<Comm*>& comms, const 
     } catch (...) {
       std::lock_guard<std::mutex> lk(mu);
       if (!err) err = std::current_exception();
-      comms[r]->abort("rank " + std::to_string(r) + " failed");
+      // one process owns every rank: abort the whole group (Q9), so ranks
+      // blocked on this one fail at once instead of at the comm timeout
+      for (Comm* c : comms) c->abort("rank " + std::to_string(r) + " failed");
     }
   };
   std::vector<std::thread> th;

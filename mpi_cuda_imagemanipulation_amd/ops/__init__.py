@@ -80,6 +80,9 @@ def _engine(W, H, Cc, chain, border, fuse, device_index, halo=True):
         cfg.backend = C.Backend.device
         eng = C.Engine(cfg)
         eng._stream = None
+        # one call at a time per engine: the C++ calls release the GIL and the
+        # engine's ping-pong buffers are shared by every call with this key
+        eng._lock = threading.Lock()
         _engines[key] = eng
         while len(_engines) > _MAX_ENGINES:
             _engines.popitem(last=False)
@@ -97,14 +100,16 @@ def apply(image, chain: str, border: str = "reflect101", fuse: bool = True):
             x = x.reshape(H, W)
         eng = _engine(W, H, Cc, chain, border, fuse, x.device.index)
         stream = torch.cuda.current_stream(x.device).cuda_stream
-        if eng._stream != stream:
-            eng.use_external_stream(stream)
-            eng._stream = stream
-        eng.load_packed_ptr(x.data_ptr(), True)
-        eng.run(1)
         cout = eng.out_channels
         out = torch.empty((H, W) if cout == 1 else (H, W, cout), dtype=torch.uint8, device=x.device)
-        eng.store_packed_ptr(out.data_ptr(), True)
+        with eng._lock:
+            if eng._stream != stream:
+                # the new stream waits for the work still queued on the old one
+                eng.use_external_stream(stream)
+                eng._stream = stream
+            eng.load_packed_ptr(x.data_ptr(), True)
+            eng.run(1)
+            eng.store_packed_ptr(out.data_ptr(), True)
         # keep x alive until the stream has consumed it
         x.record_stream(torch.cuda.current_stream(x.device))
         return out

@@ -95,6 +95,8 @@ def stencil(img, name, border="reflect101"):
             out = np.clip((s + div // 2) // div if div > 1 else s, 0, 255)
         out = out.astype(np.uint8)
         if skip:
+            # kernel.cu:83 bounds minus its wrap/OOB column W-R and row H-R
+            # (deliberate deviation, README "Parity"): those keep the input too
             H, W = ch.shape
             yy, xx = np.mgrid[0:H, 0:W]
             m = (xx <= R) | (yy <= R) | (xx >= W - R) | (yy >= H - R)
