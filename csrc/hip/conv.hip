@@ -1,18 +1,35 @@
 // Large-kernel float convolution pass (conv:K:..., K up to 33, not rank one).
 //
-// Implicit im2col -> GEMM on MFMA.  For one kernel row ky and one 16-pixel
-// n-tile the output tile
-//   out[y0:y0+16, x0:x0+16] += In[y0+ky-R : +16, x0-R : x0-R+64] . T_ky[64 x 16]
-// is a real GEMM (M = 16 output rows, N = 16 output pixels, K = 64 window
-// pixels), where T_ky is the banded Toeplitz matrix of weight row ky
-// (T[k][n] = w[ky][k-n]), the same for every n-tile.  Channels are
-// de-interleaved into f16 planes in LDS so the band only couples pixels of one
-// channel.  u8 inputs are exact in f16; each weight is split into hi + lo f16
-// parts (two MFMAs) so the f32 accumulation sees ~2^-22 relative weight error:
-// results match the f64 golden to within 1 LSB (ties only).  Windows up to
-// 5x5 (7x7 gray) take the VALU direct kernel instead (stencil.hip).  The
-// reference has no large-window convolution (its only stencil is the 3x3/5x5
-// emboss, kernel.cu:64-94); this is SURVEY config 5's im2col -> MFMA path.
+// Implicit im2col -> GEMM on MFMA (mfma_f32_16x16x32_f16).  For one 16x16
+// output tile (M = 16 output rows, N = 16 output pixels of one channel) and a
+// PAIR of kernel rows (ky0 = 2p, ky1 = 2p + 1) the product's K dimension is
+// 96 = 3 k-steps of 32:
+//     k in [0, 48)  -> input row  m + ky0, window pixel k        (T_ky0 band)
+//     k in [48, 96) -> input row  m + ky1, window pixel k - 48   (T_ky1 band)
+//   out[m][n] += A[m][k] . B[k][n],   B[k][n] = w[ky][col(k) - n]
+// A 16-pixel n-tile only needs a 16 + K - 1 <= 48 pixel window per kernel row,
+// so pairing rows packs two 48-wide windows into 3 k-steps: 1.5 MFMAs per
+// kernel row and weight part instead of the 2 of a 64-wide window per row
+// (K = 31: 96 instead of 124 MFMAs per tile).
+//
+// Data flow per workgroup (4 waves; 16*MT output rows x 64 pixels x C channels):
+//   * the input window [(16 MT + 2 np) rows][96 px] is staged ONCE into f16
+//     channel planes in LDS (u8 is exact in f16); the plane row stride is
+//     224 B, which makes every A-fragment ds_read_b128 conflict-free (the 16
+//     lanes of each b128 lane group hit 16 distinct 4-bank quads for all three
+//     k-step address patterns: quad = -2 m + g (+ const) mod 16);
+//   * a pair's B fragments (3 k-steps x weight hi + lo, 6 KiB) are DMA'd from
+//     L2 into an LDS ring once per workgroup, one pair ahead, and each
+//     fragment read feeds C x MT x 2 MFMAs (RGB, MT = 4: 24 MFMAs = 384
+//     cycles); the previous layout re-read the Toeplitz stream from L2 for
+//     every wave and every channel (12x the traffic).
+// Precision: each weight is split into f16 hi + lo parts (two MFMAs), so the
+// f32 accumulation sees ~2^-22 relative weight error: results match the f64
+// golden to within 1 LSB (ties only).  Windows up to 5x5 (7x7 gray) take the
+// VALU direct kernel instead (stencil.hip); rank-one windows (blur:K,
+// sepconv) the separable MFMA kernel (blur_sep.hip).  The reference has no
+// large-window convolution (its only stencil is the 3x3/5x5 emboss,
+// kernel.cu:64-94); this is SURVEY config 5's im2col -> MFMA path.
 #include "dev_common.h"
 #include "stripe/kernels.h"
 
@@ -26,52 +43,74 @@ typedef float float4v __attribute__((ext_vector_type(4)));
 
 struct ConvArgs {
   KArgs a;
-  const _Float16* tw;  // Toeplitz B fragments: [K][hilo 2][kstep 2][lane 64][8]
-  int K, R;
+  const half8* tw;  // B fragments: [pair][kstep 3][hilo 2][lane 64]
+  int K, R, np;     // kernel size, radius, kernel-row pairs
 };
 
-constexpr int kCTN = 64;          // output pixels per workgroup (4 waves x 16)
-constexpr int kCTK = 64;          // Toeplitz window per 16-pixel n-tile (2 k-steps x 32)
-constexpr int kCWin = 48 + kCTK;  // staged pixels per row: every wave's full 64-pixel window
-                                  // (the zero-weight tail is multiplied too: it must hold
-                                  // finite values, not stale LDS that may read as NaN)
-constexpr int kCTKP = kCWin + 8;  // LDS row stride (halves): 240 B rows spread the banks
-constexpr int kConvWaves = 4;     // waves per workgroup
-constexpr int kConvMT = 3;        // 16-row m-tiles per wave (each B fragment feeds 3 MFMAs;
-                                  // 3 planes x (48 + 32) rows x 240 B stays under 64 KiB)
-constexpr int kConvRowsPerBlock = 16 * kConvMT;  // 48 output rows
+constexpr int kCTN = 64;         // output pixels per workgroup (4 waves x 16)
+constexpr int kCWin = kCTN + 32;  // staged pixels per row (each wave's 48-pixel window)
+constexpr int kCPS = 112;        // LDS plane row stride in halves (224 B: conflict-free A reads)
+constexpr int kConvWaves = 4;
 
-// One workgroup: 48 output rows x 64 output pixels x all channels.  The input
-// window [(48 + K - 1) rows][112 px] is staged once for every channel
-// plane (dword loads of the interleaved row, de-interleaved into f16 planes);
-// wave w owns output pixels [16 w, 16 w + 16) of every row, so each Toeplitz B
-// fragment it streams from L2 feeds three MFMAs (one per 16-row m-tile).
+// m-tiles (16 rows) per wave: RGB 4 (3 planes x 96 rows x 224 B = 64.5 KiB
+// + 12 KiB B ring, two workgroups per CU), gray 8 (one plane, 160 rows + the
+// ring = 47 KiB, three per CU)
 template <int C>
-__global__ __launch_bounds__(256) void k_conv_mfma(ConvArgs ca) {
-  const KArgs& a = ca.a;
-  const int K = ca.K, R = ca.R;
-  extern __shared__ __attribute__((aligned(16))) _Float16 plane[];  // [C][rows_in][kCTKP]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int x0 = blockIdx.x * kCTN;                       // first output pixel
-  const int yb = a.ry0 + blockIdx.y * kConvRowsPerBlock;  // first output row of block
-  if (yb >= a.ry1) return;
-  const int rows_in = kConvRowsPerBlock + K - 1;
-  const int win = kCWin;  // staged pixels per row
-  // plane stride padded by 12 dwords so the three planes' writes of one pixel
-  // land in different LDS banks
-  const int plane_sz = rows_in * kCTKP + 24;
+constexpr int conv_mt() { return C == 3 ? 4 : 8; }
 
-  // ---- stage: pixels [x0 - R, x0 - R + kCWin) of rows yb - R .. (dword loads) ----
-  // A lane loads dwords q = lane and lane + 64 of every row; which plane slot
-  // each of their bytes lands in is the same for every row, so it is computed
-  // once, and each wave walks its own rows with a wave-uniform (scalar) row
-  // offset: ~10 VALU per staged dword.
+// B fragments travel global -> LDS by LDS-DMA (global_load_lds_dwordx4, no
+// register destination), one pair ahead, into a 2-slot ring shared by the
+// workgroup's 4 waves: each (pair, k-step, hi/lo) fragment set is one 1 KiB
+// wave-instruction, so the LDS image is lane-linear and every wave reads its
+// fragment with one conflict-free ds_read_b128.  A register ring was tried
+// first: hipcc folds a loop-carried ring of plain loads into one load at the
+// top of the consuming iteration, and sinks buffer-load prefetches to the end
+// of the producing one behind a vmcnt(0) for the loop-carried copies; both
+// stalled every k-step on an L2 round trip.
+constexpr int kBPair = 6 * 1024;  // bytes of one pair's B fragments (3 k-steps x hi/lo x 1 KiB)
+
+__device__ __forceinline__ void load_b_pair(const uint8_t* tw, int p, uint8_t* slot, int wave, int lane) {
+  // 6 chunks over 4 waves, 2 per wave (waves 2, 3 duplicate chunks 4, 5 with
+  // identical bytes), so every wave counts the same number of DMA loads
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = i == 0 ? wave : (wave < 2 ? wave + 4 : wave + 2);
+    __builtin_amdgcn_global_load_lds((const void*)(tw + (size_t)p * kBPair + c * 1024 + 16 * lane),
+                                     (__attribute__((address_space(3))) void*)(slot + c * 1024), 16, 0, 0);
+  }
+}
+
+// LDS caps residency at 2 (RGB) / 3 (gray) workgroups per CU: tell the
+// compiler, or it trims registers for occupancy it can never get and sinks the
+// B prefetch / serialises the A-fragment reads (one ds_read in flight).
+template <int C, int MT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 3 ? 2 : 3, C == 3 ? 2 : 3)))
+void k_conv_mfma(ConvArgs ca) {
+  const KArgs& a = ca.a;
+  const int R = ca.R, np = ca.np;
+  extern __shared__ __attribute__((aligned(16))) _Float16 plane[];  // [C][rows_in][kCPS]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int x0 = blockIdx.x * kCTN;                 // first output pixel
+  const int yb = a.ry0 + blockIdx.y * (16 * MT);    // first output row
+  if (yb >= a.ry1) return;
+  const int rows_in = 16 * MT + 2 * np;             // >= 16 MT + K - 1 (+1 zero-weight row for odd K)
+  const int pstride = rows_in * kCPS;
+
+  // pair 0's B fragments; the staging barrier below retires them (vmcnt(0))
+  load_b_pair(reinterpret_cast<const uint8_t*>(ca.tw), 0, reinterpret_cast<uint8_t*>(plane + C * pstride), wave,
+              lane);
+
+  // ---- stage pixels [x0 - R, x0 - R + kCWin) of input rows yb - R .. (dword loads) ----
+  // A lane loads dwords q = lane and lane + 64 of a row; which plane slot each
+  // byte lands in is the same for every row, so it is computed once and each
+  // wave walks its rows with a wave-uniform (scalar) row offset.
   {
     const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);
-    const int b0 = (x0 - R) * C;                // first window byte (margins hold the x-border)
-    const int b0a = b0 & ~3;                    // dword-aligned start
+    const int b0 = (x0 - R) * C;  // first window byte (the x-margins hold the border)
+    const int b0a = b0 & ~3;
     const int lead = b0 - b0a;
-    const int nd = (lead + win * C + 3) / 4;    // dwords per row (<= 84 for C = 3)
+    const int nd = (lead + kCWin * C + 3) / 4;  // dwords per row (<= 74 for C = 3)
     int dst[2][4];
 #pragma unroll
     for (int qi = 0; qi < 2; ++qi)
@@ -79,85 +118,143 @@ __global__ __launch_bounds__(256) void k_conv_mfma(ConvArgs ca) {
       for (int e = 0; e < 4; ++e) {
         const int q = lane + 64 * qi;
         const int bi = 4 * q + e - lead;  // byte index within the window
-        dst[qi][e] = (q < nd && bi >= 0 && bi < win * C) ? (bi % C) * plane_sz + bi / C : -1;
+        dst[qi][e] = (q < nd && bi >= 0 && bi < kCWin * C) ? (bi % C) * pstride + bi / C : -1;
       }
-    for (int r = wave; r < rows_in; r += kConvWaves) {
-      // rows past the range's last needed input row (ry1 - 1 + R) feed only
-      // outputs that are not stored; clamp so no read leaves the stripe + halo
-      const int y = min(yb - R + r, a.ry1 - 1 + R);
-      const uint32_t roff = in_row_off(a, y) + (uint32_t)b0a;
+    // every row of the wave in one batch: all loads are issued before the
+    // first LDS write, so staging costs one memory latency, not one per row
+    // (8-row batches measured 0.549 ms vs 0.684 ms for row-by-row on conv:31;
+    // rows_in <= 16 MT + 34)
+    constexpr int kSB = (16 * MT + 34 + kConvWaves - 1) / kConvWaves;
+    constexpr int NQ = C == 3 ? 2 : 1;  // dwords per lane per row
+    for (int rb = wave; rb < rows_in; rb += kConvWaves * kSB) {
+      uint32_t d[kSB][NQ];
 #pragma unroll
-      for (int qi = 0; qi < 2; ++qi) {
-        const int q = lane + 64 * qi;
-        // bytes past the allocation read as 0 (range check); they feed only x >= W
-        const uint32_t d = __builtin_amdgcn_raw_buffer_load_b32(rin, roff + 4u * (uint32_t)q, 0, 0);
+      for (int i = 0; i < kSB; ++i) {
+        // rows past the range's last needed input row (ry1 - 1 + R) feed only
+        // outputs that are not stored (or zero weights): clamp so no read
+        // leaves the stripe + halo; they must still hold finite values
+        const int y = min(yb - R + rb + kConvWaves * i, a.ry1 - 1 + R);
+        const uint32_t roff = in_row_off(a, y) + (uint32_t)b0a;
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (dst[qi][e] >= 0) plane[dst[qi][e] + r * kCTKP] = (_Float16)(float)((d >> (8 * e)) & 0xFFu);
+        for (int qi = 0; qi < NQ; ++qi)
+          // bytes past the allocation read as 0 (range check); they feed only x >= W
+          d[i][qi] = __builtin_amdgcn_raw_buffer_load_b32(rin, roff + 4u * (uint32_t)(lane + 64 * qi), 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < kSB; ++i) {
+        const int r = rb + kConvWaves * i;
+        if (r >= rows_in) break;  // wave-uniform
+#pragma unroll
+        for (int qi = 0; qi < NQ; ++qi)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (dst[qi][e] >= 0)
+              plane[dst[qi][e] + r * kCPS] = (_Float16)(float)((d[i][qi] >> (8 * e)) & 0xFFu);
       }
     }
   }
   __syncthreads();
 
-  const int mrow = lane & 15;      // A row (output row within an m-tile)
-  const int kq = (lane >> 4) * 8;  // A k offset within a 32-step
-  for (int c = 0; c < C; ++c) {
-    const _Float16* pl = plane + c * plane_sz + 16 * wave;  // n-tile window start
-    float4v acc[kConvMT];
+  // ---- per-lane A offsets (halves) of the three k-steps of a row pair ----
+  // A layout: lane l holds A[m = l & 15][k = 32 s + 8 (l >> 4) + j], j = 0..7
+  const int m = lane & 15, g = lane >> 4;
+  int aoff[3];
+  aoff[0] = m * kCPS + 8 * g;                                               // ky0, px 0..31
+  aoff[1] = g < 2 ? m * kCPS + 32 + 8 * g : (m + 1) * kCPS + 8 * (g - 2);  // ky0 32..47 | ky1 0..15
+  aoff[2] = (m + 1) * kCPS + 16 + 8 * g;                                    // ky1, px 16..47
 #pragma unroll
-    for (int mt = 0; mt < kConvMT; ++mt) acc[mt] = float4v{0.f, 0.f, 0.f, 0.f};
-    for (int ky = 0; ky < K; ++ky) {
+  for (int s = 0; s < 3; ++s) aoff[s] += 16 * wave;
+
+  float4v acc[C][MT];
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        half8 bfrag[2];
+  for (int c = 0; c < C; ++c)
 #pragma unroll
-        for (int hl = 0; hl < 2; ++hl)
-          bfrag[hl] = *reinterpret_cast<const half8*>(ca.tw + (((size_t)ky * 2 + hl) * 2 + ks) * 512 + lane * 8);
+    for (int mt = 0; mt < MT; ++mt) acc[c][mt] = float4v{0.f, 0.f, 0.f, 0.f};
+
+  // B ring: pair p in slot p & 1; the DMA for pair p + 1 runs while pair p
+  // computes, and the barrier at the end of each pair both publishes it and
+  // frees slot p & 1 for pair p + 2
+  uint8_t* bring = reinterpret_cast<uint8_t*>(plane + C * pstride);
+  const uint8_t* tw = reinterpret_cast<const uint8_t*>(ca.tw);
+
+  for (int p = 0; p < np; ++p) {
+    if (p + 1 < np) load_b_pair(tw, p + 1, bring + ((p + 1) & 1) * kBPair, wave, lane);
+    const _Float16* pl = plane + 2 * p * kCPS;
+    const uint8_t* bslot = bring + (p & 1) * kBPair + 16 * lane;
+    // fragments of k-step s + 1 are read while k-step s multiplies (the
+    // sched barriers pin that order: left alone, hipcc issues two reads at a
+    // time and waits lgkmcnt(0) before every MFMA pair)
+    half8 af[2][C][MT], bf[2][2];
+    auto read_step = [&](int s, int buf) __attribute__((always_inline)) {
+      bf[buf][0] = *reinterpret_cast<const half8*>(bslot + (2 * s) * 1024);
+      bf[buf][1] = *reinterpret_cast<const half8*>(bslot + (2 * s + 1) * 1024);
 #pragma unroll
-        for (int mt = 0; mt < kConvMT; ++mt) {
-          const half8 afrag = *reinterpret_cast<const half8*>(pl + (16 * mt + mrow + ky) * kCTKP + ks * 32 + kq);
-          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(afrag, bfrag[0], acc[mt], 0, 0, 0);
-          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(afrag, bfrag[1], acc[mt], 0, 0, 0);
+      for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+          af[buf][c][mt] = *reinterpret_cast<const half8*>(pl + c * pstride + aoff[s] + 16 * mt * kCPS);
+    };
+    read_step(0, 0);
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const int cur = s & 1;
+      if (s < 2) read_step(s + 1, cur ^ 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          acc[c][mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[cur][c][mt], bf[cur][0], acc[c][mt], 0, 0, 0);
+          acc[c][mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[cur][c][mt], bf[cur][1], acc[c][mt], 0, 0, 0);
         }
-      }
+      __builtin_amdgcn_sched_barrier(0);
     }
-    // C/D layout: col = lane & 15, row = (lane >> 4) * 4 + reg
-    const int x = x0 + 16 * wave + (lane & 15);
-#pragma unroll
-    for (int mt = 0; mt < kConvMT; ++mt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int y = yb + 16 * mt + (lane >> 4) * 4 + r;
-        if (y < a.ry1 && x < a.W)  // v_cvt_pk_u8_f32: round half even + saturate (the golden's nearbyint)
-          a.out[(int64_t)y * a.out_pitch + (int64_t)x * C + c] = (uint8_t)__builtin_amdgcn_cvt_pk_u8_f32(acc[mt][r], 0, 0u);
-      }
+    __syncthreads();  // vmcnt(0): pair p + 1 landed (every wave); slot p & 1 read by every wave
   }
+
+  // ---- epilogue: C/D layout col = lane & 15, row = 4 (lane >> 4) + r ----
+  // v_cvt_pk_u8_f32: round half even + saturate (the golden's nearbyint + sat)
+  const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
+  const int x = x0 + 16 * wave + m;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int y = yb + 16 * mt + 4 * g + r;
+      const uint32_t off = (y < a.ry1 && x < a.W)
+                               ? a.out_org + (uint32_t)((int64_t)y * a.out_pitch) + (uint32_t)(x * C)
+                               : kOOB;
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)__builtin_amdgcn_cvt_pk_u8_f32(acc[c][mt][r], 0, 0u), rout,
+                                             off + (uint32_t)c, 0, 0);
+    }
 }
 
 }  // namespace dev
 
-// T_ky[k][n] = w[ky][k - n] for 0 <= k - n < K (k: window pixel, n: output pixel),
-// laid out as MFMA B fragments (lane l holds B[k = 8(l>>4)+j][n = l&15], j = 0..7).
+// B fragments: pair p, k-step s, part hl, lane l (g = l >> 4, n = l & 15),
+// element j: k = 32 s + 8 g + j -> (kernel row 2p + (k >= 48), window pixel
+// k mod 48); B[k][n] = w[ky][px - n] for 0 <= px - n < K, else 0.
 void prepare_conv_consts(const Pass& p, PassConsts* pc, hipStream_t s) {
   if (sep_supported(p)) return prepare_sep_consts(p, pc, s);
   const int K = p.K;
-  STRIPE_CHECK(K - 1 + 16 <= dev::kCTK && K <= 33,
-               "conv K=" << K << " exceeds the 64-pixel Toeplitz window");
-  std::vector<_Float16> host((size_t)K * 2 * 2 * 512);
-  for (int ky = 0; ky < K; ++ky)
-    for (int hl = 0; hl < 2; ++hl)
-      for (int ks = 0; ks < 2; ++ks)
+  STRIPE_CHECK(K >= 1 && K <= 33, "conv K=" << K << " exceeds the 48-pixel Toeplitz window");
+  const int np = (K + 1) / 2;
+  std::vector<_Float16> host((size_t)np * 3 * 2 * 64 * 8);
+  for (int pr = 0; pr < np; ++pr)
+    for (int ks = 0; ks < 3; ++ks)
+      for (int hl = 0; hl < 2; ++hl)
         for (int l = 0; l < 64; ++l)
           for (int j = 0; j < 8; ++j) {
-            const int k = ks * 32 + 8 * (l >> 4) + j;  // window pixel
-            const int n = l & 15;                      // output pixel of the n-tile
-            const int d = k - n;
+            const int k = 32 * ks + 8 * (l >> 4) + j;
+            const int ky = 2 * pr + (k >= 48 ? 1 : 0);
+            const int d = (k % 48) - (l & 15);
             float w = 0.f;
-            if (d >= 0 && d < K) w = p.conv_w[(size_t)ky * K + d];
+            if (ky < K && d >= 0 && d < K) w = p.conv_w[(size_t)ky * K + d];
             const _Float16 whi = (_Float16)w;
             const float rem = w - (float)whi;
-            const _Float16 v = hl == 0 ? whi : (_Float16)rem;
-            host[((((size_t)ky * 2 + hl) * 2 + ks) * 64 + l) * 8 + j] = v;
+            host[((((size_t)pr * 3 + ks) * 2 + hl) * 64 + l) * 8 + j] = hl == 0 ? whi : (_Float16)rem;
           }
   pc->conv_bytes = host.size() * sizeof(_Float16);
   HIP_CHECK(hipMalloc(&pc->conv, pc->conv_bytes));
@@ -184,6 +281,13 @@ void launch_conv(const Pass& p, const PassConsts& pc, const PassLaunch& L, hipSt
 // Banded-Toeplitz MFMA convolution for windows beyond the direct kernel's reach.
 void launch_conv_mfma(const Pass& p, const PassConsts& pc, const PassLaunch& L, hipStream_t s) {
   STRIPE_CHECK(pc.conv != nullptr, "conv pass constants not prepared");
+  STRIPE_CHECK(p.cmid == 1 || p.cmid == 3, "MFMA conv supports 1 or 3 channels");
+  STRIPE_CHECK(p.K >= 1 && p.K <= 33 && p.R * p.cmid <= kMarginBytes, "MFMA conv window too large");
+  STRIPE_CHECK(L.in_base && L.in_bytes > 0 && L.in_bytes < (int64_t)dev::kOOB && L.out_base && L.out_bytes > 0 &&
+                   L.out_bytes < (int64_t)dev::kOOB,
+               "conv launch needs the allocation view (< 2 GiB buffers)");
+  STRIPE_CHECK(L.in_org >= kMarginBytes && L.out_org >= kMarginBytes && L.in_zero >= kMarginBytes,
+               "bad origin offsets");
   dev::ConvArgs ca{};
   dev::KArgs& a = ca.a;
   a.in = L.in;
@@ -197,23 +301,28 @@ void launch_conv_mfma(const Pass& p, const PassConsts& pc, const PassLaunch& L, 
   a.row0 = L.row0;
   a.Hg = L.Hg;
   a.border = (int)p.border;
-  ca.tw = reinterpret_cast<const _Float16*>(pc.conv);
-  ca.K = p.K;
-  ca.R = p.R;
-  const size_t lds = (size_t)p.cmid * ((dev::kConvRowsPerBlock + p.K - 1) * dev::kCTKP + 24) * sizeof(_Float16);
-  STRIPE_CHECK(L.in_base && L.in_bytes > 0 && L.in_bytes < (int64_t)dev::kOOB, "conv launch needs the allocation view");
   a.in_base = L.in_base;
   a.in_bytes = (uint32_t)L.in_bytes;
   a.in_org = (uint32_t)L.in_org;
   a.in_zero = (uint32_t)L.in_zero;
+  a.out_base = L.out_base;
+  a.out_bytes = (uint32_t)L.out_bytes;
+  a.out_org = (uint32_t)L.out_org;
+  ca.tw = reinterpret_cast<const dev::half8*>(pc.conv);
+  ca.K = p.K;
+  ca.R = p.R;
+  ca.np = (p.K + 1) / 2;
+  const int mt = p.cmid == 3 ? dev::conv_mt<3>() : dev::conv_mt<1>();
+  const int rows_in = 16 * mt + 2 * ca.np;
+  const size_t lds = (size_t)p.cmid * rows_in * dev::kCPS * sizeof(_Float16) + 2 * dev::kBPair;
   for (int r = 0; r < L.nrange; ++r) {
     const int y0 = L.ry[2 * r], y1 = L.ry[2 * r + 1];
     if (y1 <= y0) continue;
     a.ry0 = y0;
     a.ry1 = y1;
-    dim3 grid((unsigned)div_up(L.W, dev::kCTN), (unsigned)div_up(y1 - y0, dev::kConvRowsPerBlock));
-    if (p.cmid == 3) dev::k_conv_mfma<3><<<grid, 256, lds, s>>>(ca);
-    else dev::k_conv_mfma<1><<<grid, 256, lds, s>>>(ca);
+    const dim3 grid((unsigned)div_up(L.W, dev::kCTN), (unsigned)div_up(y1 - y0, 16 * mt));
+    if (p.cmid == 3) dev::k_conv_mfma<3, dev::conv_mt<3>()><<<grid, 256, lds, s>>>(ca);
+    else dev::k_conv_mfma<1, dev::conv_mt<1>()><<<grid, 256, lds, s>>>(ca);
     HIP_CHECK(hipGetLastError());
   }
 }

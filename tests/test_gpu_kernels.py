@@ -104,6 +104,23 @@ def test_mfma_sep_matches_general_conv(m, rng):
     assert np.abs(a.astype(int) - b.astype(int)).max() <= 1
 
 
+@pytest.mark.parametrize("K", [7, 9, 15, 31, 33])
+@pytest.mark.parametrize("C", [1, 3])
+@pytest.mark.parametrize("shape", [(1, 1), (37, 61), (150, 333), (70, 1100)])
+def test_mfma_general_conv(m, rng, K, C, shape):
+    # non-separable random weights through the Toeplitz MFMA kernel (paired
+    # kernel rows in the K dimension); asymmetric, so a transposed or mirrored
+    # fragment map, a wrong row pairing or a wrong channel plane shows up
+    w = rng.uniform(-0.5, 1.0, (K, K))
+    w /= w.sum()
+    img = rng.integers(0, 256, size=shape + (C,) if C == 3 else shape, dtype=np.uint8)
+    for border in ("reflect101", "constant"):
+        got = m.ops.conv2d(torch.from_numpy(img).cuda(), w, border).cpu().numpy()
+        ref = m.ops.conv2d(img, w, border)
+        d = np.abs(got.astype(int) - ref.astype(int))
+        assert d.max() <= 1 and (d == 0).mean() > 0.99, (K, C, shape, border, d.max(), (d == 0).mean())
+
+
 def test_mfma_conv_asymmetric_weights(m, rng):
     # asymmetric kernel catches transposed fragment layouts
     K = 5

@@ -54,7 +54,7 @@ def main():
         n = iters * max(1, a.iters // iters)
         ms = (t1 - t0) * 1e3 / n
         byts = sum(W * H * (p["cin"] + p["cout"]) for p in info["passes"])
-        print(json.dumps({"chain": chain, "band": band, "shape": a.shape, "ms": round(ms, 4),
+        print(json.dumps({"chain": chain if len(chain) <= 48 else chain[:40] + "...", "band": band, "shape": a.shape, "ms": round(ms, 4),
                           "mpx_s": round(W * H / ms / 1e3, 1), "GBps": round(byts / ms / 1e6, 1),
                           "passes": len(info["passes"]), "graphs": e.graph_launches > 0,
                           "bands": e.bands}), flush=True)
