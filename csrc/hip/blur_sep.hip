@@ -215,14 +215,19 @@ __global__ __launch_bounds__(kSepWaves * 64, 2) void k_blur_sep(SepArgs sa) {
     for (int j = 0; j < kSepNJ; ++j) {
       // horizontal: X tiles 2k (rows 0..15 of the pair) and 2k+1 (16..31), column j
       f4 x0 = {0.f, 0.f, 0.f, 0.f}, x1 = {0.f, 0.f, 0.f, 0.f};
+      half8 f0[KSH], f1[KSH];
 #pragma unroll
       for (int s = 0; s < KSH; ++s) {
-        const half8 f0 = *reinterpret_cast<const half8*>(frag_base + 32 * (j + 2 * s));
-        const half8 f1 = *reinterpret_cast<const half8*>(frag_base + 16 * kSepRow + 32 * (j + 2 * s));
-        x0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(f0, bh[s][0], x0, 0, 0, 0);
-        x1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(f1, bh[s][0], x1, 0, 0, 0);
-        x0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(f0, bh[s][1], x0, 0, 0, 0);
-        x1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(f1, bh[s][1], x1, 0, 0, 0);
+        f0[s] = *reinterpret_cast<const half8*>(frag_base + 32 * (j + 2 * s));
+        f1[s] = *reinterpret_cast<const half8*>(frag_base + 16 * kSepRow + 32 * (j + 2 * s));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s = 0; s < KSH; ++s) {
+        x0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(f0[s], bh[s][0], x0, 0, 0, 0);
+        x1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(f1[s], bh[s][0], x1, 0, 0, 0);
+        x0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(f0[s], bh[s][1], x0, 0, 0, 0);
+        x1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(f1[s], bh[s][1], x1, 0, 0, 0);
       }
       // accumulator layout -> A operand of the vertical product (k = X row, permuted)
       uint32_t h[4], l[4];
