@@ -58,6 +58,13 @@ constexpr int kConvWaves = 4;
 template <int C>
 constexpr int conv_mt() { return C == 3 ? 4 : 8; }
 
+// Staged input rows per plane: 16 MT + 2 np rounded up to whole staging
+// groups (3 rows per wave-instruction for RGB, 9 for gray; see the staging loop)
+template <int C, int MT>
+__host__ __device__ constexpr int conv_rows_staged(int np) {
+  return (16 * MT + 2 * np + (C == 3 ? 3 : 9) - 1) / (C == 3 ? 3 : 9) * (C == 3 ? 3 : 9);
+}
+
 // B fragments travel global -> LDS by LDS-DMA (global_load_lds_dwordx4, no
 // register destination), one pair ahead, into a 2-slot ring shared by the
 // workgroup's 4 waves: each (pair, k-step, hi/lo) fragment set is one 1 KiB
@@ -94,63 +101,65 @@ void k_conv_mfma(ConvArgs ca) {
   const int x0 = blockIdx.x * kCTN;                 // first output pixel
   const int yb = a.ry0 + blockIdx.y * (16 * MT);    // first output row
   if (yb >= a.ry1) return;
-  const int rows_in = 16 * MT + 2 * np;             // >= 16 MT + K - 1 (+1 zero-weight row for odd K)
+  const int rows_in = conv_rows_staged<C, MT>(np);  // >= 16 MT + K - 1 (+1 zero-weight row for odd K)
   const int pstride = rows_in * kCPS;
 
   // pair 0's B fragments; the staging barrier below retires them (vmcnt(0))
   load_b_pair(reinterpret_cast<const uint8_t*>(ca.tw), 0, reinterpret_cast<uint8_t*>(plane + C * pstride), wave,
               lane);
 
-  // ---- stage pixels [x0 - R, x0 - R + kCWin) of input rows yb - R .. (dword loads) ----
-  // A lane loads dwords q = lane and lane + 64 of a row; which plane slot each
-  // byte lands in is the same for every row, so it is computed once and each
-  // wave walks its rows with a wave-uniform (scalar) row offset.
+  // ---- stage pixels [x0 - R, x0 - R + kCWin) of input rows yb - R .. ----
+  // 16-byte chunks: a row's window (from its 16-byte aligned start) is NCH
+  // chunks, so one wave-instruction loads RPI rows (lane -> row rr, chunk ch).
+  // Where each of a lane's 16 bytes lands (plane, column) is the same for
+  // every row, so it is computed once; bytes outside the window (the lead, the
+  // tail, idle lanes, rows past the staged block) are written to the unused
+  // padding column kCWin of plane 0, so the byte loop has no branches.
+  // (The dword-per-lane version with a branch per byte was instruction-bound:
+  // 0.136 ms of a 0.50 ms conv:31 stripe pass with the MFMA loop removed.)
   {
     const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);
+    constexpr int NCH = C == 3 ? 19 : 7;  // ceil((15 + kCWin * C) / 16)
+    constexpr int RPI = 64 / NCH;         // rows per wave-instruction: 3 (RGB), 9 (gray)
+    static_assert(RPI == (C == 3 ? 3 : 9), "conv_rows_staged assumes this grouping");
+    constexpr int kG = (conv_rows_staged<C, MT>(17) / RPI + kConvWaves - 1) / kConvWaves;  // groups per wave (K <= 33)
     const int b0 = (x0 - R) * C;  // first window byte (the x-margins hold the border)
-    const int b0a = b0 & ~3;
+    const int b0a = b0 & ~15;     // row origins are 16-byte aligned (kMarginBytes, 256-B pitch)
     const int lead = b0 - b0a;
-    const int nd = (lead + kCWin * C + 3) / 4;  // dwords per row (<= 74 for C = 3)
-    int dst[2][4];
+    const int rr = lane / NCH, ch = lane % NCH;
+    const bool lane_ok = rr < RPI;
+    // byte address (in the plane block) of each of the lane's 16 bytes in its
+    // row of group 0; group i adds a compile-time offset (ds_write immediate)
+    int addr[16];
 #pragma unroll
-    for (int qi = 0; qi < 2; ++qi)
+    for (int e = 0; e < 16; ++e) {
+      const int bi = 16 * ch + e - lead;  // byte index within the window
+      const int dst = (lane_ok && bi >= 0 && bi < kCWin * C) ? (bi % C) * pstride + bi / C : kCWin;
+      addr[e] = 2 * (dst + (wave * RPI + (lane_ok ? rr : 0)) * kCPS);
+    }
+    const uint32_t lane_off = lane_ok ? (uint32_t)(b0a + 16 * ch) : kOOB;
+    const int ngrp = (rows_in + RPI - 1) / RPI;
+    const bool inner = rows_inside(a, yb - R, a.ry1 - 1 + R);
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 d[kG];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int q = lane + 64 * qi;
-        const int bi = 4 * q + e - lead;  // byte index within the window
-        dst[qi][e] = (q < nd && bi >= 0 && bi < kCWin * C) ? (bi % C) * pstride + bi / C : -1;
-      }
-    // every row of the wave in one batch: all loads are issued before the
-    // first LDS write, so staging costs one memory latency, not one per row
-    // (8-row batches measured 0.549 ms vs 0.684 ms for row-by-row on conv:31;
-    // rows_in <= 16 MT + 34)
-    constexpr int kSB = (16 * MT + 34 + kConvWaves - 1) / kConvWaves;
-    constexpr int NQ = C == 3 ? 2 : 1;  // dwords per lane per row
-    for (int rb = wave; rb < rows_in; rb += kConvWaves * kSB) {
-      uint32_t d[kSB][NQ];
+    for (int i = 0; i < kG; ++i) {
+      // rows past the range's last needed input row (ry1 - 1 + R) feed only
+      // outputs that are not stored (or zero weights): clamp so no read
+      // leaves the stripe + halo; they must still hold finite values
+      const int r = (wave + kConvWaves * i) * RPI + (lane_ok ? rr : 0);
+      const int y = min(yb - R + r, a.ry1 - 1 + R);
+      const uint32_t roff = inner ? a.in_org + (uint32_t)((int64_t)y * a.in_pitch) : in_row_off(a, y);
+      // bytes past the allocation read as 0 (range check); they feed only x >= W
+      d[i] = __builtin_amdgcn_raw_buffer_load_b128(rin, roff + lane_off, 0, 0);
+    }
 #pragma unroll
-      for (int i = 0; i < kSB; ++i) {
-        // rows past the range's last needed input row (ry1 - 1 + R) feed only
-        // outputs that are not stored (or zero weights): clamp so no read
-        // leaves the stripe + halo; they must still hold finite values
-        const int y = min(yb - R + rb + kConvWaves * i, a.ry1 - 1 + R);
-        const uint32_t roff = in_row_off(a, y) + (uint32_t)b0a;
+    for (int i = 0; i < kG; ++i) {
+      if (wave + kConvWaves * i >= ngrp) break;  // wave-uniform; staged rows are a multiple of RPI
 #pragma unroll
-        for (int qi = 0; qi < NQ; ++qi)
-          // bytes past the allocation read as 0 (range check); they feed only x >= W
-          d[i][qi] = __builtin_amdgcn_raw_buffer_load_b32(rin, roff + 4u * (uint32_t)(lane + 64 * qi), 0, 0);
-      }
-#pragma unroll
-      for (int i = 0; i < kSB; ++i) {
-        const int r = rb + kConvWaves * i;
-        if (r >= rows_in) break;  // wave-uniform
-#pragma unroll
-        for (int qi = 0; qi < NQ; ++qi)
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (dst[qi][e] >= 0)
-              plane[dst[qi][e] + r * kCPS] = (_Float16)(float)((d[i][qi] >> (8 * e)) & 0xFFu);
-      }
+      for (int e = 0; e < 16; ++e)
+        *reinterpret_cast<_Float16*>(reinterpret_cast<uint8_t*>(plane) + addr[e] + i * (kConvWaves * RPI * kCPS * 2)) =
+            (_Float16)(uint16_t)((d[i][e >> 2] >> (8 * (e & 3))) & 0xFFu);
     }
   }
   __syncthreads();
@@ -212,23 +221,47 @@ void k_conv_mfma(ConvArgs ca) {
     __syncthreads();  // vmcnt(0): pair p + 1 landed (every wave); slot p & 1 read by every wave
   }
 
-  // ---- epilogue: C/D layout col = lane & 15, row = 4 (lane >> 4) + r ----
+  // ---- epilogue: the tile goes through LDS so it leaves as 16-byte row chunks ----
+  // C/D layout: col = lane & 15, row = 4 (lane >> 4) + r.  The planes are
+  // free (the last pair's barrier follows every wave's last fragment read);
+  // the tile [16 MT rows][64 px x C bytes] is written there as bytes, then
+  // stored as whole 16-byte chunks (a lane's 4 rows x 1 pixel would otherwise
+  // leave as C x 4 scattered byte stores per m-tile).
   // v_cvt_pk_u8_f32: round half even + saturate (the golden's nearbyint + sat)
-  const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
-  const int x = x0 + 16 * wave + m;
+  constexpr int kOS = kCTN * C + 16;  // LDS row stride of the output tile
+  uint8_t* otile = reinterpret_cast<uint8_t*>(plane);
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int y = yb + 16 * mt + 4 * g + r;
-      const uint32_t off = (y < a.ry1 && x < a.W)
-                               ? a.out_org + (uint32_t)((int64_t)y * a.out_pitch) + (uint32_t)(x * C)
-                               : kOOB;
+    for (int r = 0; r < 4; ++r)
 #pragma unroll
       for (int c = 0; c < C; ++c)
-        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)__builtin_amdgcn_cvt_pk_u8_f32(acc[c][mt][r], 0, 0u), rout,
-                                             off + (uint32_t)c, 0, 0);
+        otile[(16 * mt + 4 * g + r) * kOS + (16 * wave + m) * C + c] =
+            (uint8_t)__builtin_amdgcn_cvt_pk_u8_f32(acc[c][mt][r], 0, 0u);
+  __syncthreads();
+  const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
+  constexpr int NCO = kCTN * C / 16;  // 16-byte chunks per tile row
+  const int E = a.W * C;
+#pragma unroll
+  for (int k = 0; k < 16 * MT * NCO / 256; ++k) {
+    const int q = tid + 256 * k;
+    const int row = q / NCO, ch = q % NCO;
+    const int y = yb + row;
+    const int b = x0 * C + 16 * ch;  // first byte of the chunk in the output row
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = *reinterpret_cast<const u32x4*>(otile + row * kOS + 16 * ch);
+    const uint32_t roff = a.out_org + (uint32_t)((int64_t)y * a.out_pitch) + (uint32_t)b;
+    if (y < a.ry1) {
+      if (b + 16 <= E) {
+        __builtin_amdgcn_raw_buffer_store_b128(v, rout, roff, 0, 0);
+      } else if (b < E) {  // the chunk that straddles the row end: bytes < E only
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v[i >> 2] >> (8 * (i & 3))), rout,
+                                               b + i < E ? roff + (uint32_t)i : kOOB, 0, 0);
+      }
     }
+  }
 }
 
 }  // namespace dev
@@ -313,7 +346,8 @@ void launch_conv_mfma(const Pass& p, const PassConsts& pc, const PassLaunch& L, 
   ca.R = p.R;
   ca.np = (p.K + 1) / 2;
   const int mt = p.cmid == 3 ? dev::conv_mt<3>() : dev::conv_mt<1>();
-  const int rows_in = 16 * mt + 2 * ca.np;
+  const int rows_in = p.cmid == 3 ? dev::conv_rows_staged<3, dev::conv_mt<3>()>(ca.np)
+                                  : dev::conv_rows_staged<1, dev::conv_mt<1>()>(ca.np);
   const size_t lds = (size_t)p.cmid * rows_in * dev::kCPS * sizeof(_Float16) + 2 * dev::kBPair;
   for (int r = 0; r < L.nrange; ++r) {
     const int y0 = L.ry[2 * r], y1 = L.ry[2 * r + 1];
