@@ -18,11 +18,11 @@
 //     224 B, which makes every A-fragment ds_read_b128 conflict-free (the 16
 //     lanes of each b128 lane group hit 16 distinct 4-bank quads for all three
 //     k-step address patterns: quad = -2 m + g (+ const) mod 16);
-//   * a pair's B fragments (3 k-steps x weight hi + lo, 6 KiB) are DMA'd from
-//     L2 into an LDS ring once per workgroup, one pair ahead, and each
-//     fragment read feeds C x MT x 2 MFMAs (RGB, MT = 4: 24 MFMAs = 384
-//     cycles); the previous layout re-read the Toeplitz stream from L2 for
-//     every wave and every channel (12x the traffic).
+//   * a k-step's B fragments (weight hi + lo, 2 KiB per wave) stream from L2
+//     through a register ring two k-steps ahead, and each feeds C x MT x 2
+//     MFMAs (RGB, MT = 4: 24 MFMAs = 384 cycles; ~11 TB/s of L2 chip-wide at
+//     full MFMA rate); the round-1 layout re-read the Toeplitz stream for
+//     every channel and fed 6 MFMAs per fragment.
 // Precision: each weight is split into f16 hi + lo parts (two MFMAs), so the
 // f32 accumulation sees ~2^-22 relative weight error: results match the f64
 // golden to within 1 LSB (ties only).  Windows up to 5x5 (7x7 gray) take the
@@ -52,9 +52,8 @@ constexpr int kCWin = kCTN + 32;  // staged pixels per row (each wave's 48-pixel
 constexpr int kCPS = 112;        // LDS plane row stride in halves (224 B: conflict-free A reads)
 constexpr int kConvWaves = 4;
 
-// m-tiles (16 rows) per wave: RGB 4 (3 planes x 96 rows x 224 B = 64.5 KiB
-// + 12 KiB B ring, two workgroups per CU), gray 8 (one plane, 160 rows + the
-// ring = 47 KiB, three per CU)
+// m-tiles (16 rows) per wave: RGB 4 (3 planes x <= 99 rows x 224 B <= 66.5 KiB,
+// two workgroups per CU), gray 8 (one plane, <= 171 rows = 37.4 KiB, four per CU)
 template <int C>
 constexpr int conv_mt() { return C == 3 ? 4 : 8; }
 
@@ -65,33 +64,13 @@ __host__ __device__ constexpr int conv_rows_staged(int np) {
   return (16 * MT + 2 * np + (C == 3 ? 3 : 9) - 1) / (C == 3 ? 3 : 9) * (C == 3 ? 3 : 9);
 }
 
-// B fragments travel global -> LDS by LDS-DMA (global_load_lds_dwordx4, no
-// register destination), one pair ahead, into a 2-slot ring shared by the
-// workgroup's 4 waves: each (pair, k-step, hi/lo) fragment set is one 1 KiB
-// wave-instruction, so the LDS image is lane-linear and every wave reads its
-// fragment with one conflict-free ds_read_b128.  A register ring was tried
-// first: hipcc folds a loop-carried ring of plain loads into one load at the
-// top of the consuming iteration, and sinks buffer-load prefetches to the end
-// of the producing one behind a vmcnt(0) for the loop-carried copies; both
-// stalled every k-step on an L2 round trip.
 constexpr int kBPair = 6 * 1024;  // bytes of one pair's B fragments (3 k-steps x hi/lo x 1 KiB)
 
-__device__ __forceinline__ void load_b_pair(const uint8_t* tw, int p, uint8_t* slot, int wave, int lane) {
-  // 6 chunks over 4 waves, 2 per wave (waves 2, 3 duplicate chunks 4, 5 with
-  // identical bytes), so every wave counts the same number of DMA loads
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int c = i == 0 ? wave : (wave < 2 ? wave + 4 : wave + 2);
-    __builtin_amdgcn_global_load_lds((const void*)(tw + (size_t)p * kBPair + c * 1024 + 16 * lane),
-                                     (__attribute__((address_space(3))) void*)(slot + c * 1024), 16, 0, 0);
-  }
-}
-
-// LDS caps residency at 2 (RGB) / 3 (gray) workgroups per CU: tell the
-// compiler, or it trims registers for occupancy it can never get and sinks the
-// B prefetch / serialises the A-fragment reads (one ds_read in flight).
+// LDS caps residency at 2 (RGB) / 4 (gray) workgroups per CU: tell the
+// compiler, or it trims registers for occupancy it can never get and
+// serialises the A-fragment reads (one ds_read in flight).
 template <int C, int MT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 3 ? 2 : 3, C == 3 ? 2 : 3)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 3 ? 2 : 4, C == 3 ? 2 : 4)))
 void k_conv_mfma(ConvArgs ca) {
   const KArgs& a = ca.a;
   const int R = ca.R, np = ca.np;
@@ -101,12 +80,8 @@ void k_conv_mfma(ConvArgs ca) {
   const int x0 = blockIdx.x * kCTN;                 // first output pixel
   const int yb = a.ry0 + blockIdx.y * (16 * MT);    // first output row
   if (yb >= a.ry1) return;
-  const int rows_in = conv_rows_staged<C, MT>(np);  // >= 16 MT + K - 1 (+1 zero-weight row for odd K)
+  const int rows_in = conv_rows_staged<C, MT>(np);  // >= 16 MT + K - 1 (+ zero-weight padding rows)
   const int pstride = rows_in * kCPS;
-
-  // pair 0's B fragments; the staging barrier below retires them (vmcnt(0))
-  load_b_pair(reinterpret_cast<const uint8_t*>(ca.tw), 0, reinterpret_cast<uint8_t*>(plane + C * pstride), wave,
-              lane);
 
   // ---- stage pixels [x0 - R, x0 - R + kCWin) of input rows yb - R .. ----
   // 16-byte chunks: a row's window (from its 16-byte aligned start) is NCH
@@ -122,7 +97,7 @@ void k_conv_mfma(ConvArgs ca) {
     constexpr int NCH = C == 3 ? 19 : 7;  // ceil((15 + kCWin * C) / 16)
     constexpr int RPI = 64 / NCH;         // rows per wave-instruction: 3 (RGB), 9 (gray)
     static_assert(RPI == (C == 3 ? 3 : 9), "conv_rows_staged assumes this grouping");
-    constexpr int kG = (conv_rows_staged<C, MT>(17) / RPI + kConvWaves - 1) / kConvWaves;  // groups per wave (K <= 33)
+    constexpr int kG = (conv_rows_staged<C, MT>(18) / RPI + kConvWaves - 1) / kConvWaves;  // groups per wave (K <= 33)
     const int b0 = (x0 - R) * C;  // first window byte (the x-margins hold the border)
     const int b0a = b0 & ~15;     // row origins are 16-byte aligned (kMarginBytes, 256-B pitch)
     const int lead = b0 - b0a;
@@ -180,46 +155,56 @@ void k_conv_mfma(ConvArgs ca) {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[c][mt] = float4v{0.f, 0.f, 0.f, 0.f};
 
-  // B ring: pair p in slot p & 1; the DMA for pair p + 1 runs while pair p
-  // computes, and the barrier at the end of each pair both publishes it and
-  // frees slot p & 1 for pair p + 2
-  uint8_t* bring = reinterpret_cast<uint8_t*>(plane + C * pstride);
-  const uint8_t* tw = reinterpret_cast<const uint8_t*>(ca.tw);
-
-  for (int p = 0; p < np; ++p) {
-    if (p + 1 < np) load_b_pair(tw, p + 1, bring + ((p + 1) & 1) * kBPair, wave, lane);
-    const _Float16* pl = plane + 2 * p * kCPS;
-    const uint8_t* bslot = bring + (p & 1) * kBPair + 16 * lane;
-    // fragments of k-step s + 1 are read while k-step s multiplies (the
-    // sched barriers pin that order: left alone, hipcc issues two reads at a
-    // time and waits lgkmcnt(0) before every MFMA pair)
-    half8 af[2][C][MT], bf[2][2];
-    auto read_step = [&](int s, int buf) __attribute__((always_inline)) {
-      bf[buf][0] = *reinterpret_cast<const half8*>(bslot + (2 * s) * 1024);
-      bf[buf][1] = *reinterpret_cast<const half8*>(bslot + (2 * s + 1) * 1024);
+  // The k-steps of all pairs form one stream t = 3 p + s.  B(t) comes from
+  // L2 through a 3-slot register ring: step t starts the load of B(t + 2)
+  // into the slot step t - 1 has just consumed (its registers are reused, so
+  // the loop carries no copies); A(t + 1) is read from the planes while step
+  // t multiplies.  No barrier inside the loop (the B ring used to be DMA'd
+  // into LDS, shared by the 4 waves, behind a barrier per pair: 14 % slower).
+  const __amdgpu_buffer_rsrc_t rtw = make_rsrc(ca.tw, (uint32_t)np * (uint32_t)kBPair);
+  const uint32_t tl = 16u * (uint32_t)lane;
+  const int nsteps = 3 * np;
+  half8 bq[3][2];
+  auto load_b = [&](int t, int slot) __attribute__((always_inline)) {
+    const uint32_t off = (uint32_t)min(t, nsteps - 1) * 2048u + tl;  // past the end: re-read (unused)
+    bq[slot][0] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(rtw, off, 0, 0));
+    bq[slot][1] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(rtw, off + 1024u, 0, 0));
+  };
+  half8 af[2][C][MT];
+  auto read_a = [&](int p, int s, int buf) __attribute__((always_inline)) {
+    const _Float16* pl = plane + 2 * p * kCPS + aoff[s];
 #pragma unroll
-      for (int c = 0; c < C; ++c)
+    for (int c = 0; c < C; ++c)
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-          af[buf][c][mt] = *reinterpret_cast<const half8*>(pl + c * pstride + aoff[s] + 16 * mt * kCPS);
-    };
-    read_step(0, 0);
+      for (int mt = 0; mt < MT; ++mt)
+        af[buf][c][mt] = *reinterpret_cast<const half8*>(pl + c * pstride + 16 * mt * kCPS);
+  };
+  load_b(0, 0);
+  load_b(1, 1);
+  read_a(0, 0, 0);
+  // 6 steps = 2 pairs per body: ring slot, A buffer and k-step are static.
+  // The pair count is even (the host pads odd ones with a zero-weight pair),
+  // so the body has no branches: a branch would make hipcc wait vmcnt(0) at
+  // the join and drain the B prefetch.
+  for (int q = 0; q < nsteps; q += 6) {
 #pragma unroll
-    for (int s = 0; s < 3; ++s) {
-      const int cur = s & 1;
-      if (s < 2) read_step(s + 1, cur ^ 1);
+    for (int i = 0; i < 6; ++i) {
+      const int t = q + i;
+      load_b(t + 2, (i + 2) % 3);  // into the slot step t - 1 has consumed
+      // the last step re-reads pair np - 1's k-step 0 (unused)
+      read_a(min((q / 3) + (i + 1) / 3, np - 1), (i + 1) % 3, (i + 1) & 1);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int c = 0; c < C; ++c)
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
-          acc[c][mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[cur][c][mt], bf[cur][0], acc[c][mt], 0, 0, 0);
-          acc[c][mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[cur][c][mt], bf[cur][1], acc[c][mt], 0, 0, 0);
+          acc[c][mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i & 1][c][mt], bq[i % 3][0], acc[c][mt], 0, 0, 0);
+          acc[c][mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i & 1][c][mt], bq[i % 3][1], acc[c][mt], 0, 0, 0);
         }
       __builtin_amdgcn_sched_barrier(0);
     }
-    __syncthreads();  // vmcnt(0): pair p + 1 landed (every wave); slot p & 1 read by every wave
   }
+  __syncthreads();  // every wave's last fragment read before the planes are reused
 
   // ---- epilogue: the tile goes through LDS so it leaves as 16-byte row chunks ----
   // C/D layout: col = lane & 15, row = 4 (lane >> 4) + r.  The planes are
@@ -266,6 +251,13 @@ void k_conv_mfma(ConvArgs ca) {
 
 }  // namespace dev
 
+// Kernel-row pairs of a K x K window, padded to an even count (a zero-weight
+// pair) so the MFMA loop runs whole 2-pair bodies.
+static int conv_pairs(int K) {
+  const int np = (K + 1) / 2;
+  return np + (np & 1);
+}
+
 // B fragments: pair p, k-step s, part hl, lane l (g = l >> 4, n = l & 15),
 // element j: k = 32 s + 8 g + j -> (kernel row 2p + (k >= 48), window pixel
 // k mod 48); B[k][n] = w[ky][px - n] for 0 <= px - n < K, else 0.
@@ -273,7 +265,7 @@ void prepare_conv_consts(const Pass& p, PassConsts* pc, hipStream_t s) {
   if (sep_supported(p)) return prepare_sep_consts(p, pc, s);
   const int K = p.K;
   STRIPE_CHECK(K >= 1 && K <= 33, "conv K=" << K << " exceeds the 48-pixel Toeplitz window");
-  const int np = (K + 1) / 2;
+  const int np = conv_pairs(K);
   std::vector<_Float16> host((size_t)np * 3 * 2 * 64 * 8);
   for (int pr = 0; pr < np; ++pr)
     for (int ks = 0; ks < 3; ++ks)
@@ -344,11 +336,11 @@ void launch_conv_mfma(const Pass& p, const PassConsts& pc, const PassLaunch& L, 
   ca.tw = reinterpret_cast<const dev::half8*>(pc.conv);
   ca.K = p.K;
   ca.R = p.R;
-  ca.np = (p.K + 1) / 2;
+  ca.np = conv_pairs(p.K);
   const int mt = p.cmid == 3 ? dev::conv_mt<3>() : dev::conv_mt<1>();
   const int rows_in = p.cmid == 3 ? dev::conv_rows_staged<3, dev::conv_mt<3>()>(ca.np)
                                   : dev::conv_rows_staged<1, dev::conv_mt<1>()>(ca.np);
-  const size_t lds = (size_t)p.cmid * rows_in * dev::kCPS * sizeof(_Float16) + 2 * dev::kBPair;
+  const size_t lds = (size_t)p.cmid * rows_in * dev::kCPS * sizeof(_Float16);
   for (int r = 0; r < L.nrange; ++r) {
     const int y0 = L.ry[2 * r], y1 = L.ry[2 * r + 1];
     if (y1 <= y0) continue;
