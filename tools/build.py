@@ -144,13 +144,15 @@ def compile_one(src: str, extra: list[str], hdr_mtime: float, verbose: bool, obj
     cmd = [HIPCC, *common_flags(), *extra]
     if src.endswith(".hip"):
         cmd += ["-x", "hip", "-Rpass-analysis=kernel-resource-usage"]
-    cmd += ["-c", str(s), "-o", str(o)]
+    tmp = o.with_name(f"{o.name}.{os.getpid()}.tmp")  # concurrent builds: rename whole objects only
+    cmd += ["-c", str(s), "-o", str(tmp)]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         sys.stderr.write(r.stdout + r.stderr)
         raise SystemExit(f"compile failed: {src}")
+    os.replace(tmp, o)
     if src.endswith(".hip"):
         remarks_for(o).write_text(r.stderr)
         noise = "\n".join(l for l in r.stderr.splitlines() if "remark:" not in l)
@@ -179,7 +181,9 @@ def write_resource_report() -> dict:
 
 def link(objs: list[Path], out: Path, shared: bool, verbose: bool, extra: list[str] | None = None) -> None:
     out.parent.mkdir(parents=True, exist_ok=True)
-    tmp = out.with_name(out.name + ".tmp")
+    # per-process temporary: concurrent builds (pytest-xdist workers building the
+    # sanitized CLI) must not rename each other's half-linked output
+    tmp = out.with_name(f"{out.name}.{os.getpid()}.tmp")
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-fPIC", *(extra or [])]
     if shared:
         cmd += ["-shared"]
