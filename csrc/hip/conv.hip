@@ -208,8 +208,8 @@ void k_conv_mfma(ConvArgs ca) {
 
   // ---- epilogue: the tile goes through LDS so it leaves as 16-byte row chunks ----
   // C/D layout: col = lane & 15, row = 4 (lane >> 4) + r.  The planes are
-  // free (the last pair's barrier follows every wave's last fragment read);
-  // the tile [16 MT rows][64 px x C bytes] is written there as bytes, then
+  // free (the barrier above follows every wave's last fragment read); the
+  // tile [16 MT rows][64 px x C bytes] is written there as bytes, then
   // stored as whole 16-byte chunks (a lane's 4 rows x 1 pixel would otherwise
   // leave as C x 4 scattered byte stores per m-tile).
   // v_cvt_pk_u8_f32: round half even + saturate (the golden's nearbyint + sat)
