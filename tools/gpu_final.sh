@@ -4,7 +4,7 @@
 # backend; the real N-GPU curve comes from the driver's SCALE runs), plus a
 # rocprofv3 kernel trace of the headline bench.  Output: gpurun_out/final/.
 set -o pipefail
-O=gpurun_out/final
+O=${O:-gpurun_out/final}
 mkdir -p $O
 S=bin/stripe
 run() { local name=$1 t=$2; shift 2; echo "== $name" >> $O/configs.txt
@@ -17,6 +17,8 @@ run "cfg3 sobel 8192x8192x1 4 local ranks on 1 GPU" 200 $S bench --synthetic 819
 run "cfg4 gaussian5 16384x16384x3 one N=8 stripe" 200 python tools/kbench.py --shape 16384x2048x3 --chains gaussian5 --bands 0 --iters 50
 run "cfg5 blur:31 16384x2048x3 one N=8 stripe" 200 python tools/kbench.py --shape 16384x2048x3 --chains blur:31 --bands 0 --iters 10 --warmup 2
 run "cfg5 blur:31 16384x16384x3 full frame" 300 python tools/kbench.py --shape 16384x16384x3 --chains blur:31 --bands 0 --iters 5 --warmup 1
+run "cfg5b conv:31 (arbitrary 31x31 weights, im2col->MFMA) 16384x2048x3 one N=8 stripe" 200 python tools/kbench.py --shape 16384x2048x3 --chains "$(cat tools/conv31_chain.txt)|" --bands 0 --iters 10 --warmup 2
+run "cfg5b conv:31 16384x16384x3 full frame" 300 python tools/kbench.py --shape 16384x16384x3 --chains "$(cat tools/conv31_chain.txt)|" --bands 0 --iters 3 --warmup 1
 run "reference chain gray:ref,contrast:3.5,emboss3 16384x16384x3" 200 python tools/kbench.py --shape 16384x16384x3 --chains "gray:ref,contrast:3.5,emboss3" --bands 0 --iters 20
 timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
 cd /tmp && export TMPDIR=/tmp
