@@ -280,6 +280,27 @@ __device__ __forceinline__ uint32_t pair_at(const uint32_t (&w)[WDW], int k) {
   return (k & 1) ? __builtin_amdgcn_alignbyte(w[(k + 1) >> 1], w[(k - 1) >> 1], 2) : w[k >> 1];
 }
 
+// op(pair at base - d, pair at base + d) for an even base (a symmetric tap
+// pair, op = packed add, or sub for antisymmetric taps).  For odd d both pairs
+// straddle dwords; applying op to the whole dwords first and extracting the
+// pair once gives the same fields (the ops are per 16-bit half), and the dword
+// op w[j] op w[j + d] is the same for neighbouring output pairs, so the
+// unrolled horizontal loop shares it: one op + one alignbyte per output pair
+// instead of two alignbytes + one op.
+template <class Op, int WDW>
+__device__ __forceinline__ uint32_t sym_pair(const uint32_t (&w)[WDW], int base, int d, Op op) {
+  if ((d & 1) == 0) return op(w[(base + d) >> 1], w[(base - d) >> 1]);
+  const uint32_t lo = op(w[(base + d - 1) >> 1], w[(base - d - 1) >> 1]);
+  const uint32_t hi = op(w[(base + d + 1) >> 1], w[(base - d + 1) >> 1]);
+  return __builtin_amdgcn_alignbyte(hi, lo, 2);
+}
+struct PkAddU16 {
+  __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return as_u32(as_u16x2(a) + as_u16x2(b)); }
+};
+struct PkSubI16 {  // a - b per field
+  __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return as_u32(as_i16x2(a) - as_i16x2(b)); }
+};
+
 // Vertical filter state.  Binomial filters: cascade of K-1 two-tap sums
 // s_k[y] = s_{k-1}[y] + s_{k-1}[y-1] (K-1 state rows); others: the last K rows.
 template <class F>
@@ -446,8 +467,8 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : 4)) void k_sep(KArgs a) {
       uint32_t h[8];
 #pragma unroll
       for (int pp = 0; pp < 8; ++pp) {
-        const i16x2 gx = as_i16x2(pair_at(w, WLO + 2 * pp + C)) - as_i16x2(pair_at(w, WLO + 2 * pp - C));
-        const i16x2 gy = as_i16x2(pair_at(wd, WLO + 2 * pp - C)) + as_i16x2(pair_at(wd, WLO + 2 * pp + C)) +
+        const i16x2 gx = as_i16x2(sym_pair(w, WLO + 2 * pp, C, PkSubI16{}));
+        const i16x2 gy = as_i16x2(sym_pair(wd, WLO + 2 * pp, C, PkAddU16{})) +
                          (as_i16x2(pair_at(wd, WLO + 2 * pp)) << (short)1);
         if constexpr (F::L2) {
           // round(sqrt(gx^2 + gy^2)) exactly: f32 sqrt lands within one of
@@ -491,10 +512,9 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : 4)) void k_sep(KArgs a) {
             }
             return as_u32(as_u16x2(s) * (unsigned short)g + as_u16x2(acc));
           };
-          uint32_t acc = pair_at(w, WLO + 2 * pp - R * C) + pair_at(w, WLO + 2 * pp + R * C);
+          uint32_t acc = sym_pair(w, WLO + 2 * pp, R * C, PkAddU16{});
 #pragma unroll
-          for (int i = 1; i < R; ++i)
-            acc = madd(pair_at(w, WLO + 2 * pp + (i - R) * C) + pair_at(w, WLO + 2 * pp + (R - i) * C), acc, F::g(i));
+          for (int i = 1; i < R; ++i) acc = madd(sym_pair(w, WLO + 2 * pp, (R - i) * C, PkAddU16{}), acc, F::g(i));
           acc = madd(pair_at(w, WLO + 2 * pp), acc, F::g(R));
           sacc = as_u16x2(acc);
           if constexpr (!T::FOLD) sacc += (u16x2)(unsigned short)(F::DIV / 2);
