@@ -20,9 +20,9 @@
 //     k-step address patterns: quad = -2 m + g (+ const) mod 16);
 //   * a k-step's B fragments (weight hi + lo, 2 KiB per wave) stream from L2
 //     through a register ring two k-steps ahead, and each feeds C x MT x 2
-//     MFMAs (RGB, MT = 4: 24 MFMAs = 384 cycles; ~11 TB/s of L2 chip-wide at
-//     full MFMA rate); the round-1 layout re-read the Toeplitz stream for
-//     every channel and fed 6 MFMAs per fragment.
+//     MFMAs (RGB, MT = 2: 12 MFMAs = 192 cycles; ~22 TB/s of L2 chip-wide at
+//     full MFMA rate, well under L2 bandwidth); the round-1 layout re-read
+//     the Toeplitz stream for every channel and fed 6 MFMAs per fragment.
 // Precision: each weight is split into f16 hi + lo parts (two MFMAs), so the
 // f32 accumulation sees ~2^-22 relative weight error: results match the f64
 // golden to within 1 LSB (ties only).  Windows up to 5x5 (7x7 gray) take the
@@ -52,10 +52,11 @@ constexpr int kCWin = kCTN + 32;  // staged pixels per row (each wave's 48-pixel
 constexpr int kCPS = 112;        // LDS plane row stride in halves (224 B: conflict-free A reads)
 constexpr int kConvWaves = 4;
 
-// m-tiles (16 rows) per wave: RGB 4 (3 planes x <= 99 rows x 224 B <= 66.5 KiB,
-// two workgroups per CU), gray 8 (one plane, <= 171 rows = 37.4 KiB, four per CU)
+// m-tiles (16 rows) per wave: RGB 2 (3 planes x <= 69 rows x 224 B <= 46.4 KiB,
+// three workgroups per CU; 4 m-tiles at two per CU measured 1-4 % slower),
+// gray 8 (one plane, <= 171 rows = 37.4 KiB, four per CU)
 template <int C>
-constexpr int conv_mt() { return C == 3 ? 4 : 8; }
+constexpr int conv_mt() { return C == 3 ? 2 : 8; }
 
 // Staged input rows per plane: 16 MT + 2 np rounded up to whole staging
 // groups (3 rows per wave-instruction for RGB, 9 for gray; see the staging loop)
@@ -66,11 +67,11 @@ __host__ __device__ constexpr int conv_rows_staged(int np) {
 
 constexpr int kBPair = 6 * 1024;  // bytes of one pair's B fragments (3 k-steps x hi/lo x 1 KiB)
 
-// LDS caps residency at 2 (RGB) / 4 (gray) workgroups per CU: tell the
+// LDS caps residency at 3 (RGB) / 4 (gray) workgroups per CU: tell the
 // compiler, or it trims registers for occupancy it can never get and
 // serialises the A-fragment reads (one ds_read in flight).
 template <int C, int MT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 3 ? 2 : 4, C == 3 ? 2 : 4)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 3 ? 3 : 4, C == 3 ? 3 : 4)))
 void k_conv_mfma(ConvArgs ca) {
   const KArgs& a = ca.a;
   const int R = ca.R, np = ca.np;
@@ -228,8 +229,9 @@ void k_conv_mfma(ConvArgs ca) {
   constexpr int NCO = kCTN * C / 16;  // 16-byte chunks per tile row
   const int E = a.W * C;
 #pragma unroll
-  for (int k = 0; k < 16 * MT * NCO / 256; ++k) {
+  for (int k = 0; k < (16 * MT * NCO + 255) / 256; ++k) {
     const int q = tid + 256 * k;
+    if (q >= 16 * MT * NCO) break;
     const int row = q / NCO, ch = q % NCO;
     const int y = yb + row;
     const int b = x0 * C + 16 * ch;  // first byte of the chunk in the output row
