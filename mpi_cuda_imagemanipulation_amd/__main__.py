@@ -7,6 +7,16 @@ gray -> contrast -> emboss, gather, write) is `run --preset ref-gpu`.
       --chain gray:ref,contrast:3.5,emboss3 --ranks 4 --backend local
   python -m mpi_cuda_imagemanipulation_amd convert in.jpg out.ppm
   python -m mpi_cuda_imagemanipulation_amd filters
+
+One process per rank, like the reference's `mpiexec -n N kernel.exe`
+(kernel.cu:104-137 Init/Bcast/Scatter, :223-225 Gather): under torchrun,
+`--backend rccl` (one GPU per process, RCCL over xGMI) or `--backend gloo`
+(CPU golden engine) - rank 0 reads the image, broadcasts its shape (the
+reference's 4-int metadata Bcast), scatters the stripes, every rank filters
+its stripe with halo exchange, rank 0 gathers and writes:
+
+  torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m mpi_cuda_imagemanipulation_amd \\
+      run --input in.jpg --output out.png --preset ref-gpu --backend rccl
 """
 from __future__ import annotations
 
@@ -28,8 +38,9 @@ def main(argv=None) -> int:
     r.add_argument("--chain", default=None)
     r.add_argument("--preset", default=None, choices=sorted(models.PRESETS))
     r.add_argument("--ranks", type=int, default=1)
-    r.add_argument("--backend", default="auto", choices=["auto", "local", "host"],
-                   help="local: N logical ranks on this process's GPU; host: CPU golden engine")
+    r.add_argument("--backend", default="auto", choices=["auto", "local", "host", "rccl", "gloo"],
+                   help="local: N logical ranks on this process's GPU; host: CPU golden engine; "
+                        "rccl / gloo: one process per rank under torchrun (RANK / WORLD_SIZE env)")
     r.add_argument("--border", default=None)
     r.add_argument("--iterations", type=int, default=1)
     c = sub.add_parser("convert", help="convert between image formats")
@@ -45,11 +56,13 @@ def main(argv=None) -> int:
     if a.cmd == "convert":
         utils.write_image(a.dst, utils.read_image(a.src))
         return 0
-    img = utils.read_image(a.input)
     if a.preset:
         pipe = models.Pipeline.preset(a.preset)
     else:
         pipe = models.Pipeline(a.chain or "gaussian5", border=a.border or "reflect101")
+    if a.backend in ("rccl", "gloo"):
+        return _run_per_process(a, pipe)
+    img = utils.read_image(a.input)
     backend = a.backend
     if backend == "auto":
         import torch
@@ -61,6 +74,44 @@ def main(argv=None) -> int:
     utils.write_image(a.output, out)
     print(json.dumps({"cmd": "run", "input": a.input, "output": a.output, "shape": list(img.shape),
                       "chain": pipe.spec.chain, "ranks": a.ranks, "backend": backend, "wall_ms": round(ms, 3)}))
+    return 0
+
+
+def _run_per_process(a, pipe) -> int:
+    """One rank per process (torchrun env): root load -> metadata broadcast ->
+    scatter -> per-stripe chain with halo exchange -> gather -> root write."""
+    import numpy as np
+    import torch.distributed as dist
+
+    from . import parallel, utils
+
+    ctx = parallel.init(a.backend)
+    img = utils.read_image(a.input) if ctx.rank == 0 else None
+    meta = [None if img is None else tuple(img.shape)]
+    if ctx.world > 1:
+        dist.broadcast_object_list(meta, src=0)
+    shape = meta[0]
+    H, W = shape[:2]
+    Cc = 1 if len(shape) == 2 else shape[2]
+    dp = parallel.DistributedPipeline(ctx, pipe, W, H, Cc, root_buffers=True)
+    dp.load_root(img)
+    if ctx.world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    dp.scatter()
+    dp.run(a.iterations)
+    dp.gather()
+    dp.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3
+    if ctx.rank == 0:
+        out = dp.result_root()
+        utils.write_image(a.output, np.ascontiguousarray(out))
+        print(json.dumps({"cmd": "run", "input": a.input, "output": a.output, "shape": list(shape),
+                          "chain": pipe.spec.chain, "ranks": ctx.world, "backend": a.backend,
+                          "stripe_rows": dp.stripe[1], "dist_ms": round(ms, 3)}))
+    if ctx.world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
     return 0
 
 

@@ -122,3 +122,32 @@ def test_bench_host_backend_multi_rank(tmp_path, nproc, depth):
     assert rec["verified_vs_golden"] is True
     if depth:
         assert rec["halo_depth"] == depth
+
+
+@pytest.mark.parametrize("nproc,preset,chain", [(3, None, "gaussian5,sobel"), (2, "ref-cpu", None)])
+def test_python_cli_one_process_per_rank(tmp_path, C, nproc, preset, chain):
+    """`torchrun -m mpi_cuda_imagemanipulation_amd run --backend gloo`: the
+    reference's mpiexec flow (root load, metadata broadcast, scatter, filter,
+    gather, root write), one process per rank; output equals the single-rank
+    run of the same pipeline."""
+    import mpi_cuda_imagemanipulation_amd as m
+
+    img = m.utils.synthetic_image(5, 83, 47, 3)
+    src, out = tmp_path / "in.ppm", tmp_path / "out.ppm"
+    m.utils.write_image(str(src), img)
+    sel = ["--preset", preset] if preset else ["--chain", chain]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "-m", "mpi_cuda_imagemanipulation_amd",
+           "run", "--input", str(src), "--output", str(out), "--backend", "gloo", *sel]
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1",
+               PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout + r.stderr
+    rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert rec["ranks"] == nproc and rec["backend"] == "gloo"
+    got = m.utils.read_image(str(out))
+    pipe = m.models.Pipeline.preset(preset) if preset else m.models.Pipeline(chain)
+    ref = pipe.run_distributed(img, nproc, backend="host")
+    assert got.shape == ref.shape and (got == ref).all()
+    if not preset:
+        assert (got == C.golden_apply(img, chain, "reflect101", True)).all()

@@ -50,3 +50,30 @@ def test_torchrun_bench_rccl(n, chain, depth):
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == n and rec["value"] > 0
     assert rec["verified_vs_golden"] is True
+
+
+@pytest.mark.parametrize("n", [1, 2, 4])
+def test_python_cli_rccl_one_process_per_gpu(tmp_path, n):
+    """`torchrun -m mpi_cuda_imagemanipulation_amd run --backend rccl`: the
+    reference's mpiexec flow with one process per GPU (n = 1 runs on every
+    box: a one-rank RCCL communicator through the same scatter/gather path)."""
+    if _ngpus() < n:
+        pytest.skip(f"needs {n} GPUs")
+    import numpy as np
+
+    sys.path.insert(0, ROOT)
+    import mpi_cuda_imagemanipulation_amd as m
+
+    img = m.utils.synthetic_image(9, 301, 157, 3)
+    src, out = tmp_path / "in.ppm", tmp_path / "out.ppm"
+    m.utils.write_image(str(src), img)
+    chain = "gray:ref,contrast:3.5,emboss3,expand"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "-m", "mpi_cuda_imagemanipulation_amd",
+           "run", "--input", str(src), "--output", str(out), "--backend", "rccl", "--chain", chain]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    got = m.utils.read_image(str(out))
+    ref = m._C.golden_apply(img, chain, "reflect101", True)
+    assert got.shape == ref.shape and np.array_equal(got, ref)
