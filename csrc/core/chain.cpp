@@ -180,16 +180,26 @@ Plan compile_chain(const std::vector<Op>& ops, int cin, Border default_border, b
     pending = PointwiseProgram{};
     pending_cin = c;
   }
-  // trailing pointwise ops: epilogue of the last stencil if LUT-only, else own pass
+  // trailing pointwise ops: epilogue of the last stencil if they are a LUT and/or
+  // an expand of its 1-channel result (the reference's gray -> emboss -> expand
+  // GPU chain, kernel.cu:192-196, is then one pass), else their own pass
   normalize(pending);
   if (!pending.identity()) {
-    if (fuse && !plan.passes.empty() && pending.lut_only() &&
-        (plan.passes.back().kind == PassKind::Separable || plan.passes.back().kind == PassKind::Direct) &&
-        !plan.passes.back().has_epi) {
-      Pass& last = plan.passes.back();
-      last.has_epi = true;
-      last.epi = pending.post;
-      last.desc += " epilogue[lut]";
+    Pass* last = plan.passes.empty() ? nullptr : &plan.passes.back();
+    const bool epi_ok = fuse && last &&
+                        (last->kind == PassKind::Separable || last->kind == PassKind::Direct) &&
+                        !last->has_epi && !last->epi_expand && !pending.gray && !pending.has_pre &&
+                        (!pending.expand || last->cmid == 1);
+    if (epi_ok) {
+      if (pending.has_post) {
+        last->has_epi = true;
+        last->epi = pending.post;
+      }
+      if (pending.expand) {
+        last->epi_expand = true;
+        last->cout = 3;
+      }
+      last->desc += " epilogue[" + prog_desc(pending) + "]";
       pending = PointwiseProgram{};
     } else {
       flush_pointwise();

@@ -152,7 +152,12 @@ void golden_pass(const Pass& p, ConstView in, MutView out, int W, RowGeom g, int
           else v = s;
           v = sat(v);
         }
-        dst[(int64_t)x * C + c] = p.has_epi ? p.epi[v] : (uint8_t)v;
+        const uint8_t b = p.has_epi ? p.epi[v] : (uint8_t)v;
+        if (p.epi_expand) {  // cmid 1 -> 3 equal channels
+          dst[(int64_t)x * 3] = dst[(int64_t)x * 3 + 1] = dst[(int64_t)x * 3 + 2] = b;
+        } else {
+          dst[(int64_t)x * C + c] = b;
+        }
       }
     }
   }

@@ -195,7 +195,9 @@ __device__ __forceinline__ void apply_skip(const KArgs& a, int cb, int gy, int R
 // After a band: edge waves rewrite the x-margins of their output rows (margin
 // pixel m <- pixel border_index(m) of the same row).  The wave's own stores are
 // complete after vmcnt(0); reads use sc0 (L2) so they see them.
-template <int C>
+// C: stencil channels (the wave tiling covers W * C bytes); CO: output bytes
+// per pixel (3 for a fused expand of a 1-channel stencil, else C).
+template <int C, int CO = C>
 __device__ __forceinline__ void band_margins(const KArgs& a, const WaveTask& t) {
   const int px = a.out_px;
   if (px == 0) return;
@@ -205,21 +207,87 @@ __device__ __forceinline__ void band_margins(const KArgs& a, const WaveTask& t) 
   if (!left && !right) return;
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this band's stores are done
   const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
-  const int nb = px * C;  // margin bytes per side
+  const int nb = px * CO;  // margin bytes per side
   const int per_row = 2 * nb;
   for (int i = t.lane; i < (t.ye - t.ys) * per_row; i += kW) {
     const int y = t.ys + i / per_row;
     const int q = i % per_row;
     const int side = q >= nb;
-    const int k = (side ? q - nb : q) / C + 1;
-    const int c = (side ? q - nb : q) % C;
+    const int k = (side ? q - nb : q) / CO + 1;
+    const int c = (side ? q - nb : q) % CO;
     if ((side == 0 && !left) || (side == 1 && !right)) continue;
     const int m = side ? a.W - 1 + k : -k;
     const int src = border_index_dev(m, a.W, a.out_border);
     const uint32_t row = a.out_org + (uint32_t)((int64_t)y * a.out_pitch);
     uint8_t v = 0;
-    if (src >= 0) v = __builtin_amdgcn_raw_buffer_load_b8(rout, row + src * C + c, 0, 1);
-    __builtin_amdgcn_raw_buffer_store_b8(v, rout, row + m * C + c, 0, 0);
+    if (src >= 0) v = __builtin_amdgcn_raw_buffer_load_b8(rout, row + src * CO + c, 0, 1);
+    __builtin_amdgcn_raw_buffer_store_b8(v, rout, row + m * CO + c, 0, 0);
+  }
+}
+
+// v_perm selector of output dword k of an expanded chunk: its bytes are
+// stencil bytes (4k + i) / 3, taken from source dwords q = (4k/3)/4 and q + 1.
+constexpr uint32_t expand_sel(int k) {
+  uint32_t s = 0;
+  const int q = (4 * k / 3) / 4;
+  for (int i = 0; i < 4; ++i) s |= (uint32_t)((4 * k + i) / 3 - 4 * q) << (8 * i);
+  return s;
+}
+
+// Output store of one row of a wave tile.  Plain: each lane stores its 16-byte
+// chunk at row + L.off[0] (kOOB-biased lanes are masked by the range check).
+// EXP (fused `expand` epilogue): a lane's 16 gray bytes become 48 bytes of 3
+// equal channels (12 v_perm).  Stored in place they would be three 16-byte
+// stores at a 48-byte lane stride (each instruction touching 3x the cache lines
+// of a contiguous one); instead the wave re-tiles them through LDS (3 KiB per
+// wave: 3 ds_write_b128 at the 48-byte stride, conflict-free per 8 lanes, and
+// 3 contiguous ds_read_b128) so store j writes chunk 64j + lane of the tile's
+// 3072 contiguous output bytes.
+struct OutLanes {
+  uint32_t off[3];  // per-lane offset from the row start (kOOB: not stored)
+};
+
+template <bool EXP>
+__device__ __forceinline__ OutLanes out_lanes(const KArgs& a, int lane, int cb0) {
+  OutLanes L;
+  if constexpr (!EXP) {
+    const int cb = cb0 + 16 * lane;
+    L.off[0] = lane >= 1 && lane <= kW - 2 && cb < a.E ? (uint32_t)cb : kOOB;
+    L.off[1] = L.off[2] = kOOB;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int c = kW * j + lane;  // output chunk of the tile
+      const int s = c / 3;          // lane that computed it
+      L.off[j] = s >= 1 && s <= kW - 2 && cb0 + 16 * s < a.E ? (uint32_t)(3 * cb0 + 16 * c) : kOOB;
+    }
+  }
+  return L;
+}
+
+template <bool EXP, int SAUX>
+__device__ __forceinline__ void store_out(const uint32_t (&o)[4], __amdgpu_buffer_rsrc_t rout, bool valid,
+                                          uint32_t row, const OutLanes& L, uint4* xb, int lane) {
+  if constexpr (!EXP) {
+    const u32x4 ov = {o[0], o[1], o[2], o[3]};
+    __builtin_amdgcn_raw_buffer_store_b128(ov, rout, valid ? row + L.off[0] : kOOB, 0, SAUX);
+  } else {
+    uint32_t e[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+      const int q = (4 * k / 3) / 4;
+      e[k] = __builtin_amdgcn_perm(o[q < 3 ? q + 1 : 3], o[q], expand_sel(k));
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) xb[3 * lane + j] = make_uint4(e[4 * j], e[4 * j + 1], e[4 * j + 2], e[4 * j + 3]);
+    wave_lds_sync();
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const uint4 v = xb[kW * j + lane];
+      const u32x4 ov = {v.x, v.y, v.z, v.w};
+      __builtin_amdgcn_raw_buffer_store_b128(ov, rout, valid ? row + L.off[j] : kOOB, 0, SAUX);
+    }
+    wave_lds_sync();  // reads done before the next row's writes (program order)
   }
 }
 
@@ -357,8 +425,9 @@ __device__ __forceinline__ void vpush(const uint32_t (&row)[8], const VState<F>&
   }
 }
 
-template <int C, class F, int PRO, bool SKIP, int SAUX>
+template <int C, class F, int PRO, bool SKIP, int SAUX, bool EXP = false>
 __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : 4)) void k_sep(KArgs a) {
+  static_assert(!EXP || C == 1, "expand epilogue needs a 1-channel stencil");
   constexpr int R = F::R, K = F::K;
   constexpr int WLO = (R * C <= 8) ? 8 : 16;  // u16 window start (relative to chunk)
   constexpr int WDW = (2 * WLO + 16) / 2;     // window dwords
@@ -369,6 +438,7 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : 4)) void k_sep(KArgs a) {
   // (sobel: planes 2..3 hold the difference row)
   constexpr int NP = F::SOBEL ? 4 : 2;
   __shared__ __attribute__((aligned(16))) uint4 vbuf[kWaves][NP][kW];
+  __shared__ __attribute__((aligned(16))) uint4 xbuf[EXP ? kWaves : 1][EXP ? 3 * kW : 1];
   __shared__ uint8_t luts[PRO == PRO_GRAYLUT ? kLutBytes : 768];
   if (PRO != PRO_NONE || a.has_epi) {
     load_luts<PRO>(a, luts);
@@ -379,13 +449,13 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : 4)) void k_sep(KArgs a) {
   const int lane = t.lane;
   const int ys = t.ys, ye = t.ye;
   const int cb = t.xt * (kOutChunks * 16) - 16 + lane * 16;
-  const bool st = lane >= 1 && lane <= kW - 2 && cb < a.E;
   const uint32_t lane_in = cb < a.E + 16 ? (uint32_t)(cb * CIN) : kOOB;
-  const uint32_t lane_out = st ? (uint32_t)cb : kOOB;
+  const OutLanes lout = out_lanes<EXP>(a, lane, cb - 16 * lane);
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);
   const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
   const uint32_t last_row = in_row_off(a, ye - 1 + R);
   uint4(*vb)[kW] = vbuf[t.wave];
+  uint4* xb = xbuf[EXP ? t.wave : 0];
   const int rl = lane == 0 ? 1 : (lane == kW - 1 ? kW - 2 : lane);  // keep LDS reads in bounds
 
   VState<F> sa, sb;
@@ -552,10 +622,8 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : 4)) void k_sep(KArgs a) {
       apply_skip<C>(a, cb, a.row0 + y, R, center, o);
     }
     if (a.has_epi) lut16(luts + 512, o);
-    const u32x4 ov = {o[0], o[1], o[2], o[3]};
     // rows past the band (tail of the 4-row group) are computed but not stored
-    __builtin_amdgcn_raw_buffer_store_b128(
-        ov, rout, valid ? a.out_org + (uint32_t)((int64_t)y * a.out_pitch) + lane_out : kOOB, 0, SAUX);
+    store_out<EXP, SAUX>(o, rout, valid, a.out_org + (uint32_t)((int64_t)y * a.out_pitch), lout, xb, lane);
   };
 
   // rows go in groups of kPF with no branch around any step, ping-ponging the
@@ -573,7 +641,7 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : 4)) void k_sep(KArgs a) {
       }
     }
   }
-  band_margins<C>(a, t);
+  band_margins<C, EXP ? 3 : C>(a, t);
 }
 
 // ------------------------------------------------------------------------------
@@ -597,8 +665,9 @@ __device__ __forceinline__ void extend_row(const uint32_t (&u)[8], uint32_t (&e)
   for (int i = 0; i < 8; ++i) e[NX + i] = u[i];
 }
 
-template <int C, class F, int PRO, bool SKIP, int SAUX>
+template <int C, class F, int PRO, bool SKIP, int SAUX, bool EXP = false>
 __global__ __launch_bounds__(kNT, (F::K >= 5 ? 3 : 4)) void k_direct(KArgs a) {
+  static_assert(!EXP || C == 1, "expand epilogue needs a 1-channel stencil");
   constexpr int R = F::R, K = F::K;
   constexpr int NX = (R * C + 1) / 2;  // neighbour dwords per side
   constexpr int NE = 8 + 2 * NX;       // extended row dwords
@@ -613,12 +682,13 @@ __global__ __launch_bounds__(kNT, (F::K >= 5 ? 3 : 4)) void k_direct(KArgs a) {
   const int lane = t.lane;
   const int ys = t.ys, ye = t.ye;
   const int cb = t.xt * (kOutChunks * 16) - 16 + lane * 16;
-  const bool st = lane >= 1 && lane <= kW - 2 && cb < a.E;
   const uint32_t lane_in = cb < a.E + 16 ? (uint32_t)(cb * CIN) : kOOB;
-  const uint32_t lane_out = st ? (uint32_t)cb : kOOB;
+  const OutLanes lout = out_lanes<EXP>(a, lane, cb - 16 * lane);
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);
   const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
   const uint32_t last_row = in_row_off(a, ye - 1 + R);
+  __shared__ __attribute__((aligned(16))) uint4 xbuf[EXP ? kWaves : 1][EXP ? 3 * kW : 1];
+  uint4* xb = xbuf[EXP ? t.wave : 0];
 
   uint32_t ring[K][NE];  // slot of input row r: (r - (ys - R)) mod K
   auto push = [&](const RawChunk<PRO>& raw, uint32_t (&slot)[NE]) __attribute__((always_inline)) {
@@ -674,12 +744,10 @@ __global__ __launch_bounds__(kNT, (F::K >= 5 ? 3 : 4)) void k_direct(KArgs a) {
         apply_skip<C>(a, cb, a.row0 + yy, R, center, o4);
       }
       if (a.has_epi) lut16(luts + 512, o4);
-      const u32x4 ov = {o4[0], o4[1], o4[2], o4[3]};
-      __builtin_amdgcn_raw_buffer_store_b128(
-          ov, rout, yy < ye ? a.out_org + (uint32_t)((int64_t)yy * a.out_pitch) + lane_out : kOOB, 0, SAUX);
+      store_out<EXP, SAUX>(o4, rout, yy < ye, a.out_org + (uint32_t)((int64_t)yy * a.out_pitch), lout, xb, lane);
     }
   }
-  band_margins<C>(a, t);
+  band_margins<C, EXP ? 3 : C>(a, t);
 }
 
 // ------------------------------------------------------------------------------
@@ -829,23 +897,30 @@ inline void plan_bands(KArgs& a, dim3& grid, int tiles, int n0, int n1, int band
   grid = dim3((unsigned)div_up((int64_t)tiles * a.nbands, kWaves));
 }
 
-template <int C, class F, int PRO>
+template <int C, class F, int PRO, bool EXP = false>
 void launch_one(bool skip, bool nt, KArgs a, int tiles, int n0, int n1, int band, hipStream_t s) {
   using K = void (*)(KArgs);
   dim3 grid;
   if constexpr (F::SEP) {
-    const K fns[4] = {k_sep<C, F, PRO, false, 0>, k_sep<C, F, PRO, false, kNtAux>, k_sep<C, F, PRO, true, 0>,
-                      k_sep<C, F, PRO, true, kNtAux>};
+    const K fns[4] = {k_sep<C, F, PRO, false, 0, EXP>, k_sep<C, F, PRO, false, kNtAux, EXP>,
+                      k_sep<C, F, PRO, true, 0, EXP>, k_sep<C, F, PRO, true, kNtAux, EXP>};
     const K fn = fns[2 * skip + nt];
     plan_bands(a, grid, tiles, n0, n1, band, F::R, resident_slots((const void*)fn));
     fn<<<grid, kNT, 0, s>>>(a);
   } else {
-    const K fns[4] = {k_direct<C, F, PRO, false, 0>, k_direct<C, F, PRO, false, kNtAux>,
-                      k_direct<C, F, PRO, true, 0>, k_direct<C, F, PRO, true, kNtAux>};
+    const K fns[4] = {k_direct<C, F, PRO, false, 0, EXP>, k_direct<C, F, PRO, false, kNtAux, EXP>,
+                      k_direct<C, F, PRO, true, 0, EXP>, k_direct<C, F, PRO, true, kNtAux, EXP>};
     const K fn = fns[2 * skip + nt];
     plan_bands(a, grid, tiles, n0, n1, band, F::R, resident_slots((const void*)fn));
     fn<<<grid, kNT, 0, s>>>(a);
   }
+}
+
+template <int PRO, class F>
+void launch_gray_out(bool expand, bool skip, bool nt, const KArgs& a, int tiles, int n0, int n1, int band,
+                     hipStream_t s) {
+  if (expand) launch_one<1, F, PRO, true>(skip, nt, a, tiles, n0, n1, band, s);
+  else launch_one<1, F, PRO, false>(skip, nt, a, tiles, n0, n1, band, s);
 }
 
 template <class F>
@@ -853,15 +928,16 @@ void launch_filter(const Pass& p, const KArgs& a, int tiles, int n0, int n1, int
   const bool gray = p.pro.gray;
   const bool lut = p.pro.has_post;
   const bool skip = p.border == Border::Skip;
+  const bool ex = p.epi_expand;
   if (p.cmid == 3) {
-    STRIPE_CHECK(!gray, "gray prologue must produce 1 channel");
+    STRIPE_CHECK(!gray && !ex, "gray prologue / expand epilogue need a 1-channel stencil");
     if (lut) launch_one<3, F, PRO_LUT>(skip, nt, a, tiles, n0, n1, band, s);
     else launch_one<3, F, PRO_NONE>(skip, nt, a, tiles, n0, n1, band, s);
   } else {
-    if (gray && a.gmode == 1) launch_one<1, F, PRO_GRAYLUT>(skip, nt, a, tiles, n0, n1, band, s);
-    else if (gray) launch_one<1, F, PRO_GRAY>(skip, nt, a, tiles, n0, n1, band, s);
-    else if (lut) launch_one<1, F, PRO_LUT>(skip, nt, a, tiles, n0, n1, band, s);
-    else launch_one<1, F, PRO_NONE>(skip, nt, a, tiles, n0, n1, band, s);
+    if (gray && a.gmode == 1) launch_gray_out<PRO_GRAYLUT, F>(ex, skip, nt, a, tiles, n0, n1, band, s);
+    else if (gray) launch_gray_out<PRO_GRAY, F>(ex, skip, nt, a, tiles, n0, n1, band, s);
+    else if (lut) launch_gray_out<PRO_LUT, F>(ex, skip, nt, a, tiles, n0, n1, band, s);
+    else launch_gray_out<PRO_NONE, F>(ex, skip, nt, a, tiles, n0, n1, band, s);
   }
 }
 

@@ -43,6 +43,9 @@ struct Pass {
   PointwiseProgram pro;    // Pointwise: the whole program; stencil: prologue
   bool has_epi = false;    // stencil epilogue LUT (channel count unchanged)
   std::array<uint8_t, 256> epi{};
+  // stencil epilogue `expand`: the 1-channel result (after epi) is stored as 3
+  // equal channels (cmid 1 -> cout 3), so gray -> stencil -> expand is one pass
+  bool epi_expand = false;
   StencilId sid = StencilId::Gaussian5;
   int K = 1, R = 0;
   Border border = Border::Reflect101;

@@ -132,6 +132,9 @@ PYBIND11_MODULE(_C, m) {
       q["R"] = ps.R;
       q["cin"] = ps.cin;
       q["cout"] = ps.cout;
+      q["cmid"] = ps.cmid;
+      q["epi_lut"] = ps.has_epi;
+      q["epi_expand"] = ps.epi_expand;
       q["out_margin_px"] = ps.out_margin_px;
       passes.append(q);
     }

@@ -36,9 +36,39 @@ def test_epilogue_and_pointwise_passes(C):
     assert "separable sobel" in info["passes"][1]["desc"]
     assert info["passes"][0]["out_margin_px"] == 0 or info["passes"][0]["out_margin_px"] == 1
     info = C.plan_info("gaussian5,expand", 1)
-    assert [p["kind"] for p in info["passes"]] == [1, 0]
+    assert [p["kind"] for p in info["passes"]] == [1] and info["passes"][0]["epi_expand"]
     info = C.plan_info("blur:31", 3)
     assert info["passes"][0]["kind"] == 3 and info["max_radius"] == 15
+
+
+def test_expand_epilogue(C):
+    # the reference's whole GPU chain (gray -> contrast -> emboss -> expand back
+    # to RGB, kernel.cu:192-196) is one pass: gray prologue, expand epilogue
+    info = C.plan_info("gray:ref,contrast:3.5,emboss3@skip,expand", 3)
+    assert len(info["passes"]) == 1
+    p = info["passes"][0]
+    assert p["cin"] == 3 and p["cmid"] == 1 and p["cout"] == 3 and p["epi_expand"] and not p["epi_lut"]
+    # 3 -> 3: iterable, so the fused pass keeps its own input's margin contract
+    assert info["in_margin_px"] == 1 and p["out_margin_px"] == 1
+    # a LUT on either side of the expand rides along (channels are copies)
+    for chain in ("gray,gaussian5,expand,invert", "gray,gaussian5,invert,expand"):
+        p = C.plan_info(chain, 3)["passes"]
+        assert len(p) == 1 and p[0]["epi_expand"] and p[0]["epi_lut"], chain
+    # a 3-channel stencil cannot expand; conv passes take no pointwise work
+    assert [p["kind"] for p in C.plan_info("gray,blur:9,expand", 3)["passes"]] == [0, 3, 0]
+    assert [p["kind"] for p in C.plan_info("gaussian5,gray,expand", 3)["passes"]] == [1, 0]
+    assert len(C.plan_info("gray,gaussian5,expand", 3, "reflect101", False)["passes"]) == 3
+
+
+def test_expand_epilogue_golden_matches_unfused(C, rng):
+    import numpy as np
+
+    img = rng.integers(0, 256, size=(23, 41, 3), dtype=np.uint8)
+    for chain in ("gray:ref,contrast:3.5,emboss3@skip,expand", "gray,sobel,invert,expand",
+                  "gray,gaussian5,expand,brightness:30"):
+        a = C.golden_apply(img, chain, "reflect101", True)
+        b = C.golden_apply(img, chain, "reflect101", False)
+        assert a.shape == (23, 41, 3) and (a == b).all(), chain
 
 
 def test_margin_contracts(C):

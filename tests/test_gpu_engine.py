@@ -152,7 +152,8 @@ def test_pipelined_halo_schedule(m, chain, ranks, H):
     assert (res[0] == res[2]).all()
 
 
-@pytest.mark.parametrize("chain", ["gaussian5", "sobel", "emboss3", "gaussian7", "gray:ref,contrast:3.5,emboss5"])
+@pytest.mark.parametrize("chain", ["gaussian5", "sobel", "emboss3", "gaussian7", "gray:ref,contrast:3.5,emboss5",
+                                   "gray:ref,contrast:3.5,emboss3@skip,expand", "gray,gaussian7,expand"])
 @pytest.mark.parametrize("ranks,H,depth", [(2, 96, 2), (4, 130, 3), (8, 233, 4), (3, 300, 8)])
 @pytest.mark.parametrize("iters", [1, 6, 7])
 def test_deep_halo_schedule(m, chain, ranks, H, depth, iters):

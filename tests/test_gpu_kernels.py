@@ -43,6 +43,22 @@ def test_stencil_exact(m, rng, name, shape, C):
         assert bad.size == 0, f"{name} {border} {img.shape}: {len(bad)} mismatches, first {bad[:5].tolist()}"
 
 
+@pytest.mark.parametrize("name", STENCILS)
+@pytest.mark.parametrize("shape", [(1, 1), (17, 15), (37, 1365), (9, 5000)])
+def test_stencil_expand_epilogue(m, rng, name, shape):
+    # gray prologue + 1-channel stencil + fused expand epilogue (48-byte stores,
+    # 3-channel x-margins) vs the golden path
+    img = rng.integers(0, 256, size=shape + (3,), dtype=np.uint8)
+    chain = f"gray,{name},expand"
+    assert m._C.plan_info(chain, 3)["passes"][0]["epi_expand"]
+    for border in ("reflect101", "replicate", "constant"):
+        got = _run(m, img, chain, border)
+        ref = m._C.golden_apply(img, chain, border, True)
+        assert got.shape == ref.shape == shape + (3,)
+        bad = np.argwhere(got != ref)
+        assert bad.size == 0, f"{chain} {border} {img.shape}: {len(bad)} mismatches, first {bad[:5].tolist()}"
+
+
 @pytest.mark.parametrize("name", ["emboss3", "emboss5", "gaussian5", "sobel", "sobel_l2"])
 def test_skip_border(m, rng, name):
     img = rng.integers(0, 256, size=(45, 77), dtype=np.uint8)
@@ -55,6 +71,8 @@ def test_skip_border(m, rng, name):
     "gray,expand", "gray:ref,contrast:3.5,emboss3", "ref-gpu", "ref-cpu,expand",
     "invert,gray,brightness:20,gaussian5,invert", "gaussian5,gaussian5,sobel", "gray,sobel,threshold:60",
     "brightness:10,gaussian3,contrast:1.5,sharpen,invert", "gaussian5@replicate,gaussian5@constant",
+    "gray:ref,contrast:3.5,emboss3@skip,expand", "gray,gaussian5,expand,invert", "gray,sobel_l2,invert,expand",
+    "gray:ref,emboss5@skip,expand,gaussian3",
 ])
 @pytest.mark.parametrize("shape", [(33, 47), (128, 1000)])
 def test_chains_exact(m, rng, chain, shape):

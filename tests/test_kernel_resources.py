@@ -51,7 +51,8 @@ def test_hot_kernels_have_occupancy(report):
 
 def test_headline_kernel_clean(report):
     # gaussian5 on RGB without prologue: the BASELINE headline kernel
-    hits = [v for k, v in report.items() if "k_sep" in k and "Gaussian5" in k and "ILi3E" in k and "Li0ELb0E" in k]
+    # (k_sep<C=3, Gaussian5, PRO_NONE, SKIP=false, any store policy>)
+    hits = [v for k, v in report.items() if "k_sepILi3ENS_4sdef9Gaussian5ELi0ELb0E" in k]
     assert hits
     for v in hits:
         assert v["SGPRs Spill"] == 0 and v["VGPRs Spill"] == 0 and v["VGPRs"] <= 128
