@@ -1,0 +1,865 @@
+// Stencil kernels (k_sep, k_direct) and their launch templates, shared by
+// the instantiation units stencil_inst_*.hip (one group of filters each, so
+// the ~440 kernel instances compile in parallel) and stencil.hip.
+#pragma once
+
+// Integer stencil passes with fused pointwise prologue/epilogue (gfx950).
+//
+// Reference: embossKernel (kernel.cu:64-94) - one thread per pixel, in place
+// (racy, Q1), runtime-indexed private weight arrays, off-by-one bounds (Q2), and
+// separate gray/contrast launches before it.  Here:
+//   * every wave works on its own tile: 64 lanes x 16 bytes = a 1 KiB row segment
+//     (62 output chunks + one halo chunk each side) marching down a band of rows;
+//     waves never wait for each other (no workgroup barrier in the hot loop), and
+//     1 KiB tiles quantise wide rows finely (8192 gray: 9 tiles for 8.3 of work);
+//   * each lane loads its 16-byte chunk of every input row once (buffer dwordx4,
+//     two rows in flight), applies the fused prologue (gray / LUT) in registers;
+//   * separable filters: vertical taps in registers as packed-u16 adds - the
+//     binomial Gaussians as a cascade of K-1 two-tap sums (no row ring) - one row
+//     of vertical sums through the wave's LDS slice (in-order within a wave), the
+//     horizontal taps as packed-u16 multiply-adds on v_alignbyte-shifted pairs;
+//   * non-separable filters: a K-row register ring of prologue-applied rows, the
+//     neighbour lanes' edge dwords by DPP; taps are compile-time literals (zero
+//     taps vanish);
+//   * every hot-loop load/store is an unconditional raw buffer op; inactive lanes
+//     get an offset that fails the descriptor range check (no divergent branches
+//     around memory ops -> exact vmcnt, prefetches survive the barriers);
+//   * out-of-place and deterministic; the x-border comes from the buffer margins,
+//     the y-border from a scalar row remap; edge waves rewrite the output margins
+//     after their band (one vmcnt(0) per band).
+
+#include <cstdlib>
+
+#include "dev_common.h"
+#include "stripe/kernels.h"
+#include "stripe/stencil_defs.h"
+
+#include <map>
+#include <mutex>
+
+namespace stripe {
+namespace dev {
+
+constexpr int kW = 64;               // lanes per wave (one tile)
+constexpr int kWaves = kNT / kW;     // independent wave tiles per workgroup
+constexpr int kOutChunks = kW - 2;   // output chunks per wave tile
+
+// Orders this wave's LDS writes before its later LDS reads of other lanes' data
+// (LDS ops of one wave execute in order; this only stops compiler reordering).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+struct WaveTask {
+  int wave;   // wave index within the workgroup (scalar)
+  int lane;
+  int xt;     // tile column
+  int ys, ye; // rows
+  bool valid;
+};
+
+__device__ __forceinline__ WaveTask wave_task(const KArgs& a) {
+  WaveTask t;
+  t.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  t.lane = threadIdx.x & 63;
+  const int w = xcd_remap((int)blockIdx.x, (int)gridDim.x, a.nxcd) * kWaves + t.wave;
+  t.xt = w % a.ntx;
+  const int bt = w / a.ntx;
+  t.valid = bt < a.nbands;
+  t.ys = t.ye = 0;
+  if (t.valid) {
+    band_range(a, bt, t.ys, t.ye);
+    t.valid = t.ys < t.ye;
+  }
+  return t;
+}
+
+enum { PRO_NONE = 0, PRO_LUT = 1, PRO_GRAY = 2, PRO_GRAYLUT = 3 };
+// PRO_GRAY: arithmetic gray (bt601 fixed point); PRO_GRAYLUT: gray:ref as three
+// per-channel table lookups (see cook_pairs).  Both read 48 RGB bytes per lane.
+constexpr bool is_gray(int pro) { return pro == PRO_GRAY || pro == PRO_GRAYLUT; }
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+typedef short i16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
+__device__ __forceinline__ uint32_t as_u32(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ i16x2 as_i16x2(uint32_t x) { return __builtin_bit_cast(i16x2, x); }
+__device__ __forceinline__ uint32_t as_u32(i16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+
+// The lane's raw input bytes of one row: 16 bytes, or 48 for a gray prologue
+// (16 RGB pixels).  Loads are issued by load_raw and the prologue (gray / LUT)
+// is applied by cook when the row is consumed, so prefetched rows stay in
+// flight instead of being waited for at the load (a LUT or gray conversion at
+// the load site forces an s_waitcnt there).
+template <int PRO>
+struct RawChunk {
+  uint32_t d[is_gray(PRO) ? 12 : 4];
+};
+
+template <int PRO>
+__device__ __forceinline__ void load_raw(__amdgpu_buffer_rsrc_t rin, uint32_t row_off, uint32_t lane_off,
+                                         RawChunk<PRO>& r) {
+  if constexpr (is_gray(PRO)) {
+    const uint32_t off = row_off + lane_off;  // lane_off already scaled by 3
+    const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(rin, off, 0, kLoadAux);
+    const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(rin, off + 16, 0, kLoadAux);
+    const u32x4 v2 = __builtin_amdgcn_raw_buffer_load_b128(rin, off + 32, 0, kLoadAux);
+    r.d[0] = v0.x; r.d[1] = v0.y; r.d[2] = v0.z; r.d[3] = v0.w;
+    r.d[4] = v1.x; r.d[5] = v1.y; r.d[6] = v1.z; r.d[7] = v1.w;
+    r.d[8] = v2.x; r.d[9] = v2.y; r.d[10] = v2.z; r.d[11] = v2.w;
+  } else {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rin, row_off + lane_off, 0, kLoadAux);
+    r.d[0] = v.x; r.d[1] = v.y; r.d[2] = v.z; r.d[3] = v.w;
+  }
+}
+
+// gray:ref (kernel.cu:40-42: per-channel truncated products, summed) as three
+// 256-entry LDS tables per pixel (luts + 768: R, G, B terms, built on the host
+// from the exact multiply-shift constants); the sum (<= 254) and the optional
+// post LUT land straight in the u16 fields the stencil arithmetic uses, so
+// there is no byte packing / unpacking.  ~9 VALU + 6-8 conflict-free LDS reads
+// per pixel pair instead of ~24 VALU for the arithmetic form.
+template <int N>
+__device__ __forceinline__ uint32_t byte_at(const uint32_t (&d)[N], int j) {
+  return (d[j >> 2] >> ((j & 3) * 8)) & 0xFFu;
+}
+
+__device__ __forceinline__ void gray_ref_pairs(const KArgs& a, const uint32_t (&d)[12], const uint8_t* luts,
+                                               uint32_t (&u)[8]) {
+  const uint8_t* tr = luts + 768;
+  const uint8_t* tg = luts + 1024;
+  const uint8_t* tb = luts + 1280;
+#pragma unroll
+  for (int pp = 0; pp < 8; ++pp) {
+    uint32_t g2[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int b0 = 3 * (2 * pp + h);
+      g2[h] = (uint32_t)tr[byte_at(d, b0)] + (uint32_t)tg[byte_at(d, b0 + 1)] + (uint32_t)tb[byte_at(d, b0 + 2)];
+      if (a.has_post) g2[h] = luts[256 + g2[h]];
+    }
+    u[pp] = g2[0] | (g2[1] << 16);
+  }
+}
+
+// Prologue: the 16 output-channel bytes of a raw chunk.
+template <int PRO>
+__device__ __forceinline__ void cook(const KArgs& a, const RawChunk<PRO>& r, const uint8_t* lut_post,
+                                     uint32_t (&o)[4]) {
+  if constexpr (PRO == PRO_GRAYLUT) {
+    uint32_t u[8];
+    gray_ref_pairs(a, r.d, lut_post - 256, u);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = __builtin_amdgcn_perm(u[2 * q + 1], u[2 * q], 0x06040200u);
+  } else if constexpr (PRO == PRO_GRAY) {
+    gray16(a, r.d, o);
+    if (a.has_post) lut16(lut_post, o);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = r.d[q];
+    if constexpr (PRO == PRO_LUT) lut16(lut_post, o);
+  }
+}
+
+// Load + prologue in one step (rows that are consumed right away).
+template <int PRO>
+__device__ __forceinline__ void load_chunk(const KArgs& a, __amdgpu_buffer_rsrc_t rin, uint32_t row_off,
+                                           uint32_t lane_off, const uint8_t* lut_post, uint32_t (&o)[4]) {
+  RawChunk<PRO> r;
+  load_raw<PRO>(rin, row_off, lane_off, r);
+  cook<PRO>(a, r, lut_post, o);
+}
+
+template <int PRO>
+__device__ __forceinline__ void load_luts(const KArgs& a, uint8_t* lds) {
+  for (int i = threadIdx.x; i < (PRO == PRO_GRAYLUT ? kLutBytes : 768); i += kNT) lds[i] = a.luts[i];
+}
+
+// Legacy skip border (kernel.cu:83 interior-only bounds): bytes of pixels in the
+// skip region keep the prologue value.
+template <int C>
+__device__ __forceinline__ void apply_skip(const KArgs& a, int cb, int gy, int R, const uint32_t (&center)[4],
+                                           uint32_t (&o)[4]) {
+  const bool row_skip = gy <= R || gy >= a.Hg - R;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t w = o[q];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int x = (cb + 4 * q + e) / C;
+      const uint32_t m = 0xFFu << (8 * e);
+      w = (row_skip || x <= R || x >= a.W - R) ? ((w & ~m) | (center[q] & m)) : w;
+    }
+    o[q] = w;
+  }
+}
+
+// After a band: edge waves rewrite the x-margins of their output rows (margin
+// pixel m <- pixel border_index(m) of the same row).  The wave's own stores are
+// complete after vmcnt(0); reads use sc0 (L2) so they see them.
+// C: stencil channels (the wave tiling covers W * C bytes); CO: output bytes
+// per pixel (3 for a fused expand of a 1-channel stencil, else C).
+template <int C, int CO = C>
+__device__ __forceinline__ void band_margins(const KArgs& a, const WaveTask& t) {
+  const int px = a.out_px;
+  if (px == 0) return;
+  const int E = a.W * C;
+  const bool left = t.xt == 0;
+  const bool right = (t.xt + 1) * kOutChunks * 16 >= E;
+  if (!left && !right) return;
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this band's stores are done
+  const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
+  const int nb = px * CO;  // margin bytes per side
+  const int per_row = 2 * nb;
+  for (int i = t.lane; i < (t.ye - t.ys) * per_row; i += kW) {
+    const int y = t.ys + i / per_row;
+    const int q = i % per_row;
+    const int side = q >= nb;
+    const int k = (side ? q - nb : q) / CO + 1;
+    const int c = (side ? q - nb : q) % CO;
+    if ((side == 0 && !left) || (side == 1 && !right)) continue;
+    const int m = side ? a.W - 1 + k : -k;
+    const int src = border_index_dev(m, a.W, a.out_border);
+    const uint32_t row = a.out_org + (uint32_t)((int64_t)y * a.out_pitch);
+    uint8_t v = 0;
+    if (src >= 0) v = __builtin_amdgcn_raw_buffer_load_b8(rout, row + src * CO + c, 0, 1);
+    __builtin_amdgcn_raw_buffer_store_b8(v, rout, row + m * CO + c, 0, 0);
+  }
+}
+
+// v_perm selector of output dword k of an expanded chunk: its bytes are
+// stencil bytes (4k + i) / 3, taken from source dwords q = (4k/3)/4 and q + 1.
+constexpr uint32_t expand_sel(int k) {
+  uint32_t s = 0;
+  const int q = (4 * k / 3) / 4;
+  for (int i = 0; i < 4; ++i) s |= (uint32_t)((4 * k + i) / 3 - 4 * q) << (8 * i);
+  return s;
+}
+
+// Output store of one row of a wave tile.  Plain: each lane stores its 16-byte
+// chunk at row + L.off[0] (kOOB-biased lanes are masked by the range check).
+// EXP (fused `expand` epilogue): a lane's 16 gray bytes become 48 bytes of 3
+// equal channels (12 v_perm).  Stored in place they would be three 16-byte
+// stores at a 48-byte lane stride (each instruction touching 3x the cache lines
+// of a contiguous one); instead the wave re-tiles them through LDS (3 KiB per
+// wave: 3 ds_write_b128 at the 48-byte stride, conflict-free per 8 lanes, and
+// 3 contiguous ds_read_b128) so store j writes chunk 64j + lane of the tile's
+// 3072 contiguous output bytes.
+struct OutLanes {
+  uint32_t off[3];  // per-lane offset from the row start (kOOB: not stored)
+};
+
+template <bool EXP>
+__device__ __forceinline__ OutLanes out_lanes(const KArgs& a, int lane, int cb0) {
+  OutLanes L;
+  if constexpr (!EXP) {
+    const int cb = cb0 + 16 * lane;
+    L.off[0] = lane >= 1 && lane <= kW - 2 && cb < a.E ? (uint32_t)cb : kOOB;
+    L.off[1] = L.off[2] = kOOB;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int c = kW * j + lane;  // output chunk of the tile
+      const int s = c / 3;          // lane that computed it
+      L.off[j] = s >= 1 && s <= kW - 2 && cb0 + 16 * s < a.E ? (uint32_t)(3 * cb0 + 16 * c) : kOOB;
+    }
+  }
+  return L;
+}
+
+template <bool EXP, int SAUX>
+__device__ __forceinline__ void store_out(const uint32_t (&o)[4], __amdgpu_buffer_rsrc_t rout, bool valid,
+                                          uint32_t row, const OutLanes& L, uint4* xb, int lane) {
+  if constexpr (!EXP) {
+    const u32x4 ov = {o[0], o[1], o[2], o[3]};
+    __builtin_amdgcn_raw_buffer_store_b128(ov, rout, valid ? row + L.off[0] : kOOB, 0, SAUX);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {  // 4 live dwords at a time
+      uint32_t e[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = 4 * j + i, q = (4 * k / 3) / 4;
+        e[i] = __builtin_amdgcn_perm(o[q < 3 ? q + 1 : 3], o[q], expand_sel(k));
+      }
+      xb[3 * lane + j] = make_uint4(e[0], e[1], e[2], e[3]);
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const uint4 v = xb[kW * j + lane];
+      const u32x4 ov = {v.x, v.y, v.z, v.w};
+      __builtin_amdgcn_raw_buffer_store_b128(ov, rout, valid ? row + L.off[j] : kOOB, 0, SAUX);
+    }
+    wave_lds_sync();  // reads done before the next row's writes (program order)
+  }
+}
+
+// ------------------------------------------------------------------------------
+// Separable filters (gaussian3/5/7, box3/5)
+// ------------------------------------------------------------------------------
+__device__ __forceinline__ void unpack16(const uint32_t (&r)[4], uint32_t (&p)[8]) {
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    p[2 * d] = __builtin_amdgcn_perm(0u, r[d], 0x0c010c00u);      // (b0, b1)
+    p[2 * d + 1] = __builtin_amdgcn_perm(0u, r[d], 0x0c030c02u);  // (b2, b3)
+  }
+}
+
+// Prologue straight to the unpacked u16-pair form of the stencil arithmetic.
+template <int PRO>
+__device__ __forceinline__ void cook_pairs(const KArgs& a, const RawChunk<PRO>& r, const uint8_t* luts,
+                                           uint32_t (&u)[8]) {
+  if constexpr (PRO == PRO_GRAYLUT) {
+    gray_ref_pairs(a, r.d, luts, u);
+  } else {
+    uint32_t c[4];
+    cook<PRO>(a, r, luts + 256, c);
+    unpack16(c, u);
+  }
+}
+
+template <class F>
+struct SepTraits {
+  static constexpr int gsum() {
+    int s = 0;
+    for (int i = 0; i < F::K; ++i) s += F::g(i);
+    return s;
+  }
+  static constexpr int log2div() {
+    int l = 0;
+    while ((1 << l) < F::DIV) ++l;
+    return (1 << l) == F::DIV ? l : -1;
+  }
+  // horizontal sums (+ rounding) fit 16 bits and the division is a shift
+  static constexpr bool H16 = log2div() >= 0 && gsum() * gsum() * 255 + F::DIV / 2 < 65536;
+  // binomial H16 filters: the rounding term DIV/2 rides on the vertical sums
+  // (+DIV/2/gsum on each, summed gsum times by the horizontal taps), added by
+  // the cascade's last stage as a third operand (v_add3_u32: the packed u16
+  // fields never carry, every partial sum is < 2^16)
+  static constexpr bool FOLD = H16 && F::BINOM && (F::DIV / 2) % gsum() == 0;
+  static constexpr uint32_t kFold = FOLD ? (uint32_t)(F::DIV / 2 / gsum()) * 0x00010001u : 0u;
+  static constexpr bool SYM = [] {
+    for (int i = 0; i < F::K; ++i)
+      if (F::g(i) != F::g(F::K - 1 - i)) return false;
+    return true;
+  }();
+};
+
+// u16 pair (v[k], v[k+1]) of the window (k: u16 index, compile-time after unroll)
+template <int WDW>
+__device__ __forceinline__ uint32_t pair_at(const uint32_t (&w)[WDW], int k) {
+  return (k & 1) ? __builtin_amdgcn_alignbyte(w[(k + 1) >> 1], w[(k - 1) >> 1], 2) : w[k >> 1];
+}
+
+// op(pair at base - d, pair at base + d) for an even base (a symmetric tap
+// pair, op = packed add, or sub for antisymmetric taps).  For odd d both pairs
+// straddle dwords; applying op to the whole dwords first and extracting the
+// pair once gives the same fields (the ops are per 16-bit half), and the dword
+// op w[j] op w[j + d] is the same for neighbouring output pairs, so the
+// unrolled horizontal loop shares it: one op + one alignbyte per output pair
+// instead of two alignbytes + one op.
+template <class Op, int WDW>
+__device__ __forceinline__ uint32_t sym_pair(const uint32_t (&w)[WDW], int base, int d, Op op) {
+  if ((d & 1) == 0) return op(w[(base + d) >> 1], w[(base - d) >> 1]);
+  const uint32_t lo = op(w[(base + d - 1) >> 1], w[(base - d - 1) >> 1]);
+  const uint32_t hi = op(w[(base + d + 1) >> 1], w[(base - d + 1) >> 1]);
+  return __builtin_amdgcn_alignbyte(hi, lo, 2);
+}
+struct PkAddU16 {
+  __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return as_u32(as_u16x2(a) + as_u16x2(b)); }
+};
+struct PkSubI16 {  // a - b per field
+  __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return as_u32(as_i16x2(a) - as_i16x2(b)); }
+};
+
+// Vertical filter state.  Binomial filters: cascade of K-1 two-tap sums
+// s_k[y] = s_{k-1}[y] + s_{k-1}[y-1] (K-1 state rows); others: the last K rows.
+template <class F>
+struct VState {
+  static constexpr int NS = F::BINOM ? F::K - 1 : F::SOBEL ? 2 : F::K;
+  uint32_t s[NS][8];
+};
+
+// Sobel: push one row; `sm` = r0 + 2 r1 + r2 (smoothing, u16) and `df` = r2 - r0
+// (difference, i16) of the row above it.  State: the two previous rows.
+template <class F>
+__device__ __forceinline__ void vpush_sobel(const uint32_t (&row)[8], const VState<F>& prev, VState<F>& next,
+                                            uint32_t (&sm)[8], uint32_t (&df)[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    next.s[0][k] = prev.s[1][k];
+    next.s[1][k] = row[k];
+    const u16x2 r0 = as_u16x2(prev.s[0][k]), r1 = as_u16x2(prev.s[1][k]), r2 = as_u16x2(row[k]);
+    sm[k] = as_u32(r0 + r2 + (r1 << (unsigned short)1));
+    df[k] = as_u32(as_i16x2(row[k]) - as_i16x2(prev.s[0][k]));
+  }
+}
+
+// Push one unpacked row; `v` receives the vertical sums of the row R above it.
+template <class F>
+__device__ __forceinline__ void vpush(const uint32_t (&row)[8], const VState<F>& prev, VState<F>& next,
+                                      uint32_t (&v)[8]) {
+  if constexpr (F::BINOM) {
+    constexpr uint32_t kf = SepTraits<F>::kFold;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      uint32_t cur = row[k];
+#pragma unroll
+      for (int st = 0; st < F::K - 1; ++st) {
+        next.s[st][k] = cur;
+        if (kf != 0 && st == F::K - 2)  // fields stay < 2^16: no carry between them
+          asm("v_add3_u32 %0, %1, %2, %3" : "=v"(cur) : "v"(cur), "v"(prev.s[st][k]), "s"(kf));
+        else
+          cur = as_u32(as_u16x2(cur) + as_u16x2(prev.s[st][k]));
+      }
+      v[k] = cur;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+#pragma unroll
+      for (int i = 0; i < F::K - 1; ++i) next.s[i][k] = prev.s[i + 1][k];
+      next.s[F::K - 1][k] = row[k];
+      u16x2 acc = as_u16x2(next.s[0][k]) * (unsigned short)F::g(0);
+#pragma unroll
+      for (int i = 1; i < F::K; ++i) acc += as_u16x2(next.s[i][k]) * (unsigned short)F::g(i);
+      v[k] = as_u32(acc);
+    }
+  }
+}
+
+// (skip border + expand epilogue, a rare combination: 2 VGPRs over the 128 of
+// 4 waves/SIMD with the gray prologue -> 3 waves rather than a scratch spill)
+template <int C, class F, int PRO, bool SKIP, int SAUX, bool EXP = false>
+__global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : (SKIP && EXP ? 3 : 4))) void k_sep(KArgs a) {
+  static_assert(!EXP || C == 1, "expand epilogue needs a 1-channel stencil");
+  constexpr int R = F::R, K = F::K;
+  constexpr int WLO = (R * C <= 8) ? 8 : 16;  // u16 window start (relative to chunk)
+  constexpr int WDW = (2 * WLO + 16) / 2;     // window dwords
+  constexpr int CIN = is_gray(PRO) ? 3 : 1;  // input bytes per output byte
+  using T = SepTraits<F>;
+  // per wave: one row of vertical sums, planar (plane h = dwords 4h..4h+3 of a
+  // lane's 8) so every ds_write_b128 / ds_read_b128 has a 16-byte lane stride
+  // (sobel: planes 2..3 hold the difference row)
+  constexpr int NP = F::SOBEL ? 4 : 2;
+  __shared__ __attribute__((aligned(16))) uint4 vbuf[kWaves][NP][kW];
+  __shared__ __attribute__((aligned(16))) uint4 xbuf[EXP ? kWaves : 1][EXP ? 3 * kW : 1];
+  __shared__ uint8_t luts[PRO == PRO_GRAYLUT ? kLutBytes : 768];
+  if (PRO != PRO_NONE || a.has_epi) {
+    load_luts<PRO>(a, luts);
+    __syncthreads();
+  }
+  const WaveTask t = wave_task(a);
+  if (!t.valid) return;
+  const int lane = t.lane;
+  const int ys = t.ys, ye = t.ye;
+  const int cb = t.xt * (kOutChunks * 16) - 16 + lane * 16;
+  const uint32_t lane_in = cb < a.E + 16 ? (uint32_t)(cb * CIN) : kOOB;
+  const OutLanes lout = out_lanes<EXP>(a, lane, cb - 16 * lane);
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);
+  const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
+  const uint32_t last_row = in_row_off(a, ye - 1 + R);
+  uint4(*vb)[kW] = vbuf[t.wave];
+  uint4* xb = xbuf[EXP ? t.wave : 0];
+  const int rl = lane == 0 ? 1 : (lane == kW - 1 ? kW - 2 : lane);  // keep LDS reads in bounds
+
+  VState<F> sa, sb;
+#pragma unroll
+  for (int i = 0; i < VState<F>::NS; ++i)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sa.s[i][k] = 0;
+  uint32_t vdummy[8];
+#pragma unroll
+  for (int i = 0; i < K - 1; ++i) {  // prime with rows ys-R .. ys+R-1
+    uint32_t u[8];
+    RawChunk<PRO> rr;
+    load_raw<PRO>(rin, in_row_off(a, ys - R + i), lane_in, rr);
+    cook_pairs<PRO>(a, rr, luts, u);
+    if constexpr (F::SOBEL) {
+      if (i & 1) vpush_sobel<F>(u, sb, sa, vdummy, vdummy);
+      else vpush_sobel<F>(u, sa, sb, vdummy, vdummy);
+    } else {
+      if (i & 1) vpush<F>(u, sb, sa, vdummy);
+      else vpush<F>(u, sa, sb, vdummy);
+    }
+  }
+  // kPF rows in flight per lane (memory-level parallelism is what this streaming
+  // kernel is bound by); loads past the band re-read its last input row
+  // (unconditional: no branch around the load)
+  // (a gray prologue reads 48 bytes per row: 2 rows give more bytes in flight
+  // than 4 plain rows, at 24 fewer registers)
+  constexpr int kPF = is_gray(PRO) ? 2 : 4;
+  RawChunk<PRO> nx[kPF];
+#pragma unroll
+  for (int i = 0; i < kPF; ++i) load_raw<PRO>(rin, ys + i < ye ? in_row_off(a, ys + i + R) : last_row, lane_in, nx[i]);
+
+  const bool inner = rows_inside(a, ys - R, ye - 1 + R);
+  auto row_step = [&](int y, const VState<F>& prev, VState<F>& next, RawChunk<PRO>& nb, bool valid) {
+    uint32_t u[8], vv[8], dd[8];
+    cook_pairs<PRO>(a, nb, luts, u);
+    load_raw<PRO>(rin, ahead_row_off(a, inner, y, kPF, ye, R, last_row), lane_in, nb);
+    if constexpr (F::SOBEL) {
+      vpush_sobel<F>(u, prev, next, vv, dd);
+      vb[2][lane] = make_uint4(dd[0], dd[1], dd[2], dd[3]);
+      vb[3][lane] = make_uint4(dd[4], dd[5], dd[6], dd[7]);
+    } else {
+      vpush<F>(u, prev, next, vv);
+    }
+    vb[0][lane] = make_uint4(vv[0], vv[1], vv[2], vv[3]);
+    vb[1][lane] = make_uint4(vv[4], vv[5], vv[6], vv[7]);
+    wave_lds_sync();
+    // lanes 0 and 63 (halo chunks) compute garbage and their store is masked
+    uint32_t w[WDW];
+#pragma unroll
+    for (int q = 0; q < WDW / 4; ++q) {
+      // window dword 4q is logical dword g = 8*rl - WLO/2 + 4q: lane g/8, plane (g/4)&1
+      const int g = 8 * rl - WLO / 2 + 4 * q;
+      // whole 16-byte chunks (volatile: the compiler would otherwise trim the
+      // window to the dwords it needs and issue ds_read_b32/b64/read2 pieces
+      // whose 16-byte lane stride conflicts 4-way under the (a/4)%32 banking)
+      const u32x4 v = *(volatile __attribute__((address_space(3))) u32x4*)(&vb[(g >> 2) & 1][g >> 3]);
+      w[4 * q] = v.x;
+      w[4 * q + 1] = v.y;
+      w[4 * q + 2] = v.z;
+      w[4 * q + 3] = v.w;
+    }
+    uint32_t wd[F::SOBEL ? WDW : 1];
+    if constexpr (F::SOBEL) {
+#pragma unroll
+      for (int q = 0; q < WDW / 4; ++q) {
+        const int g = 8 * rl - WLO / 2 + 4 * q;
+        const u32x4 v = *(volatile __attribute__((address_space(3))) u32x4*)(&vb[2 + ((g >> 2) & 1)][g >> 3]);
+        wd[4 * q] = v.x;
+        wd[4 * q + 1] = v.y;
+        wd[4 * q + 2] = v.z;
+        wd[4 * q + 3] = v.w;
+      }
+    }
+    wave_lds_sync();  // reads done before the next row's writes (program order)
+    uint32_t o[4];
+    if constexpr (F::SOBEL) {
+      // Gx = S[x+C] - S[x-C], Gy = D[x-C] + 2 D[x] + D[x+C], out = min(|Gx| + |Gy|, 255)
+      uint32_t h[8];
+#pragma unroll
+      for (int pp = 0; pp < 8; ++pp) {
+        const i16x2 gx = as_i16x2(sym_pair(w, WLO + 2 * pp, C, PkSubI16{}));
+        const i16x2 gy = as_i16x2(sym_pair(wd, WLO + 2 * pp, C, PkAddU16{})) +
+                         (as_i16x2(pair_at(wd, WLO + 2 * pp)) << (short)1);
+        if constexpr (F::L2) {
+          // round(sqrt(gx^2 + gy^2)) exactly: f32 sqrt lands within one of
+          // isqrt(n) (n < 2^21), two integer corrections make it exact, and the
+          // rounding is k + (n > k^2 + k) (sqrt(n) is never a half-integer)
+          uint32_t hv[2];
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int xg = gx[e], yg = gy[e];
+            const int n = xg * xg + yg * yg;
+            int k = (int)__builtin_sqrtf((float)n);
+            k -= k * k > n ? 1 : 0;
+            k += (k + 1) * (k + 1) <= n ? 1 : 0;
+            k += n > k * k + k ? 1 : 0;
+            hv[e] = (uint32_t)min(k, 255);
+          }
+          h[pp] = hv[0] | (hv[1] << 16);
+        } else {
+          const i16x2 m = __builtin_elementwise_max(gx, -gx) + __builtin_elementwise_max(gy, -gy);
+          h[pp] = as_u32(__builtin_elementwise_min(m, (i16x2)(short)255));
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = __builtin_amdgcn_perm(h[2 * q + 1], h[2 * q], 0x06040200u);
+    } else if constexpr (T::H16) {
+      uint32_t h[8];
+#pragma unroll
+      for (int pp = 0; pp < 8; ++pp) {
+        u16x2 sacc;
+        if constexpr (T::SYM && F::g(0) == 1) {
+          // mirrored taps share a weight: (x[-i] + x[+i]) * g, outermost pair
+          // (weight 1) first, centre last: 2R ops per output pair.  Plain u32
+          // arithmetic on the packed pair is exact (H16: every partial sum and
+          // product is < 2^16, so nothing crosses into the high field), which
+          // turns power-of-two weights into one v_lshl_add_u32.
+          auto madd = [](uint32_t s, uint32_t acc, int g) __attribute__((always_inline)) {
+            if ((g & (g - 1)) == 0) {
+              int k = 0;
+              while ((1 << k) < g) ++k;
+              return (s << k) + acc;
+            }
+            return as_u32(as_u16x2(s) * (unsigned short)g + as_u16x2(acc));
+          };
+          uint32_t acc = sym_pair(w, WLO + 2 * pp, R * C, PkAddU16{});
+#pragma unroll
+          for (int i = 1; i < R; ++i) acc = madd(sym_pair(w, WLO + 2 * pp, (R - i) * C, PkAddU16{}), acc, F::g(i));
+          acc = madd(pair_at(w, WLO + 2 * pp), acc, F::g(R));
+          sacc = as_u16x2(acc);
+          if constexpr (!T::FOLD) sacc += (u16x2)(unsigned short)(F::DIV / 2);
+        } else {
+          sacc = (u16x2)(unsigned short)(F::DIV / 2);
+#pragma unroll
+          for (int i = 0; i < K; ++i)
+            sacc += as_u16x2(pair_at(w, WLO + 2 * pp + (i - R) * C)) * (unsigned short)F::g(i);
+        }
+        if constexpr (T::log2div() != 8) sacc = sacc >> (unsigned short)T::log2div();
+        h[pp] = as_u32(sacc);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        o[q] = T::log2div() == 8 ? __builtin_amdgcn_perm(h[2 * q + 1], h[2 * q], 0x07050301u)
+                                 : __builtin_amdgcn_perm(h[2 * q + 1], h[2 * q], 0x06040200u);
+    } else {
+      uint32_t ob[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        uint32_t hs = 0;
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+          const int k = WLO + j + (i - R) * C;
+          hs += (uint32_t)F::g(i) * ((w[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu);
+        }
+        ob[j] = (hs + F::DIV / 2) / F::DIV;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = pack4(ob[4 * q], ob[4 * q + 1], ob[4 * q + 2], ob[4 * q + 3]);
+    }
+    if constexpr (SKIP) {
+      uint32_t center[4];
+      load_chunk<PRO>(a, rin, in_row_off(a, y), lane_in, luts + 256, center);
+      apply_skip<C>(a, cb, a.row0 + y, R, center, o);
+    }
+    if (a.has_epi) lut16(luts + 512, o);
+    // rows past the band (tail of the 4-row group) are computed but not stored
+    store_out<EXP, SAUX>(o, rout, valid, a.out_org + (uint32_t)((int64_t)y * a.out_pitch), lout, xb, lane);
+  };
+
+  // rows go in groups of kPF with no branch around any step, ping-ponging the
+  // filter state so no register copies are needed
+  constexpr bool live_in_b = ((K - 1) & 1) != 0;
+  for (int y = ys; y < ye; y += kPF) {
+#pragma unroll
+    for (int i = 0; i < kPF; i += 2) {
+      if (live_in_b) {
+        row_step(y + i, sb, sa, nx[i], y + i < ye);
+        row_step(y + i + 1, sa, sb, nx[i + 1], y + i + 1 < ye);
+      } else {
+        row_step(y + i, sa, sb, nx[i], y + i < ye);
+        row_step(y + i + 1, sb, sa, nx[i + 1], y + i + 1 < ye);
+      }
+    }
+  }
+  band_margins<C, EXP ? 3 : C>(a, t);
+}
+
+// ------------------------------------------------------------------------------
+// Direct (non-separable) filters: emboss3/5, sharpen, laplace
+// ------------------------------------------------------------------------------
+// The last K input rows live in registers, unpacked to u16 pairs and extended
+// by the neighbour lanes' edge dwords (DPP wave shifts: no LDS, no wave sync);
+// every tap is one packed i16 multiply-add per two outputs (|sum| <= 17*255).
+// The y loop is unrolled K times so the register ring is indexed statically,
+// and the K raw rows of the next round are in flight meanwhile.
+template <int NX>
+__device__ __forceinline__ void extend_row(const uint32_t (&u)[8], uint32_t (&e)[8 + 2 * NX]) {
+#pragma unroll
+  for (int i = 0; i < NX; ++i) {
+    // lane l gets lane l-1's dword (wave_shr:1) / lane l+1's (wave_shl:1); the
+    // halo lanes 0 and 63 receive zeros and their outputs are never stored
+    e[i] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u[8 - NX + i], 0x138, 0xf, 0xf, false);
+    e[NX + 8 + i] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u[i], 0x130, 0xf, 0xf, false);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) e[NX + i] = u[i];
+}
+
+template <int C, class F, int PRO, bool SKIP, int SAUX, bool EXP = false>
+__global__ __launch_bounds__(kNT, (F::K >= 5 ? 3 : 4)) void k_direct(KArgs a) {
+  static_assert(!EXP || C == 1, "expand epilogue needs a 1-channel stencil");
+  constexpr int R = F::R, K = F::K;
+  constexpr int NX = (R * C + 1) / 2;  // neighbour dwords per side
+  constexpr int NE = 8 + 2 * NX;       // extended row dwords
+  constexpr int CIN = is_gray(PRO) ? 3 : 1;
+  __shared__ uint8_t luts[PRO == PRO_GRAYLUT ? kLutBytes : 768];
+  if (PRO != PRO_NONE || a.has_epi) {
+    load_luts<PRO>(a, luts);
+    __syncthreads();
+  }
+  const WaveTask t = wave_task(a);
+  if (!t.valid) return;
+  const int lane = t.lane;
+  const int ys = t.ys, ye = t.ye;
+  const int cb = t.xt * (kOutChunks * 16) - 16 + lane * 16;
+  const uint32_t lane_in = cb < a.E + 16 ? (uint32_t)(cb * CIN) : kOOB;
+  const OutLanes lout = out_lanes<EXP>(a, lane, cb - 16 * lane);
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);
+  const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
+  const uint32_t last_row = in_row_off(a, ye - 1 + R);
+  __shared__ __attribute__((aligned(16))) uint4 xbuf[EXP ? kWaves : 1][EXP ? 3 * kW : 1];
+  uint4* xb = xbuf[EXP ? t.wave : 0];
+
+  uint32_t ring[K][NE];  // slot of input row r: (r - (ys - R)) mod K
+  auto push = [&](const RawChunk<PRO>& raw, uint32_t (&slot)[NE]) __attribute__((always_inline)) {
+    uint32_t u[8];
+    cook_pairs<PRO>(a, raw, luts, u);
+    extend_row<NX>(u, slot);
+  };
+#pragma unroll
+  for (int i = 0; i < K - 1; ++i) {  // rows ys-R .. ys+R-1
+    RawChunk<PRO> r;
+    load_raw<PRO>(rin, in_row_off(a, ys - R + i), lane_in, r);
+    push(r, ring[i]);
+  }
+  RawChunk<PRO> nx[K];  // row y + o + R for the step o of the current round
+#pragma unroll
+  for (int o = 0; o < K; ++o) load_raw<PRO>(rin, ys + o < ye ? in_row_off(a, ys + o + R) : last_row, lane_in, nx[o]);
+
+  const bool inner = rows_inside(a, ys - R, ye - 1 + R);
+  for (int y = ys; y < ye; y += K) {
+#pragma unroll
+    for (int o = 0; o < K; ++o) {
+      const int yy = y + o;
+      push(nx[o], ring[(o + K - 1) % K]);
+      load_raw<PRO>(rin, ahead_row_off(a, inner, yy, K, ye, R, last_row), lane_in, nx[o]);
+      uint32_t h[8];
+#pragma unroll
+      for (int pp = 0; pp < 8; ++pp) {
+        i16x2 acc = {0, 0};
+#pragma unroll
+        for (int dy = 0; dy < K; ++dy)
+#pragma unroll
+          for (int dx = 0; dx < K; ++dx) {
+            constexpr int unused = 0;
+            (void)unused;
+            const int w = F::w(dy, dx);
+            if (w == 0) continue;
+            const i16x2 v = as_i16x2(pair_at(ring[(o + dy) % K], 2 * NX + 2 * pp + (dx - R) * C));
+            if (w == 1) acc += v;
+            else if (w == -1) acc -= v;
+            else acc += v * (short)w;
+          }
+        acc = __builtin_elementwise_max(acc, (i16x2)(short)0);
+        h[pp] = as_u32(__builtin_elementwise_min(acc, (i16x2)(short)255));
+      }
+      uint32_t o4[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o4[q] = __builtin_amdgcn_perm(h[2 * q + 1], h[2 * q], 0x06040200u);
+      if constexpr (SKIP) {
+        uint32_t center[4];
+        const uint32_t(&cr)[NE] = ring[(o + R) % K];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) center[q] = __builtin_amdgcn_perm(cr[NX + 2 * q + 1], cr[NX + 2 * q], 0x06040200u);
+        apply_skip<C>(a, cb, a.row0 + yy, R, center, o4);
+      }
+      if (a.has_epi) lut16(luts + 512, o4);
+      store_out<EXP, SAUX>(o4, rout, yy < ye, a.out_org + (uint32_t)((int64_t)yy * a.out_pitch), lout, xb, lane);
+    }
+  }
+  band_margins<C, EXP ? 3 : C>(a, t);
+}
+
+// ------------------------------------------------------------------------------
+// dispatch
+// ------------------------------------------------------------------------------
+// Resident workgroups per device for a kernel (occupancy x CUs), cached.
+inline int resident_slots(const void* fn) {
+  static std::mutex mu;
+  static std::map<std::pair<const void*, int>, int> cache;
+  int dev = 0;
+  HIP_CHECK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find({fn, dev});
+  if (it != cache.end()) return it->second;
+  int per_cu = 0, cus = 0;
+  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kNT, 0));
+  HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  const int slots = std::max(1, per_cu) * std::max(1, cus);
+  cache[{fn, dev}] = slots;
+  return slots;
+}
+
+// Launch geometry: band height a multiple of 4 (rows are stepped in groups of 4).
+// Default band height: short bands keep the rows all resident workgroups touch
+// at once in a compact window (measured on MI355X, 16384-wide RGB: gaussian5
+// 0.323 ms/pass at 12 rows vs 0.370 ms with one tall band per workgroup, which
+// spreads the concurrent streams over the whole frame); the engine's autotuner
+// can override per shape.
+inline int env_nxcd() {
+  static const int v = [] {
+    const char* e = std::getenv("STRIPE_XCD");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+
+inline void plan_bands(KArgs& a, dim3& grid, int tiles, int n0, int n1, int band, int R, int slots) {
+  (void)slots;
+  a.nxcd = env_nxcd();
+  if (band <= 0) band = R >= 3 ? 16 : 12;
+  band = (int)align_up(band, 4);
+  a.band = band;
+  a.nb0 = (int)div_up(n0, band);
+  a.nbands = a.nb0 + (int)div_up(n1, band);
+  a.ntx = tiles;
+  grid = dim3((unsigned)div_up((int64_t)tiles * a.nbands, kWaves));
+}
+
+template <int C, class F, int PRO, bool EXP = false>
+void launch_one(bool skip, bool nt, KArgs a, int tiles, int n0, int n1, int band, hipStream_t s) {
+  using K = void (*)(KArgs);
+  dim3 grid;
+  if constexpr (F::SEP) {
+    const K fns[4] = {k_sep<C, F, PRO, false, 0, EXP>, k_sep<C, F, PRO, false, kNtAux, EXP>,
+                      k_sep<C, F, PRO, true, 0, EXP>, k_sep<C, F, PRO, true, kNtAux, EXP>};
+    const K fn = fns[2 * skip + nt];
+    plan_bands(a, grid, tiles, n0, n1, band, F::R, resident_slots((const void*)fn));
+    fn<<<grid, kNT, 0, s>>>(a);
+  } else {
+    const K fns[4] = {k_direct<C, F, PRO, false, 0, EXP>, k_direct<C, F, PRO, false, kNtAux, EXP>,
+                      k_direct<C, F, PRO, true, 0, EXP>, k_direct<C, F, PRO, true, kNtAux, EXP>};
+    const K fn = fns[2 * skip + nt];
+    plan_bands(a, grid, tiles, n0, n1, band, F::R, resident_slots((const void*)fn));
+    fn<<<grid, kNT, 0, s>>>(a);
+  }
+}
+
+template <int PRO, class F>
+void launch_gray_out(bool expand, bool skip, bool nt, const KArgs& a, int tiles, int n0, int n1, int band,
+                     hipStream_t s) {
+  if (expand) launch_one<1, F, PRO, true>(skip, nt, a, tiles, n0, n1, band, s);
+  else launch_one<1, F, PRO, false>(skip, nt, a, tiles, n0, n1, band, s);
+}
+
+template <class F>
+void launch_filter(const Pass& p, const KArgs& a, int tiles, int n0, int n1, int band, bool nt, hipStream_t s) {
+  const bool gray = p.pro.gray;
+  const bool lut = p.pro.has_post;
+  const bool skip = p.border == Border::Skip;
+  const bool ex = p.epi_expand;
+  if (p.cmid == 3) {
+    STRIPE_CHECK(!gray && !ex, "gray prologue / expand epilogue need a 1-channel stencil");
+    if (lut) launch_one<3, F, PRO_LUT>(skip, nt, a, tiles, n0, n1, band, s);
+    else launch_one<3, F, PRO_NONE>(skip, nt, a, tiles, n0, n1, band, s);
+  } else {
+    if (gray && a.gmode == 1) launch_gray_out<PRO_GRAYLUT, F>(ex, skip, nt, a, tiles, n0, n1, band, s);
+    else if (gray) launch_gray_out<PRO_GRAY, F>(ex, skip, nt, a, tiles, n0, n1, band, s);
+    else if (lut) launch_gray_out<PRO_LUT, F>(ex, skip, nt, a, tiles, n0, n1, band, s);
+    else launch_gray_out<PRO_NONE, F>(ex, skip, nt, a, tiles, n0, n1, band, s);
+  }
+}
+
+
+// Every filter F has launch_filter<F> compiled in exactly one stencil_inst_*.hip.
+#define STRIPE_LAUNCH_FILTER_SIG(F) \
+  void launch_filter<sdef::F>(const Pass&, const KArgs&, int, int, int, int, bool, hipStream_t)
+#define STRIPE_EXTERN_LAUNCH_FILTER(F) extern template STRIPE_LAUNCH_FILTER_SIG(F);
+#define STRIPE_INSTANTIATE_LAUNCH_FILTER(F) template STRIPE_LAUNCH_FILTER_SIG(F);
+#define STRIPE_STENCIL_FILTERS(X) \
+  X(Emboss3) X(Emboss5) X(Sharpen) X(Laplace) X(Sobel) X(SobelL2) X(Gaussian3) X(Gaussian5) X(Gaussian7) X(Box3) \
+  X(Box5)
+
+}  // namespace dev
+}  // namespace stripe

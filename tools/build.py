@@ -48,6 +48,10 @@ CORE_SOURCES = [
     "core/golden.cpp",
     "hip/pointwise.hip",
     "hip/stencil.hip",
+    "hip/stencil_inst_a.hip",
+    "hip/stencil_inst_b.hip",
+    "hip/stencil_inst_c.hip",
+    "hip/stencil_inst_d.hip",
     "hip/conv.hip",
     "hip/blur_sep.hip",
     "hip/dispatch.cpp",
