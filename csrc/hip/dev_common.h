@@ -61,6 +61,7 @@ constexpr uint32_t kOOB = 0x80000000u;  // lane offset bias that fails the range
 constexpr int kLoadAux = 0;
 constexpr int kNtAux = 2;
 constexpr int64_t kNtMinBytes = 224ll << 20;
+constexpr int kXcdCount = 8;  // MI355X: 8 XCDs of 32 CUs, one L2 each
 
 __device__ __forceinline__ int border_index_dev(int i, int n, int b) {
   if (i >= 0 && i < n) return i;

@@ -173,6 +173,13 @@ void launch_stencil(const Pass& p, const PassConsts& pc, const PassLaunch& L, hi
   const int64_t pass_bytes = (int64_t)(n0 + n1) * L.W * (p.cin + p.cout);
   bool nt = pass_bytes > dev::kNtMinBytes;
   if (const char* e = std::getenv("STRIPE_NT")) nt = std::atoi(e) != 0;  // A/B switch
+  // A pass that stays in the Infinity Cache is bound by L2 / fabric traffic: the
+  // XCD-contiguous workgroup remap turns the halo rows that vertically adjacent
+  // bands share into L2 hits (one N=8 stripe of the 16K RGB frame, gaussian5:
+  // 0.0394-0.0401 -> 0.0372 ms at 8-row bands, profiles/r2/xcd_remap_stripe.txt).
+  // A pass streaming from HBM gains nothing from it (round 1: FETCH_SIZE 1.40x ->
+  // 1.15x of ideal, time unchanged, profiles/fetch_xcd_bands_16k_r1.txt).
+  a.nxcd = pass_bytes > dev::kNtMinBytes ? 0 : dev::kXcdCount;
   using namespace sdef;
   switch (p.sid) {
     case StencilId::Emboss3: dev::launch_filter<Emboss3>(p, a, tiles, n0, n1, band, nt, s); break;

@@ -787,17 +787,21 @@ inline int resident_slots(const void* fn) {
 // 0.323 ms/pass at 12 rows vs 0.370 ms with one tall band per workgroup, which
 // spreads the concurrent streams over the whole frame); the engine's autotuner
 // can override per shape.
+// XCD-aware workgroup remap (xcd_remap): the caller sets a.nxcd (launch_stencil:
+// on for passes whose working set stays in the Infinity Cache, where halo rows
+// shared by vertically adjacent bands become L2 hits); STRIPE_XCD=<n> forces it
+// (0 = off) for A/B runs.
 inline int env_nxcd() {
   static const int v = [] {
     const char* e = std::getenv("STRIPE_XCD");
-    return e ? std::atoi(e) : 0;
+    return e ? std::atoi(e) : -1;
   }();
   return v;
 }
 
 inline void plan_bands(KArgs& a, dim3& grid, int tiles, int n0, int n1, int band, int R, int slots) {
   (void)slots;
-  a.nxcd = env_nxcd();
+  if (env_nxcd() >= 0) a.nxcd = env_nxcd();
   if (band <= 0) band = R >= 3 ? 16 : 12;
   band = (int)align_up(band, 4);
   a.band = band;
