@@ -9,6 +9,8 @@
 // rows are computed, then the boundary rows.
 #pragma once
 
+#include "stripe/cpu_exec.h"
+
 #include <hip/hip_runtime.h>
 
 #include <memory>
@@ -117,6 +119,8 @@ class Engine {
   int rank() const { return rank_; }
   int world() const { return world_; }
   bool device() const { return cfg_.backend == BackendKind::Device; }
+  // host backend: threads one rank's passes use (the hardware shared by the ranks)
+  int host_threads() const { return cpu_threads(world_); }
   int out_channels() const { return plan_.cout; }
   hipStream_t stream() const { return s_compute_; }
   // Run everything on an externally owned stream (e.g. torch's current stream).

@@ -17,6 +17,7 @@
 #include "stripe/engine.h"
 #include "stripe/trace.h"
 #include "stripe/golden.h"
+#include "stripe/cpu_exec.h"
 #include "stripe/image.h"
 #include "stripe/partition.h"
 
@@ -153,6 +154,18 @@ PYBIND11_MODULE(_C, m) {
     }
     return image_to_numpy(out);
   }, py::arg("image"), py::arg("chain"), py::arg("border") = "reflect101", py::arg("fuse") = true);
+  m.def("cpu_apply", [](const U8Array& a, const std::string& chain, const std::string& border, bool fuse,
+                        int threads) {
+    Image img = image_from_numpy(a);
+    Image out;
+    {
+      py::gil_scoped_release nogil;
+      Plan p = compile_chain(parse_chain(chain), img.C, parse_border(border), fuse);
+      out = cpu_apply_plan(img, p, threads > 0 ? threads : cpu_threads());
+    }
+    return image_to_numpy(out);
+  }, py::arg("image"), py::arg("chain"), py::arg("border") = "reflect101", py::arg("fuse") = true,
+     py::arg("threads") = 0);
   m.def("golden_apply_unfused", [](const U8Array& a, const std::string& chain, const std::string& border) {
     Image img = image_from_numpy(a);
     Image out;

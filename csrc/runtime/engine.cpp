@@ -1,5 +1,6 @@
 // Per-rank stripe engine (see engine.h).
 #include "stripe/engine.h"
+#include "stripe/cpu_exec.h"
 
 #include "stripe/trace.h"
 
@@ -476,7 +477,7 @@ void Engine::run_pass(const Pass& p, const uint8_t* in, uint8_t* out) {
   }
   if (!device()) {
     if (xchg) exchange_halo(const_cast<uint8_t*>(in), p.cin, R, nullptr);
-    golden_pass(p, ConstView{in, pitch(p.cin)}, MutView{out, pitch(p.cout)}, cfg_.W, g, 0, rows);
+    cpu_pass(p, ConstView{in, pitch(p.cin)}, MutView{out, pitch(p.cout)}, cfg_.W, g, 0, rows, host_threads());
     return;
   }
   const size_t pi = (size_t)(&p - plan_.passes.data());
@@ -703,7 +704,8 @@ void Engine::run_deep(int iterations) {
           }
           launch_pass(p, prt_[k].pc, L, s_compute_);
         } else {
-          golden_pass(p, ConstView{in, pitch(p.cin)}, MutView{out, pitch(p.cout)}, cfg_.W, geom(), y0, y1);
+          cpu_pass(p, ConstView{in, pitch(p.cin)}, MutView{out, pitch(p.cout)}, cfg_.W, geom(), y0, y1,
+                   host_threads());
         }
         cur_ ^= 1;
       }

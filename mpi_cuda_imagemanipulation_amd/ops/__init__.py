@@ -90,7 +90,8 @@ def _engine(W, H, Cc, chain, border, fuse, device_index, halo=True):
 
 
 def apply(image, chain: str, border: str = "reflect101", fuse: bool = True):
-    """Apply a filter chain to one image (tensor on GPU -> HIP; numpy/CPU -> golden)."""
+    """Apply a filter chain to one image (tensor on GPU -> HIP kernels; numpy / CPU
+    tensor -> the threaded host executor, bit-identical to the golden path)."""
     if _is_tensor(image) and image.is_cuda:
         if image.dtype != torch.uint8:
             raise TypeError("image tensor must be uint8")
@@ -119,7 +120,7 @@ def apply(image, chain: str, border: str = "reflect101", fuse: bool = True):
         raise TypeError("image must be uint8")
     if arr.ndim == 3 and arr.shape[2] == 1:
         arr = arr[:, :, 0]
-    out = C.golden_apply(np.ascontiguousarray(arr), chain, border, fuse)
+    out = C.cpu_apply(np.ascontiguousarray(arr), chain, border, fuse)
     return torch.from_numpy(out) if was_tensor else out
 
 

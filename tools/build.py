@@ -46,6 +46,7 @@ CORE_SOURCES = [
     "core/partition.cpp",
     "core/image.cpp",
     "core/golden.cpp",
+    "core/cpu_exec.cpp",
     "hip/pointwise.hip",
     "hip/stencil.hip",
     "hip/stencil_inst_a.hip",
@@ -60,6 +61,9 @@ CORE_SOURCES = [
     "runtime/engine.cpp",
     "runtime/trace.cpp",
 ]
+# plain host C++ (no device compilation): CPU multiversioning (target_clones)
+# exists only for the host target
+HOST_ONLY = {"core/cpu_exec.cpp"}
 BINDING_SOURCES = ["python/bindings.cpp"]
 CLI_SOURCES = ["cli/main.cpp"]
 
@@ -148,6 +152,8 @@ def compile_one(src: str, extra: list[str], hdr_mtime: float, verbose: bool, obj
     cmd = [HIPCC, *common_flags(), *extra]
     if src.endswith(".hip"):
         cmd += ["-x", "hip", "-Rpass-analysis=kernel-resource-usage"]
+    elif src in HOST_ONLY:
+        cmd += ["-x", "c++"]
     tmp = o.with_name(f"{o.name}.{os.getpid()}.tmp")  # concurrent builds: rename whole objects only
     cmd += ["-c", str(s), "-o", str(tmp)]
     if verbose:
