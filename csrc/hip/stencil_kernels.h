@@ -552,19 +552,18 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : (SKIP && EXP ? 3 : 4))) void 
         const i16x2 gy = as_i16x2(sym_pair(wd, WLO + 2 * pp, C, PkAddU16{})) +
                          (as_i16x2(pair_at(wd, WLO + 2 * pp)) << (short)1);
         if constexpr (F::L2) {
-          // round(sqrt(gx^2 + gy^2)) exactly: f32 sqrt lands within one of
-          // isqrt(n) (n < 2^21), two integer corrections make it exact, and the
-          // rounding is k + (n > k^2 + k) (sqrt(n) is never a half-integer)
+          // min(round(sqrt(n)), 255), n = gx^2 + gy^2, exactly, in f32: only
+          // n <= 65536 matters (a larger root saturates), n is exact in f32, and
+          // there sqrt(n) stays >= 0.25 / (2 * 256.5) ~ 4.9e-4 away from every
+          // k + 1/2 (|n - (k + 1/2)^2| >= 1/4), far beyond v_sqrt_f32's 1 ulp
+          // (3e-5 at 256): rounding the f32 root to nearest is exact (no ties).
+          // (Integer corrections of a truncated root cost 2.7x this pass's time.)
           uint32_t hv[2];
 #pragma unroll
           for (int e = 0; e < 2; ++e) {
-            const int xg = gx[e], yg = gy[e];
-            const int n = xg * xg + yg * yg;
-            int k = (int)__builtin_sqrtf((float)n);
-            k -= k * k > n ? 1 : 0;
-            k += (k + 1) * (k + 1) <= n ? 1 : 0;
-            k += n > k * k + k ? 1 : 0;
-            hv[e] = (uint32_t)min(k, 255);
+            const float fx = (float)gx[e], fy = (float)gy[e];
+            const float n = __builtin_fminf(__builtin_fmaf(fx, fx, fy * fy), 65536.0f);
+            hv[e] = min((uint32_t)__builtin_rintf(__builtin_amdgcn_sqrtf(n)), 255u);
           }
           h[pp] = hv[0] | (hv[1] << 16);
         } else {
