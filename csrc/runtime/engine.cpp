@@ -727,7 +727,10 @@ std::vector<int> Engine::bands() const {
 void Engine::autotune_bands() {
   tuned_ = true;
   if (!device() || cfg_.band > 0 || stripe().rows == 0) return;
-  const int cand[] = {8, 12, 16, 24, 32};
+  // 4-row bands pay off on small per-rank stripes, where a launch has too few
+  // waves to hide each wave's row-step latency (8192x2048 gray sobel, one
+  // rank's share of config 3 at N=4: 0.0125 ms at 4 rows vs 0.0150 at 12)
+  const int cand[] = {4, 8, 12, 16, 24, 32};
   hipEvent_t e0 = ev_[6], e1 = ev_[7];
   for (size_t i = 0; i < plan_.passes.size(); ++i) {
     const Pass& p = plan_.passes[i];

@@ -208,8 +208,25 @@ def test_autotune_bands_keep_output_exact(m, chain):
     e.synchronize()
     bands = e.bands
     assert len(bands) == len(C.plan_info(chain, 3)["passes"])
-    assert all(b in (0, 8, 12, 16, 24, 32) for b in bands), bands
+    assert all(b in (0, 4, 8, 12, 16, 24, 32) for b in bands), bands
     assert any(b > 0 for b in bands)
     got = e.store_packed()
     ref = C.golden_apply(img, chain, "reflect101", True)
     assert (got == ref).all()
+
+
+@pytest.mark.parametrize("chain", ["gaussian5", "emboss5", "sobel", "gaussian7", "sharpen",
+                                   "gray:ref,contrast:3.5,emboss3@skip,expand", "gray,gaussian5"])
+@pytest.mark.parametrize("band", [4, 8, 20])
+def test_explicit_band_heights_exact(m, chain, band):
+    """Every band height the autotuner may pick (4-row bands included: shorter
+    than k_direct's K-row steps for emboss5) leaves the stencil output exact."""
+    C = m._C
+    img = m.utils.synthetic_image(6, 333, 101, 3)
+    cfg = m.Pipeline(chain).config(333, 101, 3, "device", device=0)
+    cfg.band = band
+    e = C.Engine(cfg)
+    e.load_packed(np.ascontiguousarray(img))
+    e.run(1)
+    e.synchronize()
+    assert (e.store_packed() == C.golden_apply(img, chain, "reflect101", True)).all()
