@@ -347,7 +347,7 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
   STRIPE_CHECK(L.in_bytes > 0 && L.in_bytes < (int64_t)dev::kOOB && L.out_bytes > 0 &&
                    L.out_bytes < (int64_t)dev::kOOB - 65536,
                "stripe buffers must be < 2 GiB - 64 KiB for buffer-descriptor addressing");
-  STRIPE_CHECK(L.in_org >= kMarginBytes && L.out_org >= kMarginBytes && L.in_zero >= kMarginBytes,
+  STRIPE_CHECK((L.rebased || (L.in_org >= kMarginBytes && L.out_org >= kMarginBytes)) && L.in_zero >= kMarginBytes,
                "bad origin offsets");
   dev::SepArgs sa{};
   dev::KArgs& a = sa.a;

@@ -313,7 +313,7 @@ void launch_conv_mfma(const Pass& p, const PassConsts& pc, const PassLaunch& L, 
   STRIPE_CHECK(L.in_base && L.in_bytes > 0 && L.in_bytes < (int64_t)dev::kOOB && L.out_base && L.out_bytes > 0 &&
                    L.out_bytes < (int64_t)dev::kOOB,
                "conv launch needs the allocation view (< 2 GiB buffers)");
-  STRIPE_CHECK(L.in_org >= kMarginBytes && L.out_org >= kMarginBytes && L.in_zero >= kMarginBytes,
+  STRIPE_CHECK((L.rebased || (L.in_org >= kMarginBytes && L.out_org >= kMarginBytes)) && L.in_zero >= kMarginBytes,
                "bad origin offsets");
   dev::ConvArgs ca{};
   dev::KArgs& a = ca.a;

@@ -145,7 +145,7 @@ void launch_stencil(const Pass& p, const PassConsts& pc, const PassLaunch& L, hi
   STRIPE_CHECK(L.in_bytes > 0 && L.in_bytes < (int64_t)dev::kOOB && L.out_bytes > 0 &&
                    L.out_bytes < (int64_t)dev::kOOB,
                "stripe buffers must be < 2 GiB for buffer-descriptor addressing");
-  STRIPE_CHECK(L.in_org >= kMarginBytes && L.out_org >= kMarginBytes && L.in_zero >= kMarginBytes,
+  STRIPE_CHECK((L.rebased || (L.in_org >= kMarginBytes && L.out_org >= kMarginBytes)) && L.in_zero >= kMarginBytes,
                "bad origin offsets");
   a.in_base = L.in_base;
   a.out_base = L.out_base;
@@ -212,7 +212,7 @@ void launch_conv_small(const Pass& p, const PassLaunch& L, hipStream_t s) {
   STRIPE_CHECK(L.in_bytes > 0 && L.in_bytes < (int64_t)dev::kOOB && L.out_bytes > 0 &&
                    L.out_bytes < (int64_t)dev::kOOB,
                "stripe buffers must be < 2 GiB for buffer-descriptor addressing");
-  STRIPE_CHECK(L.in_org >= kMarginBytes && L.out_org >= kMarginBytes && L.in_zero >= kMarginBytes,
+  STRIPE_CHECK((L.rebased || (L.in_org >= kMarginBytes && L.out_org >= kMarginBytes)) && L.in_zero >= kMarginBytes,
                "bad origin offsets");
   dev::ConvSmallArgs ca{};
   dev::KArgs& a = ca.a;

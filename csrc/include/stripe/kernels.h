@@ -53,6 +53,10 @@ struct PassLaunch {
   int64_t in_bytes = 0, in_org = 0, in_zero = 0;
   uint8_t* out_base = nullptr;
   int64_t out_bytes = 0, out_org = 0;
+  // Set by launch_pass when it splits a launch whose buffers exceed the
+  // descriptor range: the views are re-based on each row chunk, so origin
+  // offsets may precede the base (they wrap in the kernels' 32-bit offsets).
+  bool rebased = false;
 };
 
 void launch_pass(const Pass& p, const PassConsts& pc, const PassLaunch& L, hipStream_t s);
