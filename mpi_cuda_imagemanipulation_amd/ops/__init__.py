@@ -2,9 +2,12 @@
 
 * torch CUDA (ROCm) uint8 tensors run on the HIP kernels (csrc/hip/*.hip) on
   torch's current stream;
-* numpy arrays / CPU tensors run on the C++ golden path (bit-exact spec).
+* numpy arrays / CPU tensors run on the threaded host executor
+  (csrc/core/cpu_exec.cpp, bit-identical to the C++ golden path).
 
-Images are HxW (gray) or HxWx3 (RGB, PPM channel order) uint8.  A chain is a
+Images are HxW (gray) or HxWx3 (RGB, PPM channel order) uint8; a batch of
+frames is BxHxWxC (C = 1 or 3) and runs frame by frame through one cached
+engine (same kernels, no per-frame setup).  A chain is a
 comma-separated filter list, e.g. "gray:ref,contrast:3.5,emboss3" (see
 `FILTERS`); consecutive pointwise ops are fused into the neighbouring stencil
 kernel.  Reference kernels: grayscaleKernel / contrastKernel / embossKernel
@@ -91,7 +94,15 @@ def _engine(W, H, Cc, chain, border, fuse, device_index, halo=True):
 
 def apply(image, chain: str, border: str = "reflect101", fuse: bool = True):
     """Apply a filter chain to one image (tensor on GPU -> HIP kernels; numpy / CPU
-    tensor -> the threaded host executor, bit-identical to the golden path)."""
+    tensor -> the threaded host executor, bit-identical to the golden path).
+    A 4-D BxHxWxC input is a batch of frames; the result stacks the frames."""
+    if image.ndim == 4:
+        if image.shape[3] not in (1, 3):
+            raise ValueError(f"a batch must be BxHxWxC with C in (1, 3), got {tuple(image.shape)}")
+        outs = [apply(image[b], chain, border, fuse) for b in range(image.shape[0])]
+        if _is_tensor(image):
+            return torch.stack(outs) if outs else image.new_empty((0,) + tuple(image.shape[1:]))
+        return np.stack(outs) if outs else np.empty((0,) + tuple(image.shape[1:]), np.uint8)
     if _is_tensor(image) and image.is_cuda:
         if image.dtype != torch.uint8:
             raise TypeError("image tensor must be uint8")

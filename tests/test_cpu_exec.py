@@ -52,3 +52,13 @@ def test_ops_apply_numpy_uses_host_executor(rng):
     img = rng.integers(0, 256, size=(50, 80, 3), dtype=np.uint8)
     assert (m.ops.apply(img, "gray:ref,contrast:3.5,emboss3@skip,expand") ==
             m._C.golden_apply(img, "gray:ref,contrast:3.5,emboss3@skip,expand", "reflect101", True)).all()
+
+
+def test_batched_frames_numpy(C, rng):
+    import mpi_cuda_imagemanipulation_amd as m
+
+    imgs = rng.integers(0, 256, size=(3, 20, 33, 3), dtype=np.uint8)
+    got = m.ops.apply(imgs, "gray,sobel")
+    assert got.shape == (3, 20, 33)
+    for b in range(3):
+        assert (got[b] == C.golden_apply(imgs[b], "gray,sobel", "reflect101", True)).all()

@@ -161,3 +161,13 @@ def test_large_frame_gaussian5(m):
     got = _run(m, img, "gaussian5")
     ref = m._C.golden_apply(img, "gaussian5", "reflect101", True)
     assert (got == ref).all()
+
+
+def test_batched_frames(m, rng):
+    # BxHxWxC runs frame by frame through one cached engine; equals per-frame results
+    imgs = rng.integers(0, 256, size=(4, 37, 91, 3), dtype=np.uint8)
+    x = torch.from_numpy(imgs).cuda()
+    for chain in ("gaussian5", "gray:ref,contrast:3.5,emboss3"):
+        got = m.ops.apply(x, chain).cpu().numpy()
+        for b in range(4):
+            assert (got[b] == m._C.golden_apply(imgs[b], chain, "reflect101", True)).all(), (chain, b)
