@@ -37,6 +37,7 @@ struct KArgs {
   int gshift[3];
   int cin;        // pointwise: input channels
   int nxcd;       // > 1: XCD-aware workgroup remap over this many L2 domains
+  int hdpp;       // separable stencils: neighbour lanes' vertical sums by DPP instead of LDS
   // buffer-descriptor view (stencil kernels): offsets of the origins in the
   // allocations; every hot-loop load/store is a raw buffer op whose range check
   // masks inactive lanes (no divergent branches around memory ops, so hipcc's
