@@ -2,7 +2,7 @@
 # Restored-tree validation: full GPU suite, smoke, headline bench, rocprofv3 kernel
 # trace of the bench, blur:31 timings (baseline of the blur scheduling work).
 set -o pipefail
-O=gpurun_out/r2d
+O=gpurun_out/${R2D_OUT:-r2d}
 mkdir -p $O
 export PYTHONUNBUFFERED=1
 timeout -k 10 900 python -u -m pytest tests/ -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
