@@ -178,31 +178,46 @@ def main():
     stages = {"resident": {k: round(v, 4) for k, v in dp.stage_times().items() if k in ("compute", "halo")}}
 
     # ---- dist scope (root -> scatter -> filter -> gather -> root) ----
-    dist_mpx = None
+    # sequential: scatter(), run(1), gather() (the reference's order, kernel.cu:135-225);
+    # pipelined (> 1 rank, single-pass chains): Engine::run_dist, stripes shipped with
+    # their halo rows in row chunks, chunk k filtered while later chunks arrive and
+    # gathered while they are filtered
+    dist_mpx = dist_seq_mpx = None
+    dist_chunks = dp.engine.dist_chunks(8)
     if a.dist_steps > 0:
         if rank == 0:
             dp.engine.load_root_synthetic(a.seed)
         dp.synchronize()
-        for _ in range(2):
+
+        def seq_step():
             dp.scatter()
             dp.run(1)
             dp.gather()
-        dp.synchronize()
-        sync()
-        barrier()
-        t0 = time.perf_counter()
-        for _ in range(a.dist_steps):
-            dp.scatter()
-            dp.run(1)
-            dp.gather()
-        dp.synchronize()
-        sync()
-        barrier()
-        t1 = time.perf_counter()
-        dms = max_over_ranks((t1 - t0) * 1e3) / a.dist_steps
-        dist_mpx = W * H / (dms * 1e-3) / 1e6
+
+        def time_dist(step):
+            for _ in range(2):
+                step()
+            dp.synchronize()
+            sync()
+            barrier()
+            t0 = time.perf_counter()
+            for _ in range(a.dist_steps):
+                step()
+            dp.synchronize()
+            sync()
+            barrier()
+            t1 = time.perf_counter()
+            dms = max_over_ranks((t1 - t0) * 1e3) / a.dist_steps
+            return W * H / (dms * 1e-3) / 1e6
+
+        dist_seq_mpx = time_dist(seq_step)
         stages["dist"] = {k: round(v, 4) for k, v in dp.stage_times().items()
                           if k in ("scatter", "compute", "halo", "gather")}
+        dist_mpx = dist_seq_mpx
+        if dist_chunks > 0:
+            dist_mpx = time_dist(lambda: dp.engine.run_dist(8))
+            stages["dist_pipelined"] = {k: round(v, 4) for k, v in dp.stage_times().items()
+                                        if k in ("scatter", "compute", "gather")}
 
     # ---- e2e scope (pinned host stripe -> H2D -> filter -> D2H -> pinned host) ----
     e2e_mpx = None
@@ -249,6 +264,8 @@ def main():
                 "scope": "resident: halo exchange + full-frame filter per step",
             },
             "dist_scope_mpx_s": None if dist_mpx is None else round(dist_mpx, 1),
+            "dist_sequential_mpx_s": None if dist_seq_mpx is None else round(dist_seq_mpx, 1),
+            "dist_chunks": dist_chunks,
             "e2e_scope_mpx_s": None if e2e_mpx is None else round(e2e_mpx, 1),
             "verified_vs_golden": verify,
             "tuned_band_rows": dp.engine.bands,

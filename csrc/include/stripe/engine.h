@@ -43,6 +43,8 @@ struct EngineConfig {
   bool autotune = false;        // time candidate band heights per stencil pass on first run()
   bool pipeline = true;         // iterated single-pass chains over > 1 ranks: core / rim /
                                 // boundary rows on two streams (Engine::run_pipelined)
+  int dist_chunks = 0;          // > 1: run_rank ships, filters and gathers single-pass chains in
+                                // this many overlapped row chunks (Engine::run_dist)
   int halo_depth = 0;           // iterated single-pass chains over > 1 ranks: iterations per
                                 // halo exchange ("deep halo": k*R rows exchanged once, the
                                 // k steps recompute a shrinking band of the neighbours' rows;
@@ -148,6 +150,13 @@ class Engine {
   // ---- output ----
   void store_packed(void* dst, bool dst_device);          // own output stripe, packed
   void gather();                                          // every stripe -> root output buffer
+  // scatter(); run(1); gather() as one pipelined call: single-pass stencil /
+  // pointwise chains over > 1 ranks ship each stripe with its halo rows in
+  // `chunks` row chunks, filter chunk k once chunk k + 1 has landed and gather
+  // it while later chunks are still arriving (falls back to the three calls)
+  void run_dist(int chunks = 8);
+  // chunks run_dist(chunks) actually pipelines (0: it falls back)
+  int dist_chunks(int chunks) const;
   void store_root(void* full, bool dst_device);           // rank 0: root output buffer, packed
 
   // ---- end-to-end (host -> device -> host) ----
@@ -225,6 +234,7 @@ class Engine {
   bool own_streams_ = false;   // s_comm_ (and the e2e streams) are ours
   bool own_compute_ = false;   // s_compute_ is ours (false after use_external_stream)
   hipEvent_t ev_[8] = {};
+  std::vector<hipEvent_t> dist_ev_;  // run_dist: per-chunk transfer / compute events
   // captured hipGraph of one cycle of iterations (1 if the pass count is even,
   // 2 if odd, so the ping-pong buffers return to the start), per start buffer
   hipGraphExec_t gexec_[2] = {};

@@ -257,7 +257,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("autotune", &EngineConfig::autotune)
       .def_readwrite("graphs", &EngineConfig::graphs)
       .def_readwrite("pipeline", &EngineConfig::pipeline)
-      .def_readwrite("halo_depth", &EngineConfig::halo_depth);
+      .def_readwrite("halo_depth", &EngineConfig::halo_depth)
+      .def_readwrite("dist_chunks", &EngineConfig::dist_chunks);
 
   py::class_<PhaseTimes>(m, "PhaseTimes")
       .def_readonly("run", &PhaseTimes::run)
@@ -361,6 +362,11 @@ PYBIND11_MODULE(_C, m) {
         py::gil_scoped_release nogil;
         e.gather();
       })
+      .def("run_dist", [](Engine& e, int chunks) {
+        py::gil_scoped_release nogil;
+        e.run_dist(chunks);
+      }, py::arg("chunks") = 8)
+      .def("dist_chunks", &Engine::dist_chunks, py::arg("chunks"))
       .def("store_packed_ptr", [](Engine& e, uintptr_t p, bool dev) {
         py::gil_scoped_release nogil;
         e.store_packed(reinterpret_cast<void*>(p), dev);

@@ -164,6 +164,7 @@ Engine::~Engine() {
       if (g) (void)hipGraphExecDestroy(g);
     for (auto& e : pev_)
       if (e) (void)hipEventDestroy(e);
+    for (auto& e : dist_ev_) (void)hipEventDestroy(e);
     if (s_edge_) (void)hipStreamDestroy(s_edge_);
     for (auto& e : ev_h2d_) (void)hipEventDestroy(e);
     for (auto& e : ev_cmp_) (void)hipEventDestroy(e);
@@ -1078,6 +1079,167 @@ void Engine::gather() {
   stage_end(Stage::Gather, s_compute_);
 }
 
+// ---------------------------------------------------------------------------
+// Pipelined distributed step (the reference's timed window, kernel.cu:135-225:
+// Scatter, the chain, Gather, there strictly one after the other).
+//
+// The root holds the whole frame, so it ships every stripe together with its
+// halo rows (no neighbour exchange) in n row chunks.  Rank r's chunk k is
+// filtered once chunk k + 1 (the R rows below it) has landed, and its output
+// travels back in the grouped call that ships chunk k + 2, so each peer's
+// xGMI link carries scatter and gather traffic in opposite directions at once
+// and the compute hides under the transfers:
+//   comm stream    T0 | T1 | T2+G0 | T3+G1 | ... | T(n-1)+G(n-3) | G(n-2)+G(n-1)
+//   compute stream      C0 (after T1) | C1 (after T2) | ... | C(n-1) (after T(n-1))
+// Every active rank derives the same n from the partition, so the grouped
+// calls match across ranks.  Only single-pass stencil / pointwise chains (the
+// pass reads exactly rows y - R .. y + R); anything else runs the three calls.
+// ---------------------------------------------------------------------------
+int Engine::dist_chunks(int chunks) const {
+  if (!comm_ || part_.active <= 1 || chunks < 2 || plan_.passes.size() != 1) return 0;
+  const Pass& p = plan_.passes[0];
+  if (p.kind != PassKind::Separable && p.kind != PassKind::Direct && p.kind != PassKind::Pointwise) return 0;
+  if (cfg_.halo && p.R > halo_) return 0;
+  int minrows = std::numeric_limits<int>::max();
+  for (int r = 0; r < part_.active; ++r) minrows = std::min(minrows, part_.of(r).rows);
+  const int n = std::min(chunks, minrows / std::max(1, p.R));  // every chunk holds >= R rows
+  return n >= 2 ? n : 0;
+}
+
+void Engine::run_dist(int chunks) {
+  const int n = dist_chunks(chunks);
+  const Stripe& st = stripe();
+  if (n == 0 || st.rows == 0) {
+    if (n == 0) {
+      scatter();
+      run(1);
+      gather();
+    }
+    return;  // idle rank of a pipelined group: no traffic, no rows
+  }
+  if (cfg_.autotune && !tuned_) autotune_bands();  // before any chunk lands in the buffers it uses
+  const Pass& p = plan_.passes[0];
+  const int R = p.R, cin = plan_.cin, cout = plan_.cout;
+  const int64_t Pin = pitch(cin), Pout = pitch(cout);
+  STRIPE_CHECK(rank_ != 0 || (root_in_.data() && root_out_.data()),
+               "root buffers not allocated (EngineConfig::root_buffers)");
+  TraceRange tr("stripe.dist");
+  fault_point("scatter", rank_);
+  // row range [lo, hi) of rank r's transfer k (halo rows ride on the first and last chunk)
+  auto cut = [&](int r, int k) { return (int)((int64_t)part_.of(r).rows * k / n); };
+  auto span = [&](int r, int k, int& lo, int& hi) {
+    const bool h = cfg_.halo && R > 0;
+    lo = cut(r, k) - (k == 0 && h && r > 0 ? R : 0);
+    hi = cut(r, k + 1) + (k == n - 1 && h && r + 1 < part_.active ? R : 0);
+  };
+  const uint8_t* rin = rank_ == 0 ? root_origin(root_in_, cin) - kMarginBytes : nullptr;
+  uint8_t* rout = rank_ == 0 ? root_origin(root_out_, cout) - kMarginBytes : nullptr;
+  uint8_t* in_org = origin(buf_[0], cin);
+  uint8_t* out_org = origin(buf_[1], cout);
+  const bool dev = device();
+  auto local_copy = [&](void* dst, const void* src, size_t bytes) {
+    if (dev) HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s_comm_));
+    else std::memcpy(dst, src, bytes);
+  };
+  // one grouped call: scatter chunk k (k < n) and gather chunk j (j >= 0)
+  auto transfer = [&](int k, int j, int j2) {
+    const bool sc = k >= 0 && k < n;
+    if (rank_ == 0) {
+      comm_->group_start();
+      for (int r = 1; r < part_.active; ++r) {
+        const Stripe& sr = part_.of(r);
+        int lo, hi;
+        if (sc) {
+          span(r, k, lo, hi);
+          comm_->send(rin + (int64_t)(sr.row0 + lo) * Pin, (size_t)((hi - lo) * Pin), r, s_comm_);
+        }
+        for (int g : {j, j2})
+          if (g >= 0)
+            comm_->recv(rout + (int64_t)(sr.row0 + cut(r, g)) * Pout, (size_t)((cut(r, g + 1) - cut(r, g)) * Pout), r,
+                        s_comm_);
+      }
+      comm_->group_end();
+      int lo, hi;
+      if (sc) {
+        span(0, k, lo, hi);
+        local_copy(in_org - kMarginBytes + (int64_t)lo * Pin, rin + (int64_t)(st.row0 + lo) * Pin,
+                   (size_t)((hi - lo) * Pin));
+      }
+      for (int g : {j, j2})
+        if (g >= 0)
+          local_copy(rout + (int64_t)(st.row0 + cut(0, g)) * Pout, out_org - kMarginBytes + (int64_t)cut(0, g) * Pout,
+                     (size_t)((cut(0, g + 1) - cut(0, g)) * Pout));
+    } else {
+      comm_->group_start();
+      int lo, hi;
+      if (sc) {
+        span(rank_, k, lo, hi);
+        comm_->recv(in_org - kMarginBytes + (int64_t)lo * Pin, (size_t)((hi - lo) * Pin), 0, s_comm_);
+      }
+      for (int g : {j, j2})
+        if (g >= 0)
+          comm_->send(out_org - kMarginBytes + (int64_t)cut(rank_, g) * Pout,
+                      (size_t)((cut(rank_, g + 1) - cut(rank_, g)) * Pout), 0, s_comm_);
+      comm_->group_end();
+    }
+  };
+  auto compute = [&](int k) {
+    const int y0 = cut(rank_, k), y1 = cut(rank_, k + 1);
+    if (dev) {
+      PassLaunch L = make_launch(p, in_org, out_org, 0);
+      L.nrange = 1;
+      L.ry[0] = y0;
+      L.ry[1] = y1;
+      launch_pass(p, prt_[0].pc, L, s_compute_);
+    } else {
+      cpu_pass(p, ConstView{in_org, Pin}, MutView{out_org, Pout}, cfg_.W, geom(), y0, y1, host_threads());
+    }
+  };
+  if (dev) {
+    while ((int)dist_ev_.size() < 2 * n + 1) {
+      hipEvent_t e;
+      HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      dist_ev_.push_back(e);
+    }
+    // earlier work on the compute stream (loads, the previous step's reads of
+    // both buffers) precedes the first transfer
+    HIP_CHECK(hipEventRecord(ev_[4], s_compute_));
+    HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_[4], 0));
+  }
+  hipEvent_t* evT = dev ? dist_ev_.data() : nullptr;      // [0, n): transfer k landed
+  hipEvent_t* evC = dev ? dist_ev_.data() + n : nullptr;  // [n, 2n): chunk k filtered; [2n]: join
+  stage_begin(Stage::Scatter, s_comm_);
+  transfer(0, -1, -1);
+  record(dev ? evT[0] : nullptr, s_comm_);
+  for (int k = 0; k < n; ++k) {
+    if (k + 1 < n) {
+      if (dev && k >= 1) HIP_CHECK(hipStreamWaitEvent(s_comm_, evC[k - 1], 0));
+      if (k == 1) stage_begin(Stage::Gather, s_comm_);
+      transfer(k + 1, k - 1, -1);
+      record(dev ? evT[k + 1] : nullptr, s_comm_);
+    }
+    if (k + 1 == n - 1) stage_end(Stage::Scatter, s_comm_);  // the last chunk is on its way
+    if (dev) HIP_CHECK(hipStreamWaitEvent(s_compute_, evT[std::min(k + 1, n - 1)], 0));
+    if (k == 0) stage_begin(Stage::Compute, s_compute_);
+    compute(k);
+    record(dev ? evC[k] : nullptr, s_compute_);
+  }
+  stage_end(Stage::Compute, s_compute_);
+  if (dev) HIP_CHECK(hipStreamWaitEvent(s_comm_, evC[n - 1], 0));
+  if (n == 2) stage_begin(Stage::Gather, s_comm_);
+  transfer(-1, n - 2, n - 1);
+  stage_end(Stage::Gather, s_comm_);
+  if (dev) {  // later work on the compute stream orders behind the gather
+    HIP_CHECK(hipEventRecord(dist_ev_[2 * n], s_comm_));
+    HIP_CHECK(hipStreamWaitEvent(s_compute_, dist_ev_[2 * n], 0));
+  }
+  run_in_buf_ = 0;
+  cur_ = 1;
+  cur_c_ = cout;
+  out_buf_ = 1;
+  out_c_ = cout;
+}
+
 void Engine::store_root(void* full, bool dst_device) {
   (void)dst_device;
   if (rank_ != 0) return;
@@ -1155,9 +1317,13 @@ Image run_rank(const EngineConfig& cfg_in, Comm* comm, int device, const Image* 
   if (device >= 0) c.device = device;
   Engine e(c, comm);
   if (rank == 0) e.load_root(input->data.data(), false);
-  e.scatter();
-  e.run(iterations);
-  e.gather();
+  if (iterations == 1 && e.dist_chunks(c.dist_chunks) > 0) {
+    e.run_dist(c.dist_chunks);
+  } else {
+    e.scatter();
+    e.run(iterations);
+    e.gather();
+  }
   Image out;
   if (rank == 0) {
     out = Image(c.W, c.H, e.out_channels());

@@ -62,12 +62,16 @@ class Pipeline:
     """
 
     def __init__(self, chain: str = "gaussian5", border: str = "reflect101", halo: bool = True,
-                 legacy_partition: bool = False, fuse: bool = True, overlap: bool = True, halo_depth: int = 0):
+                 legacy_partition: bool = False, fuse: bool = True, overlap: bool = True, halo_depth: int = 0,
+                 dist_chunks: int = 0):
         self.spec = PipelineSpec(chain, border, halo, legacy_partition)
         self.fuse = fuse
         self.overlap = overlap
         # iterations per halo exchange of iterated multi-rank runs (0 = auto, 1 = every step)
         self.halo_depth = int(halo_depth)
+        # > 1: a one-iteration distributed run ships, filters and gathers single-pass
+        # chains in this many overlapped row chunks (Engine::run_dist)
+        self.dist_chunks = int(dist_chunks)
         C.parse_chain(chain)  # validate early
 
     @classmethod
@@ -102,6 +106,7 @@ class Pipeline:
         cfg.backend = C.Backend.host if backend == "host" else C.Backend.device
         cfg.autotune = bool(autotune)
         cfg.halo_depth = self.halo_depth
+        cfg.dist_chunks = self.dist_chunks
         sched = os.environ.get("STRIPE_HALO_SCHEDULE")  # tuning: overlap | pipeline | serial
         if sched:
             cfg.pipeline = sched == "pipeline"
