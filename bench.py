@@ -183,7 +183,9 @@ def main():
     # their halo rows in row chunks, chunk k filtered while later chunks arrive and
     # gathered while they are filtered
     dist_mpx = dist_seq_mpx = None
-    dist_chunks = dp.engine.dist_chunks(8)
+    # (device ranks only: host comms run each grouped call synchronously, so on
+    # CPUs the extra calls cost time and nothing overlaps)
+    dist_chunks = dp.engine.dist_chunks(8) if dev else 0
     if a.dist_steps > 0:
         if rank == 0:
             dp.engine.load_root_synthetic(a.seed)

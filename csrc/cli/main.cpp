@@ -137,6 +137,7 @@ EngineConfig config_from(const Args& a, int W, int H, int C) {
   }
   if (a.has("graphs")) cfg.graphs = true;
   cfg.halo_depth = a.geti("halo-depth", 0);
+  cfg.dist_chunks = a.geti("dist-chunks", 0);
   if (a.has("expand-gray") && cfg.chain.find("expand") == std::string::npos) cfg.chain += ",expand";
   cfg.band = a.geti("band", 0);
   const std::string be = a.get("backend", device_count() > 0 ? "local" : "host");
@@ -358,9 +359,13 @@ int cmd_bench(const Args& a) {
           const bool iterable = e.plan().cin == e.plan().cout;
           auto step = [&]() {
             if (scope == "dist") {
-              e.scatter();
-              e.run(1);
-              e.gather();
+              if (e.dist_chunks(c.dist_chunks) > 0) {
+                e.run_dist(c.dist_chunks);  // chunked scatter / filter / gather overlap
+              } else {
+                e.scatter();
+                e.run(1);
+                e.gather();
+              }
             } else if (scope == "e2e") {
               e.run_e2e(8);
             } else {
@@ -424,10 +429,11 @@ void usage() {
                "  run   --input in.ppm --output out.ppm [--chain C | --preset ref-gpu|ref-cpu] [--ranks N]\n"
                "        [--backend rccl|local|host] [--devices 0,1,..] [--border MODE] [--no-halo]\n"
                "        [--expand-gray] [--legacy-partition] [--iterations K] [--no-fuse] [--no-overlap]\n"
+               "        [--dist-chunks K]  (> 1 ranks, single-pass chains: pipelined scatter/filter/gather)\n"
                "        one process per rank: --backend rccl --world N --rank r --rendezvous FILE [--device d]\n"
                "  bench --synthetic WxHxC [--seed S] [--chain C] [--ranks 1,2,4,8] [--iters N] [--warmup N]\n"
                "        [--scope resident|device,dist,e2e] [--backend rccl|local|host] [--json out.json]\n"
-               "        [--no-overlap] [--no-pipeline] [--graphs] [--band ROWS] [--halo-depth K]\n"
+               "        [--no-overlap] [--no-pipeline] [--graphs] [--band ROWS] [--halo-depth K] [--dist-chunks K]\n"
                "  cmp   a.ppm b.ppm [--tol T]\n"
                "  gen   --synthetic WxHxC [--seed S] --output out.ppm\n"
                "  info  [--chain C] [--channels C]\n");
