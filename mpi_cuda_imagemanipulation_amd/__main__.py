@@ -43,6 +43,9 @@ def main(argv=None) -> int:
                         "rccl / gloo: one process per rank under torchrun (RANK / WORLD_SIZE env)")
     r.add_argument("--border", default=None)
     r.add_argument("--iterations", type=int, default=1)
+    r.add_argument("--dist-chunks", type=int, default=0,
+                   help="> 1 ranks, one iteration, single-pass chains: ship / filter / gather the "
+                        "stripes in this many overlapped row chunks (bit-identical)")
     c = sub.add_parser("convert", help="convert between image formats")
     c.add_argument("src")
     c.add_argument("dst")
@@ -60,6 +63,7 @@ def main(argv=None) -> int:
         pipe = models.Pipeline.preset(a.preset)
     else:
         pipe = models.Pipeline(a.chain or "gaussian5", border=a.border or "reflect101")
+    pipe.dist_chunks = a.dist_chunks
     if a.backend in ("rccl", "gloo"):
         return _run_per_process(a, pipe)
     img = utils.read_image(a.input)
@@ -98,9 +102,12 @@ def _run_per_process(a, pipe) -> int:
     if ctx.world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    dp.scatter()
-    dp.run(a.iterations)
-    dp.gather()
+    if a.iterations == 1 and dp.engine.dist_chunks(a.dist_chunks) > 0:
+        dp.engine.run_dist(a.dist_chunks)
+    else:
+        dp.scatter()
+        dp.run(a.iterations)
+        dp.gather()
     dp.synchronize()
     ms = (time.perf_counter() - t0) * 1e3
     if ctx.rank == 0:

@@ -124,8 +124,9 @@ def test_bench_host_backend_multi_rank(tmp_path, nproc, depth):
         assert rec["halo_depth"] == depth
 
 
-@pytest.mark.parametrize("nproc,preset,chain", [(3, None, "gaussian5,sobel"), (2, "ref-cpu", None)])
-def test_python_cli_one_process_per_rank(tmp_path, C, nproc, preset, chain):
+@pytest.mark.parametrize("nproc,preset,chain,chunks", [(3, None, "gaussian5,sobel", 0), (2, "ref-cpu", None, 0),
+                                                        (3, None, "gaussian5", 4), (2, "ref-cpu", None, 3)])
+def test_python_cli_one_process_per_rank(tmp_path, C, nproc, preset, chain, chunks):
     """`torchrun -m mpi_cuda_imagemanipulation_amd run --backend gloo`: the
     reference's mpiexec flow (root load, metadata broadcast, scatter, filter,
     gather, root write), one process per rank; output equals the single-rank
@@ -138,7 +139,7 @@ def test_python_cli_one_process_per_rank(tmp_path, C, nproc, preset, chain):
     sel = ["--preset", preset] if preset else ["--chain", chain]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "-m", "mpi_cuda_imagemanipulation_amd",
-           "run", "--input", str(src), "--output", str(out), "--backend", "gloo", *sel]
+           "run", "--input", str(src), "--output", str(out), "--backend", "gloo", *sel, "--dist-chunks", str(chunks)]
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1",
                PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))

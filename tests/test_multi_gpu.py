@@ -52,8 +52,8 @@ def test_torchrun_bench_rccl(n, chain, depth):
     assert rec["verified_vs_golden"] is True
 
 
-@pytest.mark.parametrize("n", [1, 2, 4])
-def test_python_cli_rccl_one_process_per_gpu(tmp_path, n):
+@pytest.mark.parametrize("n,chunks", [(1, 0), (2, 0), (4, 0), (2, 4), (4, 8)])
+def test_python_cli_rccl_one_process_per_gpu(tmp_path, n, chunks):
     """`torchrun -m mpi_cuda_imagemanipulation_amd run --backend rccl`: the
     reference's mpiexec flow with one process per GPU (n = 1 runs on every
     box: a one-rank RCCL communicator through the same scatter/gather path)."""
@@ -70,7 +70,8 @@ def test_python_cli_rccl_one_process_per_gpu(tmp_path, n):
     chain = "gray:ref,contrast:3.5,emboss3,expand"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "-m", "mpi_cuda_imagemanipulation_amd",
-           "run", "--input", str(src), "--output", str(out), "--backend", "rccl", "--chain", chain]
+           "run", "--input", str(src), "--output", str(out), "--backend", "rccl", "--chain", chain,
+           "--dist-chunks", str(chunks)]
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110, cwd=str(tmp_path))
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
