@@ -216,10 +216,13 @@ def main():
         stages["dist"] = {k: round(v, 4) for k, v in dp.stage_times().items()
                           if k in ("scatter", "compute", "halo", "gather")}
         dist_mpx = dist_seq_mpx
-        if dist_chunks > 0:
+        if dist_chunks > 0 or (dev and dp.engine.dist_direct):
+            # (one GPU: the filter reads the root frame and writes the root output
+            # directly, the scatter and gather copies vanish)
             dist_mpx = time_dist(lambda: dp.engine.run_dist(8))
-            stages["dist_pipelined"] = {k: round(v, 4) for k, v in dp.stage_times().items()
-                                        if k in ("scatter", "compute", "gather")}
+            keys = ("scatter", "compute", "gather") if dist_chunks > 0 else ("compute",)
+            stages["dist_pipelined" if dist_chunks > 0 else "dist_direct"] = {
+                k: round(v, 4) for k, v in dp.stage_times().items() if k in keys}
 
     # ---- e2e scope (pinned host stripe -> H2D -> filter -> D2H -> pinned host) ----
     e2e_mpx = None

@@ -157,6 +157,10 @@ class Engine {
   void run_dist(int chunks = 8);
   // chunks run_dist(chunks) actually pipelines (0: it falls back)
   int dist_chunks(int chunks) const;
+  // one device rank with root buffers and a single-pass stencil / pointwise
+  // chain: run_dist filters the root input straight into the root output (no
+  // scatter / gather copies; the stripe buffers then hold no output)
+  bool dist_direct() const;
   void store_root(void* full, bool dst_device);           // rank 0: root output buffer, packed
 
   // ---- end-to-end (host -> device -> host) ----

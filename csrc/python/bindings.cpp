@@ -367,6 +367,7 @@ PYBIND11_MODULE(_C, m) {
         e.run_dist(chunks);
       }, py::arg("chunks") = 8)
       .def("dist_chunks", &Engine::dist_chunks, py::arg("chunks"))
+      .def_property_readonly("dist_direct", &Engine::dist_direct)
       .def("store_packed_ptr", [](Engine& e, uintptr_t p, bool dev) {
         py::gil_scoped_release nogil;
         e.store_packed(reinterpret_cast<void*>(p), dev);

@@ -439,15 +439,20 @@ PassLaunch Engine::make_launch(const Pass& p, const uint8_t* in, uint8_t* out, i
   L.band = prt_[pi].band > 0 ? prt_[pi].band : cfg_.band;
   const Buffer* bi = nullptr;
   const Buffer* bo = nullptr;
-  for (const Buffer& b : buf_) {
-    if (in >= b.data() && in < b.data() + b.bytes()) bi = &b;
-    if (out >= b.data() && out < b.data() + b.bytes()) bo = &b;
+  // the ping-pong pair, or the root's full-frame buffers (one-rank run_dist)
+  for (const Buffer* b : {&buf_[0], &buf_[1], &root_in_, &root_out_}) {
+    if (!b->data()) continue;
+    if (in >= b->data() && in < b->data() + b->bytes()) bi = b;
+    if (out >= b->data() && out < b->data() + b->bytes()) bo = b;
   }
   STRIPE_CHECK(bi && bo && bi != bo, "pass buffers are not the engine's ping-pong pair");
   L.in_base = bi->data();
   L.in_bytes = (int64_t)bi->bytes();
   L.in_org = in - bi->data();
-  L.in_zero = (int64_t)std::max(1, rows_alloc_) * padded_pitch(cfg_.W, plan_.max_channels) + kMarginBytes;
+  // the zero row of the Constant y-border: the spare row after the ping-pong
+  // rows, or (root buffers have none) an out-of-range offset, read as zeros
+  L.in_zero = bi == &root_in_ ? (int64_t)1 << 31
+                              : (int64_t)std::max(1, rows_alloc_) * padded_pitch(cfg_.W, plan_.max_channels) + kMarginBytes;
   L.out_base = bo->data();
   L.out_bytes = (int64_t)bo->bytes();
   L.out_org = out - bo->data();
@@ -1106,7 +1111,33 @@ int Engine::dist_chunks(int chunks) const {
   return n >= 2 ? n : 0;
 }
 
+bool Engine::dist_direct() const {
+  if (!device() || part_.active != 1 || rank_ != 0 || plan_.passes.size() != 1) return false;
+  if (!root_in_.data() || !root_out_.data()) return false;
+  const Pass& p = plan_.passes[0];
+  return p.kind == PassKind::Separable || p.kind == PassKind::Direct || p.kind == PassKind::Pointwise;
+}
+
 void Engine::run_dist(int chunks) {
+  if (dist_direct()) {
+    // one rank: its stripe is the root's frame, so the pass reads the root
+    // input and writes the root output directly (scatter and gather would be
+    // two whole-frame device copies); the stripe buffers keep no output
+    if (cfg_.autotune && !tuned_) autotune_bands();
+    const Pass& p = plan_.passes[0];
+    TraceRange tr("stripe.dist");
+    fault_point("scatter", rank_);
+    stage_begin(Stage::Compute, s_compute_);
+    PassLaunch L = make_launch(p, root_origin(root_in_, plan_.cin), root_origin(root_out_, plan_.cout), 0);
+    L.nrange = 1;
+    L.ry[0] = 0;
+    L.ry[1] = L.rows;
+    launch_pass(p, prt_[0].pc, L, s_compute_);
+    stage_end(Stage::Compute, s_compute_);
+    out_buf_ = -1;
+    out_c_ = plan_.cout;
+    return;
+  }
   const int n = dist_chunks(chunks);
   const Stripe& st = stripe();
   if (n == 0 || st.rows == 0) {
@@ -1317,7 +1348,7 @@ Image run_rank(const EngineConfig& cfg_in, Comm* comm, int device, const Image* 
   if (device >= 0) c.device = device;
   Engine e(c, comm);
   if (rank == 0) e.load_root(input->data.data(), false);
-  if (iterations == 1 && e.dist_chunks(c.dist_chunks) > 0) {
+  if (iterations == 1 && c.dist_chunks > 1 && (e.dist_chunks(c.dist_chunks) > 0 || e.dist_direct())) {
     e.run_dist(c.dist_chunks);
   } else {
     e.scatter();

@@ -161,3 +161,23 @@ def test_run_dist_local_gpu_large(rng):
     a = models.Pipeline("gaussian5").run_distributed(img, 4, "local")
     b = models.Pipeline("gaussian5", dist_chunks=8).run_distributed(img, 4, "local")
     assert (a == b).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chain", ["gaussian5", "gaussian5@constant", "emboss3@constant", "sobel",
+                                   "gray:ref,contrast:3.5,emboss3@skip,expand", "invert", "gaussian5,sobel"])
+def test_run_dist_one_rank_direct(rng, chain):
+    # one GPU rank: the pass reads the root frame and writes the root output
+    # directly (no scatter / gather copies); multi-pass chains fall back
+    img = _img(rng, 131, 1029, 3)
+    cfg = models.Pipeline(chain).config(1029, 131, 3, "device", device=0)
+    cfg.root_buffers = True
+    e = C.Engine(cfg)
+    assert e.dist_direct == (chain != "gaussian5,sobel")
+    e.load_root(img)
+    e.run_dist(8)
+    got = e.store_root()
+    ref = C.golden_apply(img, chain, "reflect101", True)
+    assert got.shape == ref.shape
+    bad = np.argwhere(got != ref)
+    assert bad.size == 0, f"{chain}: {len(bad)} mismatches, first {bad[:5].tolist()}"

@@ -9,3 +9,5 @@ timeout -k 10 400 python -u -m pytest tests/test_dist_pipelined.py tests/test_gp
 tail -3 $O/pytest.log
 timeout -k 10 600 python -u -m pytest tests/ -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > $O/pytest_all.log 2>&1 || { tail -40 $O/pytest_all.log; exit 1; }
 tail -1 $O/pytest_all.log
+timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+cat $O/bench.json
