@@ -359,7 +359,7 @@ int cmd_bench(const Args& a) {
           const bool iterable = e.plan().cin == e.plan().cout;
           auto step = [&]() {
             if (scope == "dist") {
-              if (e.dist_chunks(c.dist_chunks) > 0) {
+              if (e.dist_chunks(c.dist_chunks) > 0 || (c.dist_chunks > 1 && e.dist_direct())) {
                 e.run_dist(c.dist_chunks);  // chunked scatter / filter / gather overlap
               } else {
                 e.scatter();
