@@ -414,6 +414,22 @@ PYBIND11_MODULE(_C, m) {
     return image_to_numpy(out);
   }, py::arg("config"), py::arg("world"), py::arg("image"), py::arg("iterations") = 1);
 
+  // one process driving several GPUs: one thread per rank, an in-process RCCL
+  // communicator over `devices` (ncclCommInitAll), the same run_rank flow
+  m.def("run_rccl_group", [](const EngineConfig& cfg, const std::vector<int>& devices, const U8Array& a,
+                             int iterations) {
+    Image img = image_from_numpy(a);
+    Image out;
+    {
+      py::gil_scoped_release nogil;
+      auto owned = make_rccl_comms_all(devices);
+      std::vector<Comm*> comms;
+      for (auto& c : owned) comms.push_back(c.get());
+      out = run_group(cfg, comms, devices, img, iterations);
+    }
+    return image_to_numpy(out);
+  }, py::arg("config"), py::arg("devices"), py::arg("image"), py::arg("iterations") = 1);
+
   m.attr("kMarginBytes") = kMarginBytes;
   m.attr("kMaxRadius") = kMaxRadius;
   m.def("padded_pitch", &padded_pitch);

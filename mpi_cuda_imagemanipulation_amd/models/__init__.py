@@ -116,11 +116,17 @@ class Pipeline:
     def run_distributed(self, image: np.ndarray, ranks: int, backend: str = "host", iterations: int = 1):
         """Root -> scatter -> per-rank chain with halo exchange -> gather, on `ranks`
         in-process ranks ('local' = N logical ranks sharing this process's GPU,
-        'host' = CPU golden path).  Returns the gathered output on the host."""
+        'rccl' = one rank per GPU 0..N-1, one thread each, over an in-process
+        RCCL communicator, 'host' = CPU golden path).  Returns the gathered
+        output on the host."""
         img = np.ascontiguousarray(image, dtype=np.uint8)
         H, W = img.shape[:2]
         Cc = 1 if img.ndim == 2 else img.shape[2]
+        if backend not in ("local", "host", "rccl"):
+            raise ValueError(f"backend must be local, host or rccl, got {backend!r}")
         cfg = self.config(W, H, Cc, "host" if backend == "host" else "device", device=0 if backend != "host" else -1)
+        if backend == "rccl":
+            return C.run_rccl_group(cfg, list(range(int(ranks))), img, int(iterations))
         return C.run_local_group(cfg, int(ranks), img, int(iterations))
 
 

@@ -78,3 +78,25 @@ def test_python_cli_rccl_one_process_per_gpu(tmp_path, n, chunks):
     got = m.utils.read_image(str(out))
     ref = m._C.golden_apply(img, chain, "reflect101", True)
     assert got.shape == ref.shape and np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("n,chunks,chain", [(1, 0, "gaussian5"), (1, 8, "gaussian5"), (1, 0, "gaussian5,sobel"),
+                                            (2, 0, "gaussian5"), (2, 4, "gaussian5"), (4, 8, "emboss3"),
+                                            (8, 8, "gaussian5"), (8, 0, "blur:9")])
+def test_run_distributed_rccl_in_process(n, chunks, chain):
+    """One process driving GPUs 0..n-1 (a thread per rank, ncclCommInitAll):
+    Pipeline.run_distributed(backend='rccl') equals the golden path."""
+    if _ngpus() < n:
+        pytest.skip(f"needs {n} GPUs")
+    import numpy as np
+
+    sys.path.insert(0, ROOT)
+    import mpi_cuda_imagemanipulation_amd as m
+
+    img = m.utils.synthetic_image(11, 389, 263, 3)
+    got = m.models.Pipeline(chain, dist_chunks=chunks).run_distributed(img, n, backend="rccl")
+    ref = m._C.golden_apply(img, chain, "reflect101", True)
+    if chain.startswith("blur"):
+        assert got.shape == ref.shape and np.abs(got.astype(int) - ref).max() <= 1
+    else:
+        assert got.shape == ref.shape and np.array_equal(got, ref)
