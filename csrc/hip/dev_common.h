@@ -37,7 +37,6 @@ struct KArgs {
   int gshift[3];
   int cin;        // pointwise: input channels
   int nxcd;       // > 1: XCD-aware workgroup remap over this many L2 domains
-  int hdpp;       // separable stencils: neighbour lanes' vertical sums by DPP instead of LDS
   // buffer-descriptor view (stencil kernels): offsets of the origins in the
   // allocations; every hot-loop load/store is a raw buffer op whose range check
   // masks inactive lanes (no divergent branches around memory ops, so hipcc's
@@ -62,6 +61,9 @@ constexpr uint32_t kOOB = 0x80000000u;  // lane offset bias that fails the range
 constexpr int kLoadAux = 0;
 constexpr int kNtAux = 2;
 constexpr int64_t kNtMinBytes = 224ll << 20;
+// resident workgroups per CU of nt-store (HBM-streaming) stencil launches
+constexpr int kNtWgsSep = 2;     // separable (k_sep)
+constexpr int kNtWgsDirect = 3;  // direct (k_direct) without a gray prologue
 constexpr int kXcdCount = 8;  // MI355X: 8 XCDs of 32 CUs, one L2 each
 
 __device__ __forceinline__ int border_index_dev(int i, int n, int b) {

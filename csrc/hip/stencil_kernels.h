@@ -16,9 +16,8 @@
 //     two rows in flight), applies the fused prologue (gray / LUT) in registers;
 //   * separable filters: vertical taps in registers as packed-u16 adds - the
 //     binomial Gaussians as a cascade of K-1 two-tap sums (no row ring) - the
-//     neighbour lanes' vertical sums by DPP wave shifts (default; the older
-//     route through the wave's LDS slice stays behind STRIPE_SEP_DPP=0), the
-//     horizontal taps as packed-u16 multiply-adds on v_alignbyte-shifted pairs;
+//     neighbour lanes' vertical sums by DPP wave shifts, the horizontal taps as
+//     packed-u16 multiply-adds on v_alignbyte-shifted pairs;
 //   * non-separable filters: a K-row register ring of prologue-applied rows, the
 //     neighbour lanes' edge dwords by DPP; taps are compile-time literals (zero
 //     taps vanish);
@@ -37,6 +36,7 @@
 
 #include <map>
 #include <mutex>
+#include <tuple>
 
 namespace stripe {
 namespace dev {
@@ -460,11 +460,6 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : (SKIP && EXP ? 3 : 4))) void 
   constexpr int WDW = (2 * WLO + 16) / 2;     // window dwords
   constexpr int CIN = is_gray(PRO) ? 3 : 1;  // input bytes per output byte
   using T = SepTraits<F>;
-  // per wave: one row of vertical sums, planar (plane h = dwords 4h..4h+3 of a
-  // lane's 8) so every ds_write_b128 / ds_read_b128 has a 16-byte lane stride
-  // (sobel: planes 2..3 hold the difference row)
-  constexpr int NP = F::SOBEL ? 4 : 2;
-  __shared__ __attribute__((aligned(16))) uint4 vbuf[kWaves][NP][kW];
   __shared__ __attribute__((aligned(16))) uint4 xbuf[EXP ? kWaves : 1][EXP ? 3 * kW : 1];
   __shared__ uint8_t luts[PRO == PRO_GRAYLUT ? kLutBytes : 768];
   if (PRO != PRO_NONE || a.has_epi) {
@@ -481,9 +476,7 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : (SKIP && EXP ? 3 : 4))) void 
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);
   const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
   const uint32_t last_row = in_row_off(a, ye - 1 + R);
-  uint4(*vb)[kW] = vbuf[t.wave];
   uint4* xb = xbuf[EXP ? t.wave : 0];
-  const int rl = lane == 0 ? 1 : (lane == kW - 1 ? kW - 2 : lane);  // keep LDS reads in bounds
 
   VState<F> sa, sb;
 #pragma unroll
@@ -526,46 +519,12 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : (SKIP && EXP ? 3 : 4))) void 
       vpush<F>(u, prev, next, vv);
     }
     // lanes 0 and 63 (halo chunks) compute garbage and their store is masked
+    // neighbour lanes' vertical sums by DPP wave shifts (no LDS round trip, no
+    // wave sync; 5 % faster on gray stripes than an LDS row, profiles/r2d/sep_dpp_ab.txt)
     uint32_t w[WDW];
     uint32_t wd[F::SOBEL ? WDW : 1];
-    if (a.hdpp) {
-      // neighbour lanes' vertical sums by DPP wave shifts (no LDS round trip)
-      dpp_window<WLO, WDW>(vv, w);
-      if constexpr (F::SOBEL) dpp_window<WLO, WDW>(dd, wd);
-    } else {
-    if constexpr (F::SOBEL) {
-      vb[2][lane] = make_uint4(dd[0], dd[1], dd[2], dd[3]);
-      vb[3][lane] = make_uint4(dd[4], dd[5], dd[6], dd[7]);
-    }
-    vb[0][lane] = make_uint4(vv[0], vv[1], vv[2], vv[3]);
-    vb[1][lane] = make_uint4(vv[4], vv[5], vv[6], vv[7]);
-    wave_lds_sync();
-#pragma unroll
-    for (int q = 0; q < WDW / 4; ++q) {
-      // window dword 4q is logical dword g = 8*rl - WLO/2 + 4q: lane g/8, plane (g/4)&1
-      const int g = 8 * rl - WLO / 2 + 4 * q;
-      // whole 16-byte chunks (volatile: the compiler would otherwise trim the
-      // window to the dwords it needs and issue ds_read_b32/b64/read2 pieces
-      // whose 16-byte lane stride conflicts 4-way under the (a/4)%32 banking)
-      const u32x4 v = *(volatile __attribute__((address_space(3))) u32x4*)(&vb[(g >> 2) & 1][g >> 3]);
-      w[4 * q] = v.x;
-      w[4 * q + 1] = v.y;
-      w[4 * q + 2] = v.z;
-      w[4 * q + 3] = v.w;
-    }
-    if constexpr (F::SOBEL) {
-#pragma unroll
-      for (int q = 0; q < WDW / 4; ++q) {
-        const int g = 8 * rl - WLO / 2 + 4 * q;
-        const u32x4 v = *(volatile __attribute__((address_space(3))) u32x4*)(&vb[2 + ((g >> 2) & 1)][g >> 3]);
-        wd[4 * q] = v.x;
-        wd[4 * q + 1] = v.y;
-        wd[4 * q + 2] = v.z;
-        wd[4 * q + 3] = v.w;
-      }
-    }
-    wave_lds_sync();  // reads done before the next row's writes (program order)
-    }
+    dpp_window<WLO, WDW>(vv, w);
+    if constexpr (F::SOBEL) dpp_window<WLO, WDW>(dd, wd);
     uint32_t o[4];
     if constexpr (F::SOBEL) {
       // Gx = S[x+C] - S[x-C], Gy = D[x-C] + 2 D[x] + D[x+C], out = min(|Gx| + |Gy|, 255)
@@ -822,22 +781,9 @@ inline int env_nxcd() {
   return v;
 }
 
-// Separable stencils fetch the neighbour lanes' vertical sums by DPP (default)
-// or through an LDS row (STRIPE_SEP_DPP=0): DPP is 5 % faster on gray stripes
-// (8192x2048 sobel 0.0130 -> 0.0123 ms, gaussian5 0.0113 -> 0.0109) and neutral
-// to +1.7 % on RGB (profiles/r2d/sep_dpp_ab.txt).
-inline int env_hdpp() {
-  static const int v = [] {
-    const char* e = std::getenv("STRIPE_SEP_DPP");
-    return e ? std::atoi(e) : 1;
-  }();
-  return v;
-}
-
 inline void plan_bands(KArgs& a, dim3& grid, int tiles, int n0, int n1, int band, int R, int slots) {
   (void)slots;
   if (env_nxcd() >= 0) a.nxcd = env_nxcd();
-  a.hdpp = env_hdpp();
   if (band <= 0) band = R >= 3 ? 16 : 12;
   band = (int)align_up(band, 4);
   a.band = band;
@@ -845,6 +791,38 @@ inline void plan_bands(KArgs& a, dim3& grid, int tiles, int n0, int n1, int band
   a.nbands = a.nb0 + (int)div_up(n1, band);
   a.ntx = tiles;
   grid = dim3((unsigned)div_up((int64_t)tiles * a.nbands, kWaves));
+}
+
+// Occupancy cap of the HBM-streaming (nt-store) stencil launches: fewer
+// resident waves per SIMD keep fewer concurrent row streams open against HBM
+// (16384^2 RGB, band autotune on, profiles/r2d/nt_wgs_ab.txt: separable
+// gaussian5 0.311 -> 0.282 ms at 2 workgroups per CU, gaussian3 0.299 -> 0.269,
+// sobel 0.315 -> 0.293; direct emboss3 0.300 -> 0.283 at 3; the gray-prologue
+// direct kernels read 3 bytes per output byte and gain nothing).  The cap is an
+// LDS reservation (dynamic shared memory the kernel never touches) sized so
+// only `target` workgroups fit a CU's LDS; STRIPE_NT_WGS overrides (0 = no cap).
+inline size_t nt_lds_reserve(const void* fn, int target) {
+  static const int env = [] {
+    const char* e = std::getenv("STRIPE_NT_WGS");
+    return e ? std::atoi(e) : -1;
+  }();
+  if (env >= 0) target = env;
+  if (target <= 0) return 0;
+  static std::mutex mu;
+  static std::map<std::tuple<const void*, int, int>, size_t> cache;
+  int dev = 0;
+  HIP_CHECK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find({fn, dev, target});
+  if (it != cache.end()) return it->second;
+  int lds_cu = 0;
+  HIP_CHECK(hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev));
+  hipFuncAttributes fa{};
+  HIP_CHECK(hipFuncGetAttributes(&fa, fn));
+  const size_t total = (size_t)lds_cu / (size_t)(target + 1) + 1024;  // target fit, target + 1 do not
+  const size_t dyn = total > fa.sharedSizeBytes ? total - fa.sharedSizeBytes : 0;
+  cache[{fn, dev, target}] = dyn;
+  return dyn;
 }
 
 template <int C, class F, int PRO, bool EXP = false>
@@ -856,13 +834,13 @@ void launch_one(bool skip, bool nt, KArgs a, int tiles, int n0, int n1, int band
                       k_sep<C, F, PRO, true, 0, EXP>, k_sep<C, F, PRO, true, kNtAux, EXP>};
     const K fn = fns[2 * skip + nt];
     plan_bands(a, grid, tiles, n0, n1, band, F::R, resident_slots((const void*)fn));
-    fn<<<grid, kNT, 0, s>>>(a);
+    fn<<<grid, kNT, nt ? nt_lds_reserve((const void*)fn, kNtWgsSep) : 0, s>>>(a);
   } else {
     const K fns[4] = {k_direct<C, F, PRO, false, 0, EXP>, k_direct<C, F, PRO, false, kNtAux, EXP>,
                       k_direct<C, F, PRO, true, 0, EXP>, k_direct<C, F, PRO, true, kNtAux, EXP>};
     const K fn = fns[2 * skip + nt];
     plan_bands(a, grid, tiles, n0, n1, band, F::R, resident_slots((const void*)fn));
-    fn<<<grid, kNT, 0, s>>>(a);
+    fn<<<grid, kNT, nt ? nt_lds_reserve((const void*)fn, is_gray(PRO) ? 0 : kNtWgsDirect) : 0, s>>>(a);
   }
 }
 

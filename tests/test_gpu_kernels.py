@@ -172,40 +172,3 @@ def test_batched_frames(m, rng):
         for b in range(4):
             assert (got[b] == m._C.golden_apply(imgs[b], chain, "reflect101", True)).all(), (chain, b)
 
-
-_LDS_ROUTE_SCRIPT = r"""
-import sys
-import numpy as np
-import torch
-sys.path.insert(0, sys.argv[1])
-import mpi_cuda_imagemanipulation_amd as m
-rng = np.random.default_rng(7)
-bad = []
-for chain in ("gaussian3", "gaussian5", "gaussian7", "box5", "sobel", "sobel_l2", "gray:ref,contrast:3.5,gaussian5,expand"):
-    for shape in ((17, 15, 3), (37, 1365, 3), (9, 5000), (130, 4100)):
-        img = rng.integers(0, 256, size=shape, dtype=np.uint8)
-        if chain.startswith("gray") and img.ndim == 2:
-            continue
-        for border in ("reflect101", "constant"):
-            y = m.ops.apply(torch.from_numpy(img).cuda(), chain, border)
-            torch.cuda.synchronize()
-            if not (y.cpu().numpy() == m._C.golden_apply(img, chain, border, True)).all():
-                bad.append((chain, shape, border))
-print("BAD", bad)
-sys.exit(1 if bad else 0)
-"""
-
-
-def test_separable_lds_route(tmp_path):
-    # the separable stencils take their neighbour lanes' vertical sums by DPP by
-    # default; STRIPE_SEP_DPP=0 (read once per process) keeps the older LDS-row
-    # route, checked here in a child process
-    import os
-    import subprocess
-    import sys
-
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, STRIPE_SEP_DPP="0")
-    r = subprocess.run([sys.executable, "-c", _LDS_ROUTE_SCRIPT, root], env=env, capture_output=True, text=True,
-                       timeout=240)
-    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
