@@ -2,7 +2,7 @@
 # End-of-session validation (round 2, last session): GPU suite, smoke, headline
 # bench + rocprofv3 kernel trace, CLI runs through the pipelined / direct dist step.
 set -o pipefail
-O=gpurun_out/final_r2d
+O=gpurun_out/${FINAL_OUT:-final_r2d}
 mkdir -p $O
 T=${TMPDIR:-/tmp}
 export PYTHONUNBUFFERED=1
@@ -12,6 +12,8 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 tail -1 $O/smoke.log
 timeout -k 10 300 python bench.py --steps 100 --warmup 10 > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
 cat $O/bench.json
+STRIPE_NT_WGS=0 timeout -k 10 300 python bench.py --steps 100 --warmup 10 --dist-steps 0 --e2e-steps 0 > $O/bench_nocap.json 2>> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+cat $O/bench_nocap.json
 timeout -k 10 120 ./bin/stripe gen --synthetic 4099x2051x3 --seed 5 --output $T/in.ppm || exit 1
 for args in "--ranks 1" "--ranks 1 --dist-chunks 8" "--ranks 4" "--ranks 4 --dist-chunks 8"; do
   timeout -k 10 120 ./bin/stripe run --input $T/in.ppm --output $T/out.ppm --chain gaussian5 --backend local $args >> $O/cli.log 2>&1 || { tail -5 $O/cli.log; exit 1; }
