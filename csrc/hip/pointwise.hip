@@ -270,7 +270,22 @@ void launch_pointwise(const Pass& p, const PassConsts& pc, const PassLaunch& L, 
       const bool ntf = (int64_t)(n0_rows + n1_rows) * L.W * 2 * C > dev::kNtMinBytes &&
                        !(std::getenv("STRIPE_NT") && std::atoi(std::getenv("STRIPE_NT")) == 0);
       const dim3 gridf((unsigned)div_up(ngb, dev::kNT * dev::kFlatU), (unsigned)(y1 - y0));
-      if (ntf) dev::k_pointwise_flat<true><<<gridf, dev::kNT, 0, s>>>(a, ngb, gb0, C);
+      // streaming flat passes: at most 3 resident workgroups per CU (an LDS
+      // reservation the kernel never touches; fewer concurrent streams against
+      // HBM: 16K RGB invert 0.287 -> 0.269 ms, brightness 0.290 -> 0.268,
+      // profiles/r2d/pw_wgs_ab.txt); STRIPE_PW_WGS overrides (0 = no cap)
+      static const int pw_wgs = [] {
+        const char* e = std::getenv("STRIPE_PW_WGS");
+        return e ? std::atoi(e) : 3;
+      }();
+      size_t res = 0;
+      if (pw_wgs > 0 && ntf) {
+        int dev = 0, lds_cu = 0;
+        HIP_CHECK(hipGetDevice(&dev));
+        HIP_CHECK(hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev));
+        res = (size_t)lds_cu / (size_t)(pw_wgs + 1) + 1024 - 512;  // minus the kernel's 512-byte LUT
+      }
+      if (ntf) dev::k_pointwise_flat<true><<<gridf, dev::kNT, res, s>>>(a, ngb, gb0, C);
       else dev::k_pointwise_flat<false><<<gridf, dev::kNT, 0, s>>>(a, ngb, gb0, C);
     } else if (p.cin == 3 && p.cout == 1 && gray)
       go(dev::k_pointwise<3, 1, true, true>, dev::k_pointwise<3, 1, true, false>);
