@@ -258,9 +258,23 @@ void launch_pointwise(const Pass& p, const PassConsts& pc, const PassLaunch& L, 
     // invert 0.295 -> 0.322 ms with nt; 16K gray:ref 0.192 -> 0.184 ms)
     bool nt = p.cout == 1 && (int64_t)(n0_rows + n1_rows) * L.W * (p.cin + p.cout) > dev::kNtMinBytes;
     if (const char* e = std::getenv("STRIPE_NT")) nt = std::atoi(e) != 0;
+    // A/B knob, off: capping the resident workgroups of channel-changing passes
+    // (STRIPE_PWG_WGS, LDS reservation) only slows them - 16K gray:ref 0.187 ms
+    // uncapped, 0.212 at 4 per CU, 0.284 at 2 (profiles/r2d/pw_wgs_ab.txt)
+    static const int pwg_wgs = [] {
+      const char* e = std::getenv("STRIPE_PWG_WGS");
+      return e ? std::atoi(e) : 0;
+    }();
+    size_t resg = 0;
+    if (pwg_wgs > 0 && (int64_t)(n0_rows + n1_rows) * L.W * (p.cin + p.cout) > dev::kNtMinBytes) {
+      int dev = 0, lds_cu = 0;
+      HIP_CHECK(hipGetDevice(&dev));
+      HIP_CHECK(hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev));
+      resg = (size_t)lds_cu / (size_t)(pwg_wgs + 1) + 1024 - 512;
+    }
     auto go = [&](auto k_nt, auto k_t) {
-      if (nt) k_nt<<<grid, dev::kNT, 0, s>>>(a, ngroups, g0);
-      else k_t<<<grid, dev::kNT, 0, s>>>(a, ngroups, g0);
+      if (nt) k_nt<<<grid, dev::kNT, resg, s>>>(a, ngroups, g0);
+      else k_t<<<grid, dev::kNT, resg, s>>>(a, ngroups, g0);
     };
     if (p.cin == p.cout && !gray) {
       // byte-wise: flat 16-byte groups from the left margin to the right one
