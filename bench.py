@@ -13,11 +13,30 @@ With k = halo_depth > 1 (auto on > 1 rank) the exchange is communication-
 avoiding: k*2 rows travel once per k steps and each step also recomputes the
 shrinking band of neighbour rows the next step needs (more arithmetic, same
 bytes on the wire, bit-identical output); --halo-depth 1 exchanges every step.
-The frame stays resident in HBM ("resident" scope); the "dist" scope
-(root GPU -> scatter -> filter -> gather -> root GPU, the analogue of the
-reference's timed window kernel.cu:190-226) and a bit-exactness check against
-the C++ golden path are reported as extra fields.  Data: seeded synthetic
-random pixels (no dataset).
+
+Order of work (the timed region holds nothing but the K steps):
+  autotune (band height x occupancy cap, per pass and box; also ramps the
+  clock) -> W warmup steps -> K timed steps (barrier + device sync on both
+  sides, max over ranks) -> per-step device-event distribution -> golden
+  verification of the same engine -> copy roofline -> the other scopes.
+Round 2's driver number read 16 % slow because a host-side verification sat
+between the autotune and 5 warmup steps and the GPU clock dropped meanwhile
+(profiles/r3/headline_diag.txt).
+
+Scopes reported beside the headline ("resident": the frame stays in HBM):
+  resident_cold   the same steps rotating over enough stripe copies that the
+                  per-GPU working set exceeds the 256 MiB Infinity Cache
+                  (only when one stripe fits it: N=8 stripes do)
+  dist_*          root GPU frame -> scatter -> filter -> gather -> root GPU
+                  (the reference's window, kernel.cu:135-225, device-resident):
+                  sequential three calls, the pipelined run_dist (direct on
+                  one GPU), and on > 1 GPU the link-aware weighted split
+                  (plan_dist_split from a measured link probe)
+  ref_window      the reference's exact window end, kernel.cu:190-226:
+                  filter + D2H + gather into rank 0's host memory (every rank
+                  downloads its stripe into its slice of a shared host frame)
+  e2e             pinned host stripe -> H2D -> filter -> D2H -> pinned host
+Data: seeded synthetic random pixels (no dataset).
 
 Prints ONE JSON line on rank 0 (driver contract).
 """
@@ -25,7 +44,9 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
+import socket
 import sys
 import time
 
@@ -33,6 +54,7 @@ import numpy as np
 
 METRIC = "Mpixels/sec, 5x5 Gaussian blur on 16384x16384 RGB at 1/2/4/8 MI355X"
 BASELINE_MPX = None  # the reference publishes no number
+MALL_BYTES = 256 << 20  # MI355X Infinity Cache
 
 
 def parse():
@@ -49,13 +71,40 @@ def parse():
     ap.add_argument("--band", type=int, default=0)
     ap.add_argument("--halo-depth", type=int, default=0,
                     help="steps per halo exchange (0: auto, 1: exchange every step)")
-    ap.add_argument("--dist-steps", type=int, default=5, help="steps of the dist-scope measurement (0: skip)")
+    ap.add_argument("--dist-steps", type=int, default=5, help="steps of each dist-scope measurement (0: skip)")
+    ap.add_argument("--ref-steps", type=int, default=3, help="steps of the ref-window measurement (0: skip)")
     ap.add_argument("--e2e-steps", type=int, default=3, help="steps of the e2e-scope measurement (0: skip)")
+    ap.add_argument("--cold-steps", type=int, default=-1,
+                    help="steps of the cache-cold resident scope (-1: --steps; 0: skip)")
     ap.add_argument("--no-verify", action="store_true")
-    ap.add_argument("--no-autotune", action="store_true", help="skip the per-shape band-height autotune")
+    ap.add_argument("--no-autotune", action="store_true", help="skip the per-shape band / occupancy autotune")
     ap.add_argument("--backend", default="rccl", choices=["rccl", "host"],
                     help="rccl: GPU engine + RCCL (the benchmark); host: CPU golden engine + gloo (plumbing tests)")
     return ap.parse_args()
+
+
+def stats(ms):
+    v = sorted(ms)
+    if not v:
+        return None
+    return {"median": round(v[len(v) // 2], 5), "min": round(v[0], 5),
+            "p90": round(v[min(len(v) - 1, int(math.ceil(0.9 * len(v))) - 1)], 5),
+            "mean": round(sum(v) / len(v), 5), "n": len(v)}
+
+
+def build_info(root):
+    """What the in-tree native build was made from (the GPU box has no .git)."""
+    info = {}
+    try:
+        with open(os.path.join(root, "mpi_cuda_imagemanipulation_amd", "_build_info.json")) as f:
+            info = json.load(f)
+        sys.path.insert(0, os.path.join(root, "tools"))
+        import build as _b  # tools/build.py
+
+        info["source_matches_build"] = _b.source_hash() == info.get("source_hash")
+    except Exception as e:  # noqa: BLE001
+        info["error"] = str(e)
+    return info
 
 
 def main():
@@ -73,8 +122,10 @@ def main():
     from mpi_cuda_imagemanipulation_amd import parallel
     from mpi_cuda_imagemanipulation_amd._native import C
     from mpi_cuda_imagemanipulation_amd.models import Pipeline
+    from mpi_cuda_imagemanipulation_amd.utils.log import get_logger
 
     ctx = parallel.init("rccl" if a.backend == "rccl" else "gloo")
+    log = get_logger("bench", ctx.rank)
     dev = ctx.device
     tdev = "cuda" if dev else "cpu"
 
@@ -98,12 +149,57 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    dp = parallel.DistributedPipeline(ctx, pipe, W, H, Cc, root_buffers=a.dist_steps > 0,
-                                      autotune=not a.no_autotune)
-    row0, rows = dp.stripe
+    def all_ok(ok: bool) -> bool:
+        t = torch.tensor([1.0 if ok else 0.0], device=tdev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item() == 1.0)
+
+    def from_root(vals):
+        """rank 0's floats on every rank (so every rank plans the same split)"""
+        t = torch.tensor(vals, dtype=torch.float64, device=tdev)
+        if world > 1:
+            dist.broadcast(t, 0)
+        return [float(x) for x in t.tolist()]
 
     pinfo = C.plan_info(a.chain, Cc)
     iterable = pinfo["cin"] == pinfo["cout"]
+    R = max(1, pinfo["max_radius"])
+    # float conv passes (blur:K, conv:K) match the f64 golden within 1 LSB (ties)
+    tol = 1 if any(p["kind"] == 3 for p in pinfo["passes"]) else 0
+
+    def gold(band, n=1):
+        for _ in range(n):
+            band = C.golden_apply(band, a.chain, "reflect101", True)
+        return band
+
+    def same(x, y):
+        return x.shape == y.shape and bool((np.abs(x.astype(np.int16) - y.astype(np.int16)) <= tol).all())
+
+    def check_frame_rows(get_rows, cuts, n_it=1):
+        """golden check of an assembled frame region: frame edges and the rows
+        around every stripe boundary in `cuts` (get_rows(lo, hi) -> rows)"""
+        reach = n_it * R
+        crop = max(48, 4 * reach)
+        ok = True
+        for lo in (0, H - crop):
+            if lo < 0:
+                continue
+            ref = gold(C.synth_rows(a.seed, W, Cc, lo, crop), n_it)
+            sel = slice(0, crop - reach) if lo == 0 else slice(reach, crop)
+            ok &= same(get_rows(lo, lo + crop)[sel], ref[sel])
+        for c in cuts:
+            lo = c - 2 * reach
+            if 0 < c < H and lo >= 0 and c + 2 * reach <= H:
+                ref = gold(C.synth_rows(a.seed, W, Cc, lo, 4 * reach), n_it)
+                ok &= same(get_rows(lo, lo + 4 * reach)[reach:3 * reach], ref[reach:3 * reach])
+        return ok
+
+    dp = parallel.DistributedPipeline(ctx, pipe, W, H, Cc, autotune=not a.no_autotune)
+    if a.band > 0:
+        dp.engine.set_tuning([a.band] * len(dp.engine.bands), [-1] * len(dp.engine.bands))
+    row0, rows = dp.stripe
+    part, active = C.plan_rows(H, world, R)
 
     def run_steps(n):
         # iterable chains ping-pong in one call; a chain that changes the channel
@@ -115,50 +211,9 @@ def main():
                 dp.engine.rewind()
                 dp.run(1)
 
-    # ---- correctness (untimed): n_it iterated steps through the same schedule
-    # as the timed loop (deep halo included) vs the golden path on edge crops
-    # and on this stripe's upper seam ----
-    verify = None
-    if not a.no_verify:
-        n_it = max(2, dp.engine.halo_depth + 1) if iterable else 1
-        dp.load_synthetic(a.seed)
-        if iterable:
-            dp.run(n_it)
-        else:
-            dp.run(1)
-        out = dp.result_stripe()
-        ok = True
-        R = max(1, pinfo["max_radius"])
-        reach = n_it * R  # rows a band-edge border error travels in n_it steps
-        crop = max(48, 4 * reach)
-        # float conv passes (blur:K, conv:K) match the f64 golden within 1 LSB (ties)
-        tol = 1 if any(p["kind"] == 3 for p in pinfo["passes"]) else 0
-
-        def gold(band):
-            for _ in range(n_it):
-                band = C.golden_apply(band, a.chain, "reflect101", True)
-            return band
-
-        def same(x, y):
-            return bool((np.abs(x.astype(np.int16) - y.astype(np.int16)) <= tol).all())
-        edges = ([0] if row0 == 0 else []) + ([H - crop] if row0 + rows == H else [])
-        for lo in [e for e in edges if row0 <= e and e + crop <= row0 + rows]:  # crops inside this stripe
-            # golden on a band of full rows; rows far enough from the band edge are exact
-            ref = gold(C.synth_rows(a.seed, W, Cc, lo, crop))
-            sel = slice(0, crop - reach) if lo == 0 else slice(reach, crop)
-            got = out[lo - row0:lo - row0 + crop][sel]
-            ok &= same(got, ref[sel])
-        if rows >= reach and row0 >= 2 * reach and row0 + 2 * reach <= H:
-            # interior stripe seam: the first rows depend on the neighbour's halo
-            ref = gold(C.synth_rows(a.seed, W, Cc, row0 - 2 * reach, 4 * reach))
-            ok &= same(out[0:reach], ref[2 * reach:3 * reach])
-        okt = torch.tensor([1.0 if ok else 0.0], device=tdev)
-        if world > 1:
-            dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-        verify = bool(okt.item() == 1.0)
-
-    # ---- resident scope (headline) ----
+    # ---- resident scope (headline): tune -> warmup -> K timed steps ----
     dp.load_synthetic(a.seed)
+    dp.engine.tune()
     if a.warmup > 0:
         run_steps(a.warmup)
     sync()
@@ -173,59 +228,242 @@ def main():
     ms = max_over_ranks((t1 - t0) * 1e3)
     ms_per_step = ms / a.steps
     mpx = W * H / (ms_per_step * 1e-3) / 1e6
-    # device-event stage times of the last call on rank 0 (compute = the whole
-    # timed run(K) call, halo = its last exchange)
+    # device-event stage times of the timed call on rank 0 (compute = the whole
+    # run(K) call, halo = its last exchange)
     stages = {"resident": {k: round(v, 4) for k, v in dp.stage_times().items() if k in ("compute", "halo")}}
+    log.info("resident: %.5f ms/step over %d steps", ms_per_step, a.steps)
 
-    # ---- dist scope (root -> scatter -> filter -> gather -> root) ----
-    # sequential: scatter(), run(1), gather() (the reference's order, kernel.cu:135-225);
-    # pipelined (> 1 rank, single-pass chains): Engine::run_dist, stripes shipped with
-    # their halo rows in row chunks, chunk k filtered while later chunks arrive and
-    # gathered while they are filtered
-    dist_mpx = dist_seq_mpx = None
-    # (device ranks only: host comms run each grouped call synchronously, so on
-    # CPUs the extra calls cost time and nothing overlaps)
-    dist_chunks = dp.engine.dist_chunks(8) if dev else 0
+    # per-step device time distribution (events between calls; a call is one
+    # deep-halo block on > 1 rank, so its time is split over its steps)
+    per = max(1, dp.engine.halo_depth) if iterable else 1
+    step_ms = None
+    if dev and rows > 0:
+        calls = dp.engine.run_timed(max(per, a.steps), per, not iterable)
+        step_ms = stats([c / per for c in calls])
+
+    # ---- correctness of the timed engine (untimed, after the timed region):
+    # n_it iterated steps through the same schedule vs the golden path on edge
+    # crops and on this stripe's upper seam ----
+    verify = None
+    if not a.no_verify:
+        n_it = max(2, dp.engine.halo_depth + 1) if iterable else 1
+        dp.load_synthetic(a.seed)
+        dp.run(n_it)
+        out = dp.result_stripe()
+        ok = True
+        reach = n_it * R
+        crop = max(48, 4 * reach)
+        edges = ([0] if row0 == 0 else []) + ([H - crop] if row0 + rows == H else [])
+        for lo in [e for e in edges if row0 <= e and e + crop <= row0 + rows]:  # crops inside this stripe
+            # golden on a band of full rows; rows far enough from the band edge are exact
+            ref = gold(C.synth_rows(a.seed, W, Cc, lo, crop), n_it)
+            sel = slice(0, crop - reach) if lo == 0 else slice(reach, crop)
+            ok &= same(out[lo - row0:lo - row0 + crop][sel], ref[sel])
+        if rows >= reach and row0 >= 2 * reach and row0 + 2 * reach <= H:
+            # interior stripe seam: the first rows depend on the neighbour's halo
+            ref = gold(C.synth_rows(a.seed, W, Cc, row0 - 2 * reach, 4 * reach), n_it)
+            ok &= same(out[0:reach], ref[2 * reach:3 * reach])
+        verify = all_ok(ok)
+
+    # ---- same-box roofline: a device copy of the same bytes per step ----
+    bytes_in = rows * W * pinfo["cin"]
+    bytes_out = rows * W * pinfo["cout"]
+    step_bytes = bytes_in + bytes_out
+    copy_ms = None
+    if dev and rows > 0:
+        n = step_bytes // 2
+        src = torch.empty(n, dtype=torch.uint8, device="cuda").random_(0, 256)
+        dst = torch.empty_like(src)
+        for _ in range(3):
+            dst.copy_(src)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(21)]
+        ev[0].record()
+        for i in range(20):
+            dst.copy_(src)
+            ev[i + 1].record()
+        ev[-1].synchronize()
+        copy_ms = sorted(ev[i].elapsed_time(ev[i + 1]) for i in range(20))[10]
+        del src, dst
+        torch.cuda.empty_cache()
+    fits_mall = step_bytes <= MALL_BYTES
+    max_rows = max(r for _, r in part)
+    ws_max = max_rows * W * (pinfo["cin"] + pinfo["cout"])  # the same on every rank
+
+    # ---- resident scope, Infinity-Cache cold: rotate over enough stripe
+    # copies that each step's input was last touched > 256 MiB ago ----
+    scopes = {"resident": {"mpx_s": round(mpx, 1), "ms": round(ms_per_step, 5), "verified": verify}}
+    cold_steps = a.steps if a.cold_steps < 0 else a.cold_steps
+    nrot = int(math.ceil(2 * MALL_BYTES / max(1, ws_max))) + 1
+    if cold_steps > 0 and ws_max <= MALL_BYTES and iterable and nrot <= 8:
+        engines = [dp] + [parallel.DistributedPipeline(ctx, pipe, W, H, Cc) for _ in range(nrot - 1)]
+        for e in engines[1:]:
+            e.engine.set_tuning(dp.engine.bands, dp.engine.caps)
+        for e in engines:
+            e.load_synthetic(a.seed)
+        for i in range(2 * nrot):  # warm: every copy once
+            engines[i % nrot].run(1)
+        for e in engines:
+            e.synchronize()
+        sync()
+        barrier()
+        t0 = time.perf_counter()
+        for i in range(cold_steps):
+            engines[i % nrot].run(1)
+        for e in engines:
+            e.synchronize()
+        sync()
+        barrier()
+        cms = max_over_ranks((time.perf_counter() - t0) * 1e3) / cold_steps
+        scopes["resident_cold"] = {"mpx_s": round(W * H / (cms * 1e-3) / 1e6, 1), "ms": round(cms, 5),
+                                   "stripe_copies": nrot, "halo_every_step": True}
+        del engines
+    elif cold_steps > 0 and ws_max > MALL_BYTES:
+        scopes["resident_cold"] = {"same_as": "resident",
+                                   "note": f"per-GPU working set {ws_max} B exceeds the 256 MiB Infinity Cache"}
+
+    # ---- dist scopes (root frame -> scatter -> filter -> gather -> root) ----
+    dist_chunks = 0
     if a.dist_steps > 0:
+        dd = parallel.DistributedPipeline(ctx, pipe, W, H, Cc, root_buffers=True)
+        dd.engine.set_tuning(dp.engine.bands, dp.engine.caps)
         if rank == 0:
-            dp.engine.load_root_synthetic(a.seed)
-        dp.synchronize()
+            dd.engine.load_root_synthetic(a.seed)
+        dd.synchronize()
 
-        def seq_step():
-            dp.scatter()
-            dp.run(1)
-            dp.gather()
+        def verify_root(d, cuts):
+            if rank != 0:
+                return all_ok(True)
+            full = d.engine.store_root()
+            return all_ok(check_frame_rows(lambda lo, hi: full[lo:hi], cuts))
 
-        def time_dist(step):
+        def time_dist(d, step):
             for _ in range(2):
                 step()
-            dp.synchronize()
+            d.synchronize()
             sync()
             barrier()
             t0 = time.perf_counter()
             for _ in range(a.dist_steps):
                 step()
-            dp.synchronize()
+            d.synchronize()
             sync()
             barrier()
-            t1 = time.perf_counter()
-            dms = max_over_ranks((t1 - t0) * 1e3) / a.dist_steps
-            return W * H / (dms * 1e-3) / 1e6
+            dms = max_over_ranks((time.perf_counter() - t0) * 1e3) / a.dist_steps
+            return dms
 
-        dist_seq_mpx = time_dist(seq_step)
-        stages["dist"] = {k: round(v, 4) for k, v in dp.stage_times().items()
-                          if k in ("scatter", "compute", "halo", "gather")}
-        dist_mpx = dist_seq_mpx
-        if dist_chunks > 0 or (dev and dp.engine.dist_direct):
-            # (one GPU: the filter reads the root frame and writes the root output
-            # directly, the scatter and gather copies vanish)
-            dist_mpx = time_dist(lambda: dp.engine.run_dist(8))
-            keys = ("scatter", "compute", "gather") if dist_chunks > 0 else ("compute",)
-            stages["dist_pipelined" if dist_chunks > 0 else "dist_direct"] = {
-                k: round(v, 4) for k, v in dp.stage_times().items() if k in keys}
+        def seq_step():
+            dd.scatter()
+            dd.run(1)
+            dd.gather()
+
+        cuts = [r0 for r0, r in part[1:active]]
+        seq_step()
+        dd.synchronize()
+        ok = verify_root(dd, cuts) if not a.no_verify else None
+        dms = time_dist(dd, seq_step)
+        scopes["dist_sequential"] = {"mpx_s": round(W * H / (dms * 1e-3) / 1e6, 1), "ms": round(dms, 5),
+                                     "verified": ok}
+        stages["dist_sequential"] = {k: round(v, 4) for k, v in dd.stage_times().items()
+                                     if k in ("scatter", "compute", "halo", "gather")}
+        # (device ranks only: host comms run each grouped call synchronously)
+        dist_chunks = dd.engine.dist_chunks(8) if dev else 0
+        direct = dev and world == 1 and dd.engine.dist_direct
+        if dist_chunks > 0 or direct:
+            name = "dist_direct" if direct else "dist_pipelined"
+            dd.engine.run_dist(8)
+            dd.synchronize()
+            ok = verify_root(dd, cuts) if not a.no_verify else None
+            dms = time_dist(dd, lambda: dd.engine.run_dist(8))
+            scopes[name] = {"mpx_s": round(W * H / (dms * 1e-3) / 1e6, 1), "ms": round(dms, 5), "verified": ok,
+                            "chunks": dist_chunks, "rows": [r for _, r in part]}
+            stages[name] = {k: round(v, 4) for k, v in dd.stage_times().items()
+                            if k in ("scatter", "compute", "gather")}
+        del dd
+        # link-aware weighted split: the root keeps the share that balances its
+        # in-place filter against each peer link's transfer time
+        if world > 1 and dev and pinfo["passes"] and len(pinfo["passes"]) == 1:
+            link = C.probe_link_rate(ctx.comm, ctx.local_rank, 64 << 20, 3)  # bytes/ms per link, one way
+            rows_per_ms = rows / step_ms["median"] if step_ms else 1.0
+            hbm = step_bytes / copy_ms if copy_ms else 1.0
+            rows_per_ms, link, hbm = from_root([rows_per_ms, link, hbm])
+            plan = C.plan_dist_split(H, world, W * pinfo["cin"], W * pinfo["cout"], rows_per_ms, rows_per_ms,
+                                     link, hbm, 8, R)
+            dw = parallel.DistributedPipeline(ctx, pipe, W, H, Cc, root_buffers=True, row_weights=plan["weights"])
+            if dw.engine.dist_chunks(8) > 0:
+                dw.engine.set_tuning(dp.engine.bands, dp.engine.caps)
+                if rank == 0:
+                    dw.engine.load_root_synthetic(a.seed)
+                dw.engine.run_dist(8)
+                dw.synchronize()
+                wcuts = list(np.cumsum(plan["rows"])[:-1])
+                ok = verify_root(dw, [int(c) for c in wcuts]) if not a.no_verify else None
+                dms = time_dist(dw, lambda: dw.engine.run_dist(8))
+                scopes["dist_weighted"] = {
+                    "mpx_s": round(W * H / (dms * 1e-3) / 1e6, 1), "ms": round(dms, 5), "verified": ok,
+                    "rows": plan["rows"], "link_gb_s": round(link * 1e3 / 1e9, 2),
+                    "model": {k: round(plan[k], 5) for k in ("root_ms", "peer_ms", "floor_ms", "predicted_ms",
+                                                             "even_ms")}}
+                stages["dist_weighted"] = {k: round(v, 4) for k, v in dw.stage_times().items()
+                                           if k in ("scatter", "compute", "gather")}
+            del dw
+
+    # ---- reference window: filter + D2H + gather into rank 0's host memory
+    # (kernel.cu:190-226).  Every rank downloads its stripe, chunk by chunk as
+    # it is filtered, into its slice of one host frame shared with rank 0
+    # (POSIX shared memory, page-locked in every process: each GPU's own PCIe
+    # link carries its stripe, and no host copy follows). ----
+    if a.ref_steps > 0 and dev:
+        from multiprocessing import shared_memory
+
+        nbytes = H * W * pinfo["cout"]
+        shm = None
+        if world > 1:
+            names = [f"stripe_refwin_{os.getpid()}" if rank == 0 else None]
+            dist.broadcast_object_list(names, src=0)
+            if rank == 0:
+                shm = shared_memory.SharedMemory(name=names[0], create=True, size=nbytes)
+            barrier()
+            if rank != 0:
+                shm = shared_memory.SharedMemory(name=names[0])
+            frame = np.ndarray((nbytes,), dtype=np.uint8, buffer=shm.buf)
+        else:
+            frame_t = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)  # keeps the pages alive
+            frame = frame_t.numpy()
+        base = frame.ctypes.data
+        pinned = world == 1 or C.host_register(base, nbytes)
+        mine = base + row0 * W * pinfo["cout"]
+        dp.load_synthetic(a.seed)
+        dp.synchronize()
+        dp.engine.run_to_host_ptr(mine, 8)
+        dp.synchronize()
+        barrier()
+        ok = None
+        if not a.no_verify:
+            full = frame.reshape(H, W, -1) if pinfo["cout"] > 1 else frame.reshape(H, W)
+            ok = all_ok(rank != 0 or check_frame_rows(lambda lo, hi: full[lo:hi], [r0 for r0, _ in part[1:active]]))
+        dp.engine.run_to_host_ptr(mine, 8)
+        dp.synchronize()
+        sync()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(a.ref_steps):
+            dp.engine.run_to_host_ptr(mine, 8)
+            dp.synchronize()
+            barrier()  # rank 0's window ends when every stripe is in its memory
+        rms = max_over_ranks((time.perf_counter() - t0) * 1e3) / a.ref_steps
+        scopes["ref_window"] = {"mpx_s": round(W * H / (rms * 1e-3) / 1e6, 1), "ms": round(rms, 5), "verified": ok,
+                                "host_frame": "shared memory" if world > 1 else "pinned", "pinned": bool(pinned)}
+        stages["ref_window"] = {k: round(v, 4) for k, v in dp.stage_times().items() if k in ("compute", "d2h", "e2e")}
+        if world > 1:
+            if pinned:
+                C.host_unregister(base)
+            del frame
+            barrier()
+            shm.close()
+            if rank == 0:
+                shm.unlink()
 
     # ---- e2e scope (pinned host stripe -> H2D -> filter -> D2H -> pinned host) ----
-    e2e_mpx = None
     if a.e2e_steps > 0 and dev:
         eng = dp.engine
         eng.alloc_host_io()
@@ -239,13 +477,13 @@ def main():
             eng.run_e2e(8)
         eng.synchronize()
         barrier()
-        t1 = time.perf_counter()
-        ems = max_over_ranks((t1 - t0) * 1e3) / a.e2e_steps
-        e2e_mpx = W * H / (ems * 1e-3) / 1e6
+        ems = max_over_ranks((time.perf_counter() - t0) * 1e3) / a.e2e_steps
+        scopes["e2e"] = {"mpx_s": round(W * H / (ems * 1e-3) / 1e6, 1), "ms": round(ems, 5)}
         stages["e2e"] = {k: round(v, 4) for k, v in dp.stage_times().items()
                          if k in ("h2d", "compute", "halo", "d2h", "e2e")}
 
     if rank == 0:
+        med = step_ms["median"] if step_ms else None
         rec = {
             "metric": METRIC,
             "value": round(mpx, 1),
@@ -268,14 +506,24 @@ def main():
                 "parallelism": f"rowpart{world}+halo",
                 "scope": "resident: halo exchange + full-frame filter per step",
             },
-            "dist_scope_mpx_s": None if dist_mpx is None else round(dist_mpx, 1),
-            "dist_sequential_mpx_s": None if dist_seq_mpx is None else round(dist_seq_mpx, 1),
-            "dist_chunks": dist_chunks,
-            "e2e_scope_mpx_s": None if e2e_mpx is None else round(e2e_mpx, 1),
             "verified_vs_golden": verify,
-            "tuned_band_rows": dp.engine.bands,
+            # rank 0's per-step device time (HIP events between steps) and the
+            # same-box copy of the same per-GPU bytes (read + write)
+            "step_ms_device": step_ms,
+            "bytes_per_step_per_gpu": step_bytes,
+            "copy_roofline_ms": None if copy_ms is None else round(copy_ms, 5),
+            "frac_of_copy_roofline": None if not (copy_ms and med) else round(copy_ms / med, 4),
+            "hbm_tb_s": None if not med else round(step_bytes / (med * 1e-3) / 1e12, 3),
+            "working_set_fits_mall": fits_mall,
+            "scopes": scopes,
+            "tuned": {"band_rows": dp.engine.bands, "occupancy_caps": dp.engine.caps},
             "halo_depth": dp.engine.halo_depth,
+            "stripe_rows": [r for _, r in part],
             "stage_ms_rank0": stages,
+            "device": C.device_info(ctx.local_rank) if dev else {},
+            "build": build_info(root),
+            "host": socket.gethostname(),
+            "torch": torch.__version__,
         }
         os.write(json_fd, (json.dumps(rec) + "\n").encode())
     if world > 1:

@@ -6,6 +6,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <thread>
 #include <vector>
 
@@ -89,12 +90,29 @@ void parallel_rows(int y0, int y1, int64_t row_bytes, int threads, F&& f) {
     f(y0, y1);
     return;
   }
+  // a worker's exception (or a thread that fails to start) must surface in
+  // the caller as a C++ exception, not std::terminate: the first error is
+  // kept and rethrown after every started worker has joined
+  std::vector<std::exception_ptr> err((size_t)T);
+  auto guarded = [&f, &err](int t, int ya, int yb) {
+    try {
+      f(ya, yb);
+    } catch (...) {
+      err[(size_t)t] = std::current_exception();
+    }
+  };
   std::vector<std::thread> th;
   th.reserve((size_t)T - 1);
-  for (int t = 1; t < T; ++t)
-    th.emplace_back([&f, y0, n, t, T] { f(y0 + (int)((int64_t)n * t / T), y0 + (int)((int64_t)n * (t + 1) / T)); });
-  f(y0, y0 + (int)((int64_t)n / T));
+  try {
+    for (int t = 1; t < T; ++t)
+      th.emplace_back(guarded, t, y0 + (int)((int64_t)n * t / T), y0 + (int)((int64_t)n * (t + 1) / T));
+  } catch (...) {
+    err[0] = std::current_exception();  // thread creation failed: the started workers still join
+  }
+  if (!err[0]) guarded(0, y0, y0 + (int)((int64_t)n / T));
   for (auto& t : th) t.join();
+  for (auto& e : err)
+    if (e) std::rethrow_exception(e);
 }
 
 // Prologued local row y with R border pixels each side ((W + 2R) * cmid bytes),

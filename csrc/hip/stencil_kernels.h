@@ -825,8 +825,17 @@ inline size_t nt_lds_reserve(const void* fn, int target) {
   return dyn;
 }
 
+// Occupancy cap of one launch: wgs >= 0 is the engine's choice (its autotuner
+// times the caps per pass and box, since the best cap depends on the clock
+// and memory behaviour of the box: round-2 driver run);
+// wgs < 0 takes the family default, applied to HBM-streaming launches only.
+inline int stencil_cap(bool nt, int wgs, int family_default) {
+  if (wgs >= 0) return wgs;
+  return nt ? family_default : 0;
+}
+
 template <int C, class F, int PRO, bool EXP = false>
-void launch_one(bool skip, bool nt, KArgs a, int tiles, int n0, int n1, int band, hipStream_t s) {
+void launch_one(bool skip, bool nt, int wgs, KArgs a, int tiles, int n0, int n1, int band, hipStream_t s) {
   using K = void (*)(KArgs);
   dim3 grid;
   if constexpr (F::SEP) {
@@ -834,45 +843,46 @@ void launch_one(bool skip, bool nt, KArgs a, int tiles, int n0, int n1, int band
                       k_sep<C, F, PRO, true, 0, EXP>, k_sep<C, F, PRO, true, kNtAux, EXP>};
     const K fn = fns[2 * skip + nt];
     plan_bands(a, grid, tiles, n0, n1, band, F::R, resident_slots((const void*)fn));
-    fn<<<grid, kNT, nt ? nt_lds_reserve((const void*)fn, kNtWgsSep) : 0, s>>>(a);
+    fn<<<grid, kNT, nt_lds_reserve((const void*)fn, stencil_cap(nt, wgs, kNtWgsSep)), s>>>(a);
   } else {
     const K fns[4] = {k_direct<C, F, PRO, false, 0, EXP>, k_direct<C, F, PRO, false, kNtAux, EXP>,
                       k_direct<C, F, PRO, true, 0, EXP>, k_direct<C, F, PRO, true, kNtAux, EXP>};
     const K fn = fns[2 * skip + nt];
     plan_bands(a, grid, tiles, n0, n1, band, F::R, resident_slots((const void*)fn));
-    fn<<<grid, kNT, nt ? nt_lds_reserve((const void*)fn, is_gray(PRO) ? 0 : kNtWgsDirect) : 0, s>>>(a);
+    fn<<<grid, kNT, nt_lds_reserve((const void*)fn, stencil_cap(nt, wgs, is_gray(PRO) ? 0 : kNtWgsDirect)), s>>>(a);
   }
 }
 
 template <int PRO, class F>
-void launch_gray_out(bool expand, bool skip, bool nt, const KArgs& a, int tiles, int n0, int n1, int band,
+void launch_gray_out(bool expand, bool skip, bool nt, int wgs, const KArgs& a, int tiles, int n0, int n1, int band,
                      hipStream_t s) {
-  if (expand) launch_one<1, F, PRO, true>(skip, nt, a, tiles, n0, n1, band, s);
-  else launch_one<1, F, PRO, false>(skip, nt, a, tiles, n0, n1, band, s);
+  if (expand) launch_one<1, F, PRO, true>(skip, nt, wgs, a, tiles, n0, n1, band, s);
+  else launch_one<1, F, PRO, false>(skip, nt, wgs, a, tiles, n0, n1, band, s);
 }
 
 template <class F>
-void launch_filter(const Pass& p, const KArgs& a, int tiles, int n0, int n1, int band, bool nt, hipStream_t s) {
+void launch_filter(const Pass& p, const KArgs& a, int tiles, int n0, int n1, int band, bool nt, int wgs,
+                   hipStream_t s) {
   const bool gray = p.pro.gray;
   const bool lut = p.pro.has_post;
   const bool skip = p.border == Border::Skip;
   const bool ex = p.epi_expand;
   if (p.cmid == 3) {
     STRIPE_CHECK(!gray && !ex, "gray prologue / expand epilogue need a 1-channel stencil");
-    if (lut) launch_one<3, F, PRO_LUT>(skip, nt, a, tiles, n0, n1, band, s);
-    else launch_one<3, F, PRO_NONE>(skip, nt, a, tiles, n0, n1, band, s);
+    if (lut) launch_one<3, F, PRO_LUT>(skip, nt, wgs, a, tiles, n0, n1, band, s);
+    else launch_one<3, F, PRO_NONE>(skip, nt, wgs, a, tiles, n0, n1, band, s);
   } else {
-    if (gray && a.gmode == 1) launch_gray_out<PRO_GRAYLUT, F>(ex, skip, nt, a, tiles, n0, n1, band, s);
-    else if (gray) launch_gray_out<PRO_GRAY, F>(ex, skip, nt, a, tiles, n0, n1, band, s);
-    else if (lut) launch_gray_out<PRO_LUT, F>(ex, skip, nt, a, tiles, n0, n1, band, s);
-    else launch_gray_out<PRO_NONE, F>(ex, skip, nt, a, tiles, n0, n1, band, s);
+    if (gray && a.gmode == 1) launch_gray_out<PRO_GRAYLUT, F>(ex, skip, nt, wgs, a, tiles, n0, n1, band, s);
+    else if (gray) launch_gray_out<PRO_GRAY, F>(ex, skip, nt, wgs, a, tiles, n0, n1, band, s);
+    else if (lut) launch_gray_out<PRO_LUT, F>(ex, skip, nt, wgs, a, tiles, n0, n1, band, s);
+    else launch_gray_out<PRO_NONE, F>(ex, skip, nt, wgs, a, tiles, n0, n1, band, s);
   }
 }
 
 
 // Every filter F has launch_filter<F> compiled in exactly one stencil_inst_*.hip.
 #define STRIPE_LAUNCH_FILTER_SIG(F) \
-  void launch_filter<sdef::F>(const Pass&, const KArgs&, int, int, int, int, bool, hipStream_t)
+  void launch_filter<sdef::F>(const Pass&, const KArgs&, int, int, int, int, bool, int, hipStream_t)
 #define STRIPE_EXTERN_LAUNCH_FILTER(F) extern template STRIPE_LAUNCH_FILTER_SIG(F);
 #define STRIPE_INSTANTIATE_LAUNCH_FILTER(F) template STRIPE_LAUNCH_FILTER_SIG(F);
 #define STRIPE_STENCIL_FILTERS(X) \

@@ -50,6 +50,9 @@ struct EngineConfig {
                                 // k steps recompute a shrinking band of the neighbours' rows;
                                 // bit-exact).  0 = auto (STRIPE_HALO_DEPTH or a size rule),
                                 // 1 = exchange every iteration (overlap / pipelined schedules)
+  std::vector<double> row_weights;  // non-empty: weighted row split, one weight per rank
+                                // (plan_rows_weighted; the link-aware split of the
+                                // root-resident dist step, plan_dist_split)
   bool graphs = false;          // replay iterated chains from a captured hipGraph when a run()
                                 // involves no collective (single rank, or no halo exchange).
                                 // Off by default: measured on MI355X/ROCm 7, graph replay of
@@ -137,6 +140,11 @@ class Engine {
 
   // ---- compute ----
   void run(int iterations = 1);
+  // run(per) repeated until `iterations` steps ran, with a device event on the
+  // compute stream between the calls: per-call milliseconds (per-step device
+  // time distribution for the benchmark; rewind_each re-runs the same input,
+  // for chains that change the channel count)
+  std::vector<float> run_timed(int iterations, int per = 1, bool rewind_each = false);
   // Make the input of the last run() the current input again (benchmarks of
   // chains that change the channel count; the data may have been overwritten).
   void rewind();
@@ -144,8 +152,16 @@ class Engine {
   int graph_launches() const { return graph_launches_; }
   // Iterations per chain-level halo exchange (0: one exchange per pass and iteration).
   int halo_depth() const { return depth_; }
-  // Tuned band heights per pass (after autotune), for reporting.
+  // Tuned band heights and occupancy caps per pass (after autotune), for reporting.
   std::vector<int> bands() const;
+  std::vector<int> caps() const;
+  // Run the band / occupancy-cap autotune now (EngineConfig::autotune; otherwise
+  // the first run() does it): keeps the tuning out of a timed region.
+  void tune() {
+    if (cfg_.autotune && !tuned_) autotune_bands();
+  }
+  // Adopt another engine's tuning (same chain and stripe shape; skips autotune).
+  void set_tuning(const std::vector<int>& bands, const std::vector<int>& caps);
 
   // ---- output ----
   void store_packed(void* dst, bool dst_device);          // own output stripe, packed
@@ -162,6 +178,14 @@ class Engine {
   // scatter / gather copies; the stripe buffers then hold no output)
   bool dist_direct() const;
   void store_root(void* full, bool dst_device);           // rank 0: root output buffer, packed
+  // The reference's timed window ends in rank 0's host memory (kernel.cu:190-226:
+  // kernels, D2H, gray->BGR, MPI_Gather).  One step of it from the resident
+  // stripe: the chain (halo exchange included), its output rows downloaded in
+  // `chunks` row chunks as they are filtered, into `dst` (packed rows of this
+  // rank's stripe; pinned or registered host memory, e.g. this rank's slice of
+  // a frame shared with rank 0).  The input is left as it was (the step can
+  // be repeated on the same frame).
+  void run_to_host(void* dst, int chunks = 8);
 
   // ---- end-to-end (host -> device -> host) ----
   // Pinned host input/output stripes owned by the engine (packed rows).
@@ -188,6 +212,7 @@ class Engine {
     PassConsts pc;
     Buffer luts;
     int band = 0;  // tuned stencil band height (0: kernel default / cfg.band)
+    int wgs = -1;  // tuned occupancy cap (resident workgroups per CU; -1: family default)
   };
   void autotune_bands();
   bool tuned_ = false;
@@ -259,6 +284,13 @@ Image run_rank(const EngineConfig& cfg, Comm* comm, int device, const Image* inp
                PhaseTimes* times = nullptr);
 // Small host buffer broadcast over a communicator (metadata, <= 256 bytes).
 void broadcast_small(Comm* comm, void* host, size_t bytes, int root, int device);
+
+// Root <-> peer transfer rate of this communicator: rank 0 sends `bytes` to
+// every peer and receives `bytes` from every peer in one grouped call (the
+// traffic pattern of the pipelined dist step: every link busy both ways),
+// median of `reps` timed calls.  Returns bytes per millisecond per link (one
+// direction), the same value on every rank; 0 for a one-rank communicator.
+double probe_link_rate(Comm* comm, int device, size_t bytes, int reps = 3);
 
 // Convenience driver: run the whole distributed pipeline on `world` in-process
 // ranks (local device backend or host backend), root -> scatter -> run -> gather.

@@ -47,6 +47,8 @@ struct PassLaunch {
                                  // cover (deep-halo schedule; stencil passes only)
   const uint8_t* zero_row = nullptr;  // origin of an all-zero row (Constant y-border)
   int band = 0;                  // rows per workgroup (0 = auto)
+  int wgs = -1;                  // stencil occupancy cap, resident workgroups per CU
+                                 // (-1: the kernel family's default, 0: no cap)
   // Allocation view for buffer-descriptor kernels (branch-free OOB masking):
   // origin = base + org, zero row origin = in_base + in_zero; sizes < 2 GiB.
   const uint8_t* in_base = nullptr;

@@ -183,6 +183,29 @@ PYBIND11_MODULE(_C, m) {
     for (const auto& s : p.stripes) v.emplace_back(s.row0, s.rows);
     return py::make_tuple(v, p.active);
   }, py::arg("H"), py::arg("world"), py::arg("min_rows") = 1, py::arg("legacy") = false);
+  m.def("plan_rows_weighted", [](int H, const std::vector<double>& w, int min_rows) {
+    Partition p = plan_rows_weighted(H, w, min_rows);
+    std::vector<std::pair<int, int>> v;
+    for (const auto& s : p.stripes) v.emplace_back(s.row0, s.rows);
+    return py::make_tuple(v, p.active);
+  }, py::arg("H"), py::arg("weights"), py::arg("min_rows") = 1);
+  m.def("plan_dist_split", [](int H, int world, double row_in, double row_out, double root_rows_per_ms,
+                              double peer_rows_per_ms, double link_bytes_per_ms, double hbm_bytes_per_ms, int chunks,
+                              int min_rows) {
+    const DistSplit d = plan_dist_split(H, world, row_in, row_out, root_rows_per_ms, peer_rows_per_ms,
+                                        link_bytes_per_ms, hbm_bytes_per_ms, chunks, min_rows);
+    py::dict r;
+    r["weights"] = d.weights;
+    r["rows"] = d.rows;
+    r["root_ms"] = d.root_ms;
+    r["peer_ms"] = d.peer_ms;
+    r["floor_ms"] = d.floor_ms;
+    r["predicted_ms"] = d.predicted_ms;
+    r["even_ms"] = d.even_ms;
+    return r;
+  }, py::arg("H"), py::arg("world"), py::arg("row_in_bytes"), py::arg("row_out_bytes"), py::arg("root_rows_per_ms"),
+     py::arg("peer_rows_per_ms"), py::arg("link_bytes_per_ms"), py::arg("hbm_bytes_per_ms"), py::arg("chunks") = 8,
+     py::arg("min_rows") = 1);
 
   // ---- comm ----
   py::class_<PyComm>(m, "Comm")
@@ -198,6 +221,55 @@ PYBIND11_MODULE(_C, m) {
     return py::bytes(id.data(), id.size());
   });
   m.def("rccl_version", &rccl_version);
+  m.def("probe_link_rate", [](PyComm* c, int device, size_t bytes, int reps) {
+    if (!c) return 0.0;
+    py::gil_scoped_release nogil;
+    return probe_link_rate(c->comm.get(), device, bytes, reps);
+  }, py::arg("comm"), py::arg("device"), py::arg("bytes"), py::arg("reps") = 3);
+  // Page-lock an existing host range (e.g. a shared-memory frame every rank
+  // downloads its stripe into) so hipMemcpyAsync DMAs it without staging.
+  m.def("host_register", [](uintptr_t p, size_t bytes) {
+    const hipError_t e = hipHostRegister(reinterpret_cast<void*>(p), bytes, hipHostRegisterPortable);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    return true;
+  });
+  m.def("host_unregister", [](uintptr_t p) {
+    (void)hipHostUnregister(reinterpret_cast<void*>(p));
+    (void)hipGetLastError();
+  });
+  // Device / runtime identity for benchmark records (SURVEY §5 metrics): lets a
+  // box-to-box difference be told apart from a regression.  Empty dict when no
+  // HIP device is visible.
+  m.def("device_info", [](int dev) {
+    py::dict d;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= dev) {
+      (void)hipGetLastError();
+      return d;
+    }
+    hipDeviceProp_t pr{};
+    HIP_CHECK(hipGetDeviceProperties(&pr, dev));
+    int rt = 0, drv = 0;
+    (void)hipRuntimeGetVersion(&rt);
+    (void)hipDriverGetVersion(&drv);
+    d["name"] = std::string(pr.name);
+    d["gcn_arch"] = std::string(pr.gcnArchName);
+    d["cu_count"] = pr.multiProcessorCount;
+    d["sclk_max_mhz"] = pr.clockRate / 1000;
+    d["mclk_max_mhz"] = pr.memoryClockRate / 1000;
+    d["mem_bus_bits"] = pr.memoryBusWidth;
+    d["hbm_gib"] = (double)pr.totalGlobalMem / (double)(1ull << 30);
+    d["l2_bytes"] = pr.l2CacheSize;
+    d["lds_per_cu"] = (int64_t)pr.maxSharedMemoryPerMultiProcessor;
+    d["pci_bus_id"] = pr.pciBusID;
+    d["hip_runtime"] = rt;
+    d["hip_driver"] = drv;
+    d["rccl"] = rccl_version();
+    return d;
+  }, py::arg("device") = 0);
   m.def("make_rccl_comm", [](py::bytes uid, int rank, int world, int device) {
     std::string s(uid);
     STRIPE_CHECK(s.size() == 128, "unique id must be 128 bytes");
@@ -258,7 +330,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("graphs", &EngineConfig::graphs)
       .def_readwrite("pipeline", &EngineConfig::pipeline)
       .def_readwrite("halo_depth", &EngineConfig::halo_depth)
-      .def_readwrite("dist_chunks", &EngineConfig::dist_chunks);
+      .def_readwrite("dist_chunks", &EngineConfig::dist_chunks)
+      .def_readwrite("row_weights", &EngineConfig::row_weights);
 
   py::class_<PhaseTimes>(m, "PhaseTimes")
       .def_readonly("run", &PhaseTimes::run)
@@ -358,6 +431,11 @@ PYBIND11_MODULE(_C, m) {
         e.run_e2e(chunks);
       }, py::arg("chunks") = 8)
       .def_property_readonly("bands", &Engine::bands)
+      .def_property_readonly("caps", &Engine::caps)
+      .def("run_timed", [](Engine& e, int it, int per, bool rewind_each) {
+        py::gil_scoped_release rel;
+        return e.run_timed(it, per, rewind_each);
+      }, py::arg("iterations"), py::arg("per") = 1, py::arg("rewind_each") = false)
       .def("gather", [](Engine& e) {
         py::gil_scoped_release nogil;
         e.gather();
@@ -367,6 +445,15 @@ PYBIND11_MODULE(_C, m) {
         e.run_dist(chunks);
       }, py::arg("chunks") = 8)
       .def("dist_chunks", &Engine::dist_chunks, py::arg("chunks"))
+      .def("run_to_host_ptr", [](Engine& e, uintptr_t p, int chunks) {
+        py::gil_scoped_release nogil;
+        e.run_to_host(reinterpret_cast<void*>(p), chunks);
+      }, py::arg("ptr"), py::arg("chunks") = 8)
+      .def("set_tuning", &Engine::set_tuning)
+      .def("tune", [](Engine& e) {
+        py::gil_scoped_release nogil;
+        e.tune();
+      })
       .def_property_readonly("dist_direct", &Engine::dist_direct)
       .def("store_packed_ptr", [](Engine& e, uintptr_t p, bool dev) {
         py::gil_scoped_release nogil;

@@ -34,7 +34,8 @@ class RcclComm final : public Comm {
     HIP_CHECK(hipMalloc(&bar_buf_, sizeof(int)));
   }
   ~RcclComm() override {
-    if (comm_) ncclCommDestroy(comm_);  // an aborted communicator is already gone
+    if (comm_ && aborted_.load()) ncclCommAbort(comm_);  // flagged, never torn down by a call
+    else if (comm_) ncclCommDestroy(comm_);            // (a torn-down communicator is already gone)
     if (bar_buf_) (void)hipFree(bar_buf_);
     if (bar_stream_) (void)hipStreamDestroy(bar_stream_);
     (void)hipGetLastError();
@@ -43,37 +44,49 @@ class RcclComm final : public Comm {
   int size() const override { return world_; }
   const char* backend() const override { return "rccl"; }
   bool device_buffers() const override { return true; }
-  void group_start() override { NCCL_CHECK(ncclGroupStart()); }
-  // enqueue calls hold the lock, so a concurrent abort() never frees the
-  // communicator under them (group_end may block on peers: it does not)
+  // Every RCCL call on this communicator (enqueue, group end, error query,
+  // abort) runs on the thread that drives this rank: abort() only raises the
+  // flag, and the driving thread tears the communicator down at its next call
+  // or inside wait().  So ncclCommAbort can never free the communicator under
+  // a send/recv that is between group_start and group_end, or under a
+  // group_end blocked on a peer (run_group aborts every rank from the thread
+  // of the rank that failed).
+  void group_start() override {
+    enter();
+    NCCL_CHECK(ncclGroupStart());
+    in_group_ = true;
+  }
   void send(const void* buf, size_t bytes, int peer, hipStream_t s) override {
-    std::lock_guard<std::mutex> lk(mu_);
-    NCCL_CHECK(ncclSend(buf, bytes, ncclUint8, peer, live_locked(), s));
+    enter();
+    NCCL_CHECK(ncclSend(buf, bytes, ncclUint8, peer, comm_, s));
   }
   void recv(void* buf, size_t bytes, int peer, hipStream_t s) override {
-    std::lock_guard<std::mutex> lk(mu_);
-    NCCL_CHECK(ncclRecv(buf, bytes, ncclUint8, peer, live_locked(), s));
+    enter();
+    NCCL_CHECK(ncclRecv(buf, bytes, ncclUint8, peer, comm_, s));
   }
-  void group_end() override { NCCL_CHECK(ncclGroupEnd()); }
+  void group_end() override {
+    // an abort raised between group_start and here still closes the group
+    // (the RCCL group state is per thread), then takes effect
+    in_group_ = false;
+    const ncclResult_t r = ncclGroupEnd();
+    enter();
+    if (r != ncclSuccess) NCCL_CHECK(r);
+  }
   void barrier() override {
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      NCCL_CHECK(ncclAllReduce(bar_buf_, bar_buf_, 1, ncclInt32, ncclSum, live_locked(), bar_stream_));
-    }
+    enter();
+    NCCL_CHECK(ncclAllReduce(bar_buf_, bar_buf_, 1, ncclInt32, ncclSum, comm_, bar_stream_));
     wait(bar_stream_);
   }
-  // Collective abort (Q9), callable from any thread: ncclCommAbort stops this
-  // rank's queued RCCL kernels and proxy, and a wait() blocked in another
-  // thread (run_group aborts every rank of an in-process group when one
-  // fails) sees the flag and raises at once instead of running into
-  // STRIPE_COMM_TIMEOUT_S.  A second abort is a no-op.
+  // Collective abort (Q9), callable from any thread: run_group aborts every
+  // rank of an in-process group when one fails.  The flag makes this rank's
+  // next call (or its wait(), which polls it) abort the communicator on the
+  // driving thread and raise, instead of running into STRIPE_COMM_TIMEOUT_S.
+  // A second abort is a no-op.
   void abort(const std::string& why) override {
     std::lock_guard<std::mutex> lk(mu_);
     if (aborted_.load()) return;
     why_ = why;
     aborted_.store(true);
-    if (comm_) ncclCommAbort(comm_);
-    comm_ = nullptr;
   }
 
   // Bounded wait: poll the stream and the communicator's asynchronous error
@@ -84,51 +97,47 @@ class RcclComm final : public Comm {
     const auto t0 = std::chrono::steady_clock::now();
     const double limit = comm_timeout_s();
     for (int it = 0;; ++it) {
-      check_aborted();
+      enter();
       const hipError_t e = hipStreamQuery(s);
       if (e == hipSuccess) {
-        check_aborted();  // kernels stopped by an abort also complete the stream
+        enter();  // kernels stopped by an abort also complete the stream
         return;
       }
       if (e != hipErrorNotReady) HIP_CHECK(e);
       (void)hipGetLastError();  // NotReady is not an error; keep the sticky state clean
-      {
-        std::lock_guard<std::mutex> lk(mu_);
-        ncclResult_t ar = ncclSuccess;
-        if (comm_) ncclCommGetAsyncError(comm_, &ar);
-        if (ar != ncclSuccess && ar != ncclInProgress) {
-          why_ = std::string("RCCL asynchronous error on rank ") + std::to_string(rank_) + ": " +
-                 ncclGetErrorString(ar);
-          aborted_.store(true);
-          ncclCommAbort(comm_);
-          comm_ = nullptr;
-        }
-      }
+      ncclResult_t ar = ncclSuccess;
+      if (comm_) ncclCommGetAsyncError(comm_, &ar);
+      if (ar != ncclSuccess && ar != ncclInProgress)
+        abort(std::string("RCCL asynchronous error on rank ") + std::to_string(rank_) + ": " + ncclGetErrorString(ar));
       const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-      if (el > limit) {
+      if (el > limit)
         abort("rank " + std::to_string(rank_) + ": collective did not complete within " + std::to_string(limit) +
               " s (STRIPE_COMM_TIMEOUT_S)");
-        check_aborted();
-      }
       if (it > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
   }
 
  private:
-  ncclComm_t live_locked() {  // caller holds mu_
-    if (aborted_.load()) fail("RCCL communicator of rank " + std::to_string(rank_) + " was aborted: " + why_);
-    return comm_;
+  // driving thread: abort the communicator once (outside any open group)
+  void teardown() {
+    if (in_group_) return;  // group_end() closes the group first, then calls enter()
+    if (comm_) ncclCommAbort(comm_);
+    comm_ = nullptr;
   }
-  void check_aborted() {
+  // entry of every call on the driving thread: a raised abort flag tears the
+  // communicator down and raises
+  void enter() {
     if (!aborted_.load()) return;
+    teardown();
     std::lock_guard<std::mutex> lk(mu_);
-    live_locked();
+    fail("RCCL communicator of rank " + std::to_string(rank_) + " was aborted: " + why_);
   }
 
   ncclComm_t comm_ = nullptr;
   int rank_, world_, dev_;
-  std::mutex mu_;                    // guards comm_ / why_ against a concurrent abort()
+  std::mutex mu_;                    // guards why_ against a concurrent abort()
   std::atomic<bool> aborted_{false};
+  bool in_group_ = false;            // driving thread only
   std::string why_;
   hipStream_t bar_stream_ = nullptr;
   int* bar_buf_ = nullptr;

@@ -98,7 +98,14 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
                  "comm backend '" << comm_->backend() << "' does not match the engine backend");
   }
   plan_ = compile_chain(parse_chain(cfg_.chain), cfg_.C, cfg_.border, cfg_.fuse);
-  part_ = plan_rows(cfg_.H, world_, std::max(1, plan_.max_radius), cfg_.legacy_partition);
+  if (cfg_.row_weights.empty()) {
+    part_ = plan_rows(cfg_.H, world_, std::max(1, plan_.max_radius), cfg_.legacy_partition);
+  } else {
+    STRIPE_CHECK((int)cfg_.row_weights.size() == world_,
+                 "row_weights has " << cfg_.row_weights.size() << " entries for " << world_ << " ranks");
+    STRIPE_CHECK(!cfg_.legacy_partition, "row_weights and the legacy split are exclusive");
+    part_ = plan_rows_weighted(cfg_.H, cfg_.row_weights, std::max(1, plan_.max_radius));
+  }
   halo_ = plan_.max_radius;
   depth_ = choose_depth();
   if (depth_ >= 1) halo_ = std::max(halo_, depth_ * chain_reach());
@@ -437,6 +444,7 @@ PassLaunch Engine::make_launch(const Pass& p, const uint8_t* in, uint8_t* out, i
   L.Hg = g.Hg;
   L.zero_row = zero_.data() + kMarginBytes;
   L.band = prt_[pi].band > 0 ? prt_[pi].band : cfg_.band;
+  L.wgs = prt_[pi].wgs;
   const Buffer* bi = nullptr;
   const Buffer* bo = nullptr;
   // the ping-pong pair, or the root's full-frame buffers (one-rank run_dist)
@@ -728,8 +736,27 @@ std::vector<int> Engine::bands() const {
   return b;
 }
 
-// Time each candidate band height on this rank's stripe (kernels only, no halo
-// exchange; outputs land in the scratch ping-pong buffer) and keep the fastest.
+std::vector<int> Engine::caps() const {
+  std::vector<int> b;
+  for (const auto& p : prt_) b.push_back(p.wgs);
+  return b;
+}
+
+void Engine::set_tuning(const std::vector<int>& bands, const std::vector<int>& caps) {
+  STRIPE_CHECK(bands.size() == prt_.size() && caps.size() == prt_.size(), "tuning needs one entry per pass");
+  for (size_t i = 0; i < prt_.size(); ++i) {
+    prt_[i].band = bands[i];
+    prt_[i].wgs = caps[i];
+  }
+  tuned_ = true;
+}
+
+// Time each candidate band height, then each occupancy cap at the best band,
+// on this rank's stripe (kernels only, no halo exchange; outputs land in the
+// scratch ping-pong buffer) and keep the fastest.  The cap is tuned per box:
+// the HBM-streaming cap that made a warm 16K RGB gaussian5 pass 9 % faster
+// (0.311 -> 0.282 ms) reads no better than no cap on a cold clock
+// (profiles/r3/headline_diag.txt), so it is measured here rather than fixed.
 void Engine::autotune_bands() {
   tuned_ = true;
   if (!device() || cfg_.band > 0 || stripe().rows == 0) return;
@@ -737,24 +764,26 @@ void Engine::autotune_bands() {
   // waves to hide each wave's row-step latency (8192x2048 gray sobel, one
   // rank's share of config 3 at N=4: 0.0125 ms at 4 rows vs 0.0150 at 12)
   const int cand[] = {4, 8, 12, 16, 24, 32};
+  // -1: the family default (separable 2 / direct 3 workgroups per CU on
+  // HBM-streaming passes, none on cache-resident ones), 0: no cap
+  const int caps[] = {-1, 0, 2, 3, 4};
+  const bool fixed_cap = std::getenv("STRIPE_NT_WGS") != nullptr;  // A/B runs pin the cap
   hipEvent_t e0 = ev_[6], e1 = ev_[7];
   for (size_t i = 0; i < plan_.passes.size(); ++i) {
     const Pass& p = plan_.passes[i];
     if (p.kind != PassKind::Separable && p.kind != PassKind::Direct) continue;
-    float best = 1e30f;
-    int best_band = 0;
-    for (int b : cand) {
-      prt_[i].band = b;
-      // median over 5 timed bursts (after one warmup burst) of kBurst
-      // back-to-back launches: the steady state of an iterated run, where one
-      // launch's tail overlaps the next one's ramp (isolated launches favour
-      // taller bands by ~5 % on 20-90 us kernels); bursts of a 40-300 us kernel
-      // still jitter by a few percent, about the gap between bands
-      constexpr int kBurst = 4;
-      PassLaunch L = make_launch(p, origin(buf_[cur_], p.cin), origin(buf_[cur_ ^ 1], p.cout), (int)i);
-      L.band = b;
-      L.ry[0] = 0;
-      L.ry[1] = L.rows;
+    PassLaunch L = make_launch(p, origin(buf_[cur_], p.cin), origin(buf_[cur_ ^ 1], p.cout), (int)i);
+    L.ry[0] = 0;
+    L.ry[1] = L.rows;
+    // median over 5 timed bursts (after one warmup burst) of kBurst
+    // back-to-back launches: the steady state of an iterated run, where one
+    // launch's tail overlaps the next one's ramp (isolated launches favour
+    // taller bands by ~5 % on 20-90 us kernels); bursts of a 40-300 us kernel
+    // still jitter by a few percent, about the gap between bands
+    constexpr int kBurst = 4;
+    auto time_it = [&](int band, int wgs) {
+      L.band = band;
+      L.wgs = wgs;
       std::vector<float> t;
       for (int rep = 0; rep < 6; ++rep) {
         HIP_CHECK(hipEventRecord(e0, s_compute_));
@@ -764,13 +793,40 @@ void Engine::autotune_bands() {
         if (rep > 0) t.push_back(elapsed(e0, e1) / kBurst);
       }
       std::nth_element(t.begin(), t.begin() + t.size() / 2, t.end());
-      const float med = t[t.size() / 2];
-      if (med < best) {
-        best = med;
+      return t[t.size() / 2];
+    };
+    // clock ramp: the first candidate must not be timed on an idle-clocked GPU
+    {
+      L.band = 0;
+      L.wgs = -1;
+      const auto t0 = std::chrono::steady_clock::now();
+      for (int k = 0; k < 200; ++k) {
+        for (int j = 0; j < 4; ++j) launch_pass(p, prt_[i].pc, L, s_compute_);
+        HIP_CHECK(hipStreamSynchronize(s_compute_));
+        if (std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() > 30.0) break;
+      }
+    }
+    float best = 1e30f;
+    int best_band = 0, best_wgs = -1;
+    for (int b : cand) {
+      const float t = time_it(b, -1);
+      if (t < best) {
+        best = t;
         best_band = b;
       }
     }
+    if (!fixed_cap) {
+      for (int c : caps) {
+        if (c < 0) continue;  // the default was timed in the band sweep
+        const float t = time_it(best_band, c);
+        if (t < best * 0.995f) {  // a cap must beat the default by more than the noise floor
+          best = t;
+          best_wgs = c;
+        }
+      }
+    }
     prt_[i].band = best_band;
+    prt_[i].wgs = best_wgs;
   }
 }
 
@@ -842,6 +898,38 @@ void Engine::run(int iterations) {
   time_halo_ = true;
   out_buf_ = cur_;
   out_c_ = plan_.cout;
+}
+
+std::vector<float> Engine::run_timed(int iterations, int per, bool rewind_each) {
+  STRIPE_CHECK(iterations >= 1 && per >= 1, "run_timed needs iterations, per >= 1");
+  const int calls = (iterations + per - 1) / per;
+  std::vector<float> ms;
+  if (!device()) {  // host backend: run() is synchronous, the host clock is exact
+    for (int k = 0; k < calls; ++k) {
+      const double t0 = host_ms();
+      if (rewind_each && k > 0) rewind();
+      run(std::min(per, iterations - k * per));
+      ms.push_back((float)(host_ms() - t0));
+    }
+    return ms;
+  }
+  std::vector<hipEvent_t> ev((size_t)calls + 1);
+  for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
+  try {
+    HIP_CHECK(hipEventRecord(ev[0], s_compute_));
+    for (int k = 0; k < calls; ++k) {
+      if (rewind_each && k > 0) rewind();
+      run(std::min(per, iterations - k * per));
+      HIP_CHECK(hipEventRecord(ev[(size_t)k + 1], s_compute_));
+    }
+    synchronize();
+    for (int k = 0; k < calls; ++k) ms.push_back(elapsed(ev[(size_t)k], ev[(size_t)k + 1]));
+  } catch (...) {
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    throw;
+  }
+  for (auto& e : ev) (void)hipEventDestroy(e);
+  return ms;
 }
 
 void Engine::rewind() {
@@ -1088,17 +1176,22 @@ void Engine::gather() {
 // Pipelined distributed step (the reference's timed window, kernel.cu:135-225:
 // Scatter, the chain, Gather, there strictly one after the other).
 //
-// The root holds the whole frame, so it ships every stripe together with its
-// halo rows (no neighbour exchange) in n row chunks.  Rank r's chunk k is
-// filtered once chunk k + 1 (the R rows below it) has landed, and its output
-// travels back in the grouped call that ships chunk k + 2, so each peer's
-// xGMI link carries scatter and gather traffic in opposite directions at once
-// and the compute hides under the transfers:
-//   comm stream    T0 | T1 | T2+G0 | T3+G1 | ... | T(n-1)+G(n-3) | G(n-2)+G(n-1)
-//   compute stream      C0 (after T1) | C1 (after T2) | ... | C(n-1) (after T(n-1))
-// Every active rank derives the same n from the partition, so the grouped
-// calls match across ranks.  Only single-pass stencil / pointwise chains (the
-// pass reads exactly rows y - R .. y + R); anything else runs the three calls.
+// The root holds the whole frame, so it ships every peer's stripe together
+// with its halo rows (no neighbour exchange) in n row chunks, and filters its
+// own share in place: one launch from the root input straight into the root
+// output (no copies), beside the transfers.  Peer r's chunk k is filtered
+// once chunk k + 1 (the R rows below it) has landed, and its output travels
+// back in the grouped call that ships chunk k + 2, so each peer's xGMI link
+// carries scatter and gather traffic in opposite directions at once and the
+// peers' compute hides under the transfers:
+//   root comm      T0 | T1 | T2+G0 | T3+G1 | ... | T(n-1)+G(n-3) | G(n-2)+G(n-1)
+//   root compute   its whole share (no dependency on the transfers)
+//   peer compute        C0 (after T1) | C1 (after T2) | ... | C(n-1) (after T(n-1))
+// With row_weights from plan_dist_split the root keeps the share that
+// balances its filter time against the per-link transfer time.  Every active
+// rank derives the same n from the partition, so the grouped calls match.
+// Only single-pass stencil / pointwise chains (the pass reads exactly rows
+// y - R .. y + R); anything else runs the three calls.
 // ---------------------------------------------------------------------------
 int Engine::dist_chunks(int chunks) const {
   if (!comm_ || part_.active <= 1 || chunks < 2 || plan_.passes.size() != 1) return 0;
@@ -1106,7 +1199,7 @@ int Engine::dist_chunks(int chunks) const {
   if (p.kind != PassKind::Separable && p.kind != PassKind::Direct && p.kind != PassKind::Pointwise) return 0;
   if (cfg_.halo && p.R > halo_) return 0;
   int minrows = std::numeric_limits<int>::max();
-  for (int r = 0; r < part_.active; ++r) minrows = std::min(minrows, part_.of(r).rows);
+  for (int r = 1; r < part_.active; ++r) minrows = std::min(minrows, part_.of(r).rows);  // peers' chunks
   const int n = std::min(chunks, minrows / std::max(1, p.R));  // every chunk holds >= R rows
   return n >= 2 ? n : 0;
 }
@@ -1152,31 +1245,27 @@ void Engine::run_dist(int chunks) {
   const Pass& p = plan_.passes[0];
   const int R = p.R, cin = plan_.cin, cout = plan_.cout;
   const int64_t Pin = pitch(cin), Pout = pitch(cout);
-  STRIPE_CHECK(rank_ != 0 || (root_in_.data() && root_out_.data()),
-               "root buffers not allocated (EngineConfig::root_buffers)");
+  const bool root = rank_ == 0;
+  STRIPE_CHECK(!root || (root_in_.data() && root_out_.data()), "root buffers not allocated (EngineConfig::root_buffers)");
   TraceRange tr("stripe.dist");
   fault_point("scatter", rank_);
-  // row range [lo, hi) of rank r's transfer k (halo rows ride on the first and last chunk)
+  // row range [lo, hi) of peer r's transfer k (halo rows ride on the first and last chunk)
   auto cut = [&](int r, int k) { return (int)((int64_t)part_.of(r).rows * k / n); };
   auto span = [&](int r, int k, int& lo, int& hi) {
     const bool h = cfg_.halo && R > 0;
     lo = cut(r, k) - (k == 0 && h && r > 0 ? R : 0);
     hi = cut(r, k + 1) + (k == n - 1 && h && r + 1 < part_.active ? R : 0);
   };
-  const uint8_t* rin = rank_ == 0 ? root_origin(root_in_, cin) - kMarginBytes : nullptr;
-  uint8_t* rout = rank_ == 0 ? root_origin(root_out_, cout) - kMarginBytes : nullptr;
+  const uint8_t* rin = root ? root_origin(root_in_, cin) - kMarginBytes : nullptr;
+  uint8_t* rout = root ? root_origin(root_out_, cout) - kMarginBytes : nullptr;
   uint8_t* in_org = origin(buf_[0], cin);
   uint8_t* out_org = origin(buf_[1], cout);
   const bool dev = device();
-  auto local_copy = [&](void* dst, const void* src, size_t bytes) {
-    if (dev) HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s_comm_));
-    else std::memcpy(dst, src, bytes);
-  };
-  // one grouped call: scatter chunk k (k < n) and gather chunk j (j >= 0)
+  // one grouped call: scatter chunk k (k < n) and gather chunks j, j2 (>= 0)
   auto transfer = [&](int k, int j, int j2) {
     const bool sc = k >= 0 && k < n;
-    if (rank_ == 0) {
-      comm_->group_start();
+    comm_->group_start();
+    if (root) {
       for (int r = 1; r < part_.active; ++r) {
         const Stripe& sr = part_.of(r);
         int lo, hi;
@@ -1189,19 +1278,7 @@ void Engine::run_dist(int chunks) {
             comm_->recv(rout + (int64_t)(sr.row0 + cut(r, g)) * Pout, (size_t)((cut(r, g + 1) - cut(r, g)) * Pout), r,
                         s_comm_);
       }
-      comm_->group_end();
-      int lo, hi;
-      if (sc) {
-        span(0, k, lo, hi);
-        local_copy(in_org - kMarginBytes + (int64_t)lo * Pin, rin + (int64_t)(st.row0 + lo) * Pin,
-                   (size_t)((hi - lo) * Pin));
-      }
-      for (int g : {j, j2})
-        if (g >= 0)
-          local_copy(rout + (int64_t)(st.row0 + cut(0, g)) * Pout, out_org - kMarginBytes + (int64_t)cut(0, g) * Pout,
-                     (size_t)((cut(0, g + 1) - cut(0, g)) * Pout));
     } else {
-      comm_->group_start();
       int lo, hi;
       if (sc) {
         span(rank_, k, lo, hi);
@@ -1211,7 +1288,22 @@ void Engine::run_dist(int chunks) {
         if (g >= 0)
           comm_->send(out_org - kMarginBytes + (int64_t)cut(rank_, g) * Pout,
                       (size_t)((cut(rank_, g + 1) - cut(rank_, g)) * Pout), 0, s_comm_);
-      comm_->group_end();
+    }
+    comm_->group_end();
+  };
+  // the root's own share: root input -> root output in place (its local rows
+  // are the frame's rows 0 .. rows - 1, so the root buffers are its stripe)
+  auto compute_root = [&]() {
+    const uint8_t* ri = root_origin(root_in_, cin);
+    uint8_t* ro = root_origin(root_out_, cout);
+    if (dev) {
+      PassLaunch L = make_launch(p, ri, ro, 0);
+      L.nrange = 1;
+      L.ry[0] = 0;
+      L.ry[1] = st.rows;
+      launch_pass(p, prt_[0].pc, L, s_compute_);
+    } else {
+      cpu_pass(p, ConstView{ri, Pin}, MutView{ro, Pout}, cfg_.W, geom(), 0, st.rows, host_threads());
     }
   };
   auto compute = [&](int k) {
@@ -1242,21 +1334,31 @@ void Engine::run_dist(int chunks) {
   stage_begin(Stage::Scatter, s_comm_);
   transfer(0, -1, -1);
   record(dev ? evT[0] : nullptr, s_comm_);
+  if (root) {  // beside the transfers: nothing it reads or writes is in flight
+    stage_begin(Stage::Compute, s_compute_);
+    compute_root();
+    stage_end(Stage::Compute, s_compute_);
+  }
   for (int k = 0; k < n; ++k) {
     if (k + 1 < n) {
-      if (dev && k >= 1) HIP_CHECK(hipStreamWaitEvent(s_comm_, evC[k - 1], 0));
+      // a peer's gather of chunk k - 1 waits for its filter (the root's
+      // received rows are written by the transfer itself)
+      if (dev && !root && k >= 1) HIP_CHECK(hipStreamWaitEvent(s_comm_, evC[k - 1], 0));
       if (k == 1) stage_begin(Stage::Gather, s_comm_);
       transfer(k + 1, k - 1, -1);
       record(dev ? evT[k + 1] : nullptr, s_comm_);
     }
     if (k + 1 == n - 1) stage_end(Stage::Scatter, s_comm_);  // the last chunk is on its way
+    if (root) continue;
     if (dev) HIP_CHECK(hipStreamWaitEvent(s_compute_, evT[std::min(k + 1, n - 1)], 0));
     if (k == 0) stage_begin(Stage::Compute, s_compute_);
     compute(k);
     record(dev ? evC[k] : nullptr, s_compute_);
   }
-  stage_end(Stage::Compute, s_compute_);
-  if (dev) HIP_CHECK(hipStreamWaitEvent(s_comm_, evC[n - 1], 0));
+  if (!root) {
+    stage_end(Stage::Compute, s_compute_);
+    if (dev) HIP_CHECK(hipStreamWaitEvent(s_comm_, evC[n - 1], 0));
+  }
   if (n == 2) stage_begin(Stage::Gather, s_comm_);
   transfer(-1, n - 2, n - 1);
   stage_end(Stage::Gather, s_comm_);
@@ -1264,11 +1366,82 @@ void Engine::run_dist(int chunks) {
     HIP_CHECK(hipEventRecord(dist_ev_[2 * n], s_comm_));
     HIP_CHECK(hipStreamWaitEvent(s_compute_, dist_ev_[2 * n], 0));
   }
+  if (root) {  // the root's output is in the root buffer only (as with dist_direct)
+    out_buf_ = -1;
+    out_c_ = cout;
+    return;
+  }
   run_in_buf_ = 0;
   cur_ = 1;
   cur_c_ = cout;
   out_buf_ = 1;
   out_c_ = cout;
+}
+
+void Engine::run_to_host(void* dst, int chunks) {
+  STRIPE_CHECK(device(), "run_to_host needs the device backend");
+  STRIPE_CHECK(cur_c_ == plan_.cin, "engine input has " << cur_c_ << " channels, chain expects " << plan_.cin);
+  const Stripe& st = stripe();
+  const int rows = st.rows;
+  if (rows == 0) return;
+  if (cfg_.autotune && !tuned_) autotune_bands();
+  TraceRange tr("stripe.to_host");
+  if (!s_d2h_) HIP_CHECK(hipStreamCreateWithFlags(&s_d2h_, hipStreamNonBlocking));
+  chunks = std::max(1, std::min(chunks, rows));
+  while ((int)ev_cmp_.size() < chunks + 1) {
+    hipEvent_t e1, e2;
+    HIP_CHECK(hipEventCreateWithFlags(&e1, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&e2, hipEventDisableTiming));
+    ev_h2d_.push_back(e1);
+    ev_cmp_.push_back(e2);
+  }
+  const int cout = plan_.cout;
+  const int64_t Eout = (int64_t)cfg_.W * cout;
+  uint8_t* host = static_cast<uint8_t*>(dst);
+  const int in_buf = cur_;
+  // the previous step's download must be done before its rows are rewritten
+  HIP_CHECK(hipEventRecord(ev_[2], s_d2h_));
+  HIP_CHECK(hipStreamWaitEvent(s_compute_, ev_[2], 0));
+  stage_begin(Stage::E2E, s_compute_);
+  const Pass& p0 = plan_.passes[0];
+  const bool single = plan_.passes.size() == 1 &&
+                      (p0.kind == PassKind::Separable || p0.kind == PassKind::Direct || p0.kind == PassKind::Pointwise);
+  if (!single) {  // multi-pass chains: the chain, then the download in chunks
+    run(1);
+    const int ob = out_buf_;
+    HIP_CHECK(hipEventRecord(ev_cmp_[0], s_compute_));
+    HIP_CHECK(hipStreamWaitEvent(s_d2h_, ev_cmp_[0], 0));
+    stage_begin(Stage::D2H, s_d2h_);
+    copy2d(host, Eout, origin(buf_[ob], cout), pitch(cout), Eout, rows, s_d2h_, 0);
+  } else {
+    stage_begin(Stage::Compute, s_compute_);
+    const bool xchg = cfg_.halo && p0.R > 0 && part_.active > 1;
+    uint8_t* in = origin(buf_[in_buf], p0.cin);
+    uint8_t* out = origin(buf_[in_buf ^ 1], cout);
+    if (xchg) exchange_halo(in, p0.cin, p0.R, s_compute_);
+    PassLaunch L = make_launch(p0, in, out, 0);
+    for (int i = 0; i < chunks; ++i) {
+      const int y0 = (int)((int64_t)rows * i / chunks), y1 = (int)((int64_t)rows * (i + 1) / chunks);
+      L.nrange = 1;
+      L.ry[0] = y0;
+      L.ry[1] = y1;
+      launch_pass(p0, prt_[0].pc, L, s_compute_);
+      HIP_CHECK(hipEventRecord(ev_cmp_[i], s_compute_));
+      HIP_CHECK(hipStreamWaitEvent(s_d2h_, ev_cmp_[i], 0));
+      if (i == 0) stage_begin(Stage::D2H, s_d2h_);
+      copy2d(host + (int64_t)y0 * Eout, Eout, out + (int64_t)y0 * pitch(cout), pitch(cout), Eout, y1 - y0, s_d2h_, 0);
+    }
+    stage_end(Stage::Compute, s_compute_);
+    out_buf_ = in_buf ^ 1;
+    out_c_ = cout;
+  }
+  stage_end(Stage::D2H, s_d2h_);
+  stage_end(Stage::E2E, s_d2h_);
+  join_d2h();
+  // the input stays current: the next step filters the same frame
+  cur_ = in_buf;
+  cur_c_ = plan_.cin;
+  run_in_buf_ = in_buf;
 }
 
 void Engine::store_root(void* full, bool dst_device) {
@@ -1325,6 +1498,72 @@ void broadcast_small(Comm* comm, void* host, size_t bytes, int root, int device)
     HIP_CHECK(hipFree(buf));
     HIP_CHECK(hipStreamDestroy(s));
   }
+}
+
+double probe_link_rate(Comm* comm, int device, size_t bytes, int reps) {
+  if (!comm || comm->size() <= 1) return 0.0;
+  STRIPE_CHECK(bytes >= 1 && reps >= 1, "probe needs bytes, reps >= 1");
+  const bool dev = comm->device_buffers();
+  const int rank = comm->rank(), world = comm->size();
+  const int peers = rank == 0 ? world - 1 : 1;
+  hipStream_t s = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  Buffer sendb(bytes * (size_t)peers, dev), recvb(bytes * (size_t)peers, dev);
+  if (dev) {
+    if (device >= 0) HIP_CHECK(hipSetDevice(device));
+    HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    HIP_CHECK(hipEventCreate(&e0));
+    HIP_CHECK(hipEventCreate(&e1));
+  }
+  auto one = [&]() {
+    comm->group_start();
+    if (rank == 0) {
+      for (int r = 1; r < world; ++r) {
+        comm->send(sendb.data() + (size_t)(r - 1) * bytes, bytes, r, s);
+        comm->recv(recvb.data() + (size_t)(r - 1) * bytes, bytes, r, s);
+      }
+    } else {
+      comm->recv(recvb.data(), bytes, 0, s);
+      comm->send(sendb.data(), bytes, 0, s);
+    }
+    comm->group_end();
+  };
+  std::vector<double> t;
+  try {
+    one();  // connection setup and warmup
+    if (dev) comm->wait(s);
+    for (int i = 0; i < reps; ++i) {
+      if (dev) {
+        HIP_CHECK(hipEventRecord(e0, s));
+        one();
+        HIP_CHECK(hipEventRecord(e1, s));
+        comm->wait(s);
+        float ms = 0;
+        HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        t.push_back(ms);
+      } else {
+        const double t0 = host_ms();
+        one();
+        t.push_back(host_ms() - t0);
+      }
+    }
+  } catch (...) {
+    if (dev) {
+      (void)hipEventDestroy(e0);
+      (void)hipEventDestroy(e1);
+      (void)hipStreamDestroy(s);
+    }
+    throw;
+  }
+  if (dev) {
+    HIP_CHECK(hipEventDestroy(e0));
+    HIP_CHECK(hipEventDestroy(e1));
+    HIP_CHECK(hipStreamDestroy(s));
+  }
+  std::nth_element(t.begin(), t.begin() + t.size() / 2, t.end());
+  double rate = (double)bytes / std::max(1e-6, t[t.size() / 2]);
+  broadcast_small(comm, &rate, sizeof rate, 0, device);  // the root's view, on every rank
+  return rate;
 }
 
 Image run_rank(const EngineConfig& cfg_in, Comm* comm, int device, const Image* input, int iterations,

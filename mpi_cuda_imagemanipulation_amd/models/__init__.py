@@ -93,7 +93,8 @@ class Pipeline:
 
         return ops.apply(image, self.spec.chain, self.spec.border, self.fuse)
 
-    def config(self, W: int, H: int, Cc: int, backend: str = "device", device: int = -1, autotune: bool = False):
+    def config(self, W: int, H: int, Cc: int, backend: str = "device", device: int = -1, autotune: bool = False,
+               row_weights=None):
         cfg = C.EngineConfig()
         cfg.W, cfg.H, cfg.C = int(W), int(H), int(Cc)
         cfg.chain = self.spec.chain
@@ -107,24 +108,29 @@ class Pipeline:
         cfg.autotune = bool(autotune)
         cfg.halo_depth = self.halo_depth
         cfg.dist_chunks = self.dist_chunks
+        if row_weights is not None:
+            cfg.row_weights = [float(w) for w in row_weights]
         sched = os.environ.get("STRIPE_HALO_SCHEDULE")  # tuning: overlap | pipeline | serial
         if sched:
             cfg.pipeline = sched == "pipeline"
             cfg.overlap = sched != "serial"
         return cfg
 
-    def run_distributed(self, image: np.ndarray, ranks: int, backend: str = "host", iterations: int = 1):
+    def run_distributed(self, image: np.ndarray, ranks: int, backend: str = "host", iterations: int = 1,
+                        row_weights=None):
         """Root -> scatter -> per-rank chain with halo exchange -> gather, on `ranks`
         in-process ranks ('local' = N logical ranks sharing this process's GPU,
         'rccl' = one rank per GPU 0..N-1, one thread each, over an in-process
         RCCL communicator, 'host' = CPU golden path).  Returns the gathered
-        output on the host."""
+        output on the host.  row_weights: one share per rank (weighted split,
+        e.g. plan_dist_split's link-aware root share); default even rows."""
         img = np.ascontiguousarray(image, dtype=np.uint8)
         H, W = img.shape[:2]
         Cc = 1 if img.ndim == 2 else img.shape[2]
         if backend not in ("local", "host", "rccl"):
             raise ValueError(f"backend must be local, host or rccl, got {backend!r}")
-        cfg = self.config(W, H, Cc, "host" if backend == "host" else "device", device=0 if backend != "host" else -1)
+        cfg = self.config(W, H, Cc, "host" if backend == "host" else "device", device=0 if backend != "host" else -1,
+                          row_weights=row_weights)
         if backend == "rccl":
             return C.run_rccl_group(cfg, list(range(int(ranks))), img, int(iterations))
         return C.run_local_group(cfg, int(ranks), img, int(iterations))

@@ -118,10 +118,10 @@ class DistributedPipeline:
     """Per-rank handle on the native engine for one image geometry."""
 
     def __init__(self, ctx: DistContext, pipeline, W: int, H: int, Cc: int = 3, root_buffers: bool = False,
-                 autotune: bool = False):
+                 autotune: bool = False, row_weights=None):
         self.ctx = ctx
         cfg = pipeline.config(W, H, Cc, "device" if ctx.device else "host",
-                              device=ctx.local_rank if ctx.device else -1, autotune=autotune)
+                              device=ctx.local_rank if ctx.device else -1, autotune=autotune, row_weights=row_weights)
         cfg.root_buffers = root_buffers
         self.engine = C.Engine(cfg, ctx.comm)
         self.W, self.H, self.C = W, H, Cc

@@ -209,6 +209,43 @@ def link(objs: list[Path], out: Path, shared: bool, verbose: bool, extra: list[s
     print(f"  linked {out.relative_to(ROOT)}", flush=True)
 
 
+def source_hash() -> str:
+    """sha256 over every csrc/ source and header (path + bytes): the build id."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for p in sorted(CSRC.rglob("*")):
+        if p.is_file() and p.suffix in (".cpp", ".hip", ".h"):
+            h.update(str(p.relative_to(CSRC)).encode())
+            h.update(p.read_bytes())
+    return h.hexdigest()[:16]
+
+
+def write_build_info() -> None:
+    """mpi_cuda_imagemanipulation_amd/_build_info.json: what the in-tree .so was
+    built from (benchmark records carry it; the GPU box has no .git)."""
+    import json
+    import time
+
+    def run(cmd):
+        try:
+            return subprocess.run(cmd, capture_output=True, text=True, cwd=ROOT, timeout=30).stdout.strip()
+        except Exception:
+            return ""
+
+    ver = run([HIPCC, "--version"]).splitlines()
+    info = {
+        "source_hash": source_hash(),
+        "git_head": run(["git", "rev-parse", "--short=12", "HEAD"]),
+        "git_dirty": bool(run(["git", "status", "--porcelain", "--", "csrc"])),
+        "arch": ARCH,
+        "hipcc": next((l for l in ver if "version" in l.lower()), ""),
+        "flags": " ".join(f for f in common_flags() if not f.startswith("-I")),
+        "built_at": time.strftime("%Y-%m-%dT%H:%M:%S"),
+    }
+    (PKG / "_build_info.json").write_text(json.dumps(info, indent=1))
+
+
 def build(jobs: int | None = None, verbose: bool = False, clean: bool = False, cli: bool = True) -> None:
     if clean and BUILD.exists():
         shutil.rmtree(BUILD)
@@ -231,6 +268,7 @@ def build(jobs: int | None = None, verbose: bool = False, clean: bool = False, c
         if not exe.exists() or any(o.stat().st_mtime > exe.stat().st_mtime for o in core + [objs[CLI_SOURCES[0]]]):
             link(core + [objs[s] for s in CLI_SOURCES], exe, shared=False, verbose=verbose)
     write_resource_report()
+    write_build_info()
 
 
 def build_sanitized(jobs: int | None = None, verbose: bool = False) -> Path:
