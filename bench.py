@@ -76,6 +76,8 @@ def parse():
     ap.add_argument("--e2e-steps", type=int, default=3, help="steps of the e2e-scope measurement (0: skip)")
     ap.add_argument("--cold-steps", type=int, default=-1,
                     help="steps of the cache-cold resident scope (-1: --steps; 0: skip)")
+    ap.add_argument("--ref-shm", action="store_true",
+                    help="ref-window host frame in POSIX shared memory even on one rank (tests the multi-rank path)")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-autotune", action="store_true", help="skip the per-shape band / occupancy autotune")
     ap.add_argument("--backend", default="rccl", choices=["rccl", "host"],
@@ -241,6 +243,16 @@ def main():
         calls = dp.engine.run_timed(max(per, a.steps), per, not iterable)
         step_ms = stats([c / per for c in calls])
 
+    def ramp(ms_target=30.0):
+        """GPU clock ramp before a timed scope: the host-side checks between
+        scopes leave the GPU idle long enough to drop its clock"""
+        if not dev or rows == 0:
+            return
+        dp.load_synthetic(a.seed)
+        n = max(1, int(ms_target / max(1e-3, ms_per_step)))
+        run_steps(min(n, 2000))
+        dp.synchronize()
+
     # ---- correctness of the timed engine (untimed, after the timed region):
     # n_it iterated steps through the same schedule vs the golden path on edge
     # crops and on this stripe's upper seam ----
@@ -300,6 +312,7 @@ def main():
             e.engine.set_tuning(dp.engine.bands, dp.engine.caps)
         for e in engines:
             e.load_synthetic(a.seed)
+        ramp()
         for i in range(2 * nrot):  # warm: every copy once
             engines[i % nrot].run(1)
         for e in engines:
@@ -337,6 +350,7 @@ def main():
             return all_ok(check_frame_rows(lambda lo, hi: full[lo:hi], cuts))
 
         def time_dist(d, step):
+            ramp()
             for _ in range(2):
                 step()
             d.synchronize()
@@ -417,7 +431,7 @@ def main():
 
         nbytes = H * W * pinfo["cout"]
         shm = None
-        if world > 1:
+        if world > 1 or a.ref_shm:
             names = [f"stripe_refwin_{os.getpid()}" if rank == 0 else None]
             dist.broadcast_object_list(names, src=0)
             if rank == 0:
@@ -430,7 +444,7 @@ def main():
             frame_t = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)  # keeps the pages alive
             frame = frame_t.numpy()
         base = frame.ctypes.data
-        pinned = world == 1 or C.host_register(base, nbytes)
+        pinned = shm is None or C.host_register(base, nbytes)
         mine = base + row0 * W * pinfo["cout"]
         dp.load_synthetic(a.seed)
         dp.synchronize()
@@ -438,9 +452,11 @@ def main():
         dp.synchronize()
         barrier()
         ok = None
+        full = None
         if not a.no_verify:
             full = frame.reshape(H, W, -1) if pinfo["cout"] > 1 else frame.reshape(H, W)
             ok = all_ok(rank != 0 or check_frame_rows(lambda lo, hi: full[lo:hi], [r0 for r0, _ in part[1:active]]))
+        ramp()
         dp.engine.run_to_host_ptr(mine, 8)
         dp.synchronize()
         sync()
@@ -452,12 +468,12 @@ def main():
             barrier()  # rank 0's window ends when every stripe is in its memory
         rms = max_over_ranks((time.perf_counter() - t0) * 1e3) / a.ref_steps
         scopes["ref_window"] = {"mpx_s": round(W * H / (rms * 1e-3) / 1e6, 1), "ms": round(rms, 5), "verified": ok,
-                                "host_frame": "shared memory" if world > 1 else "pinned", "pinned": bool(pinned)}
+                                "host_frame": "shared memory" if shm is not None else "pinned", "pinned": bool(pinned)}
         stages["ref_window"] = {k: round(v, 4) for k, v in dp.stage_times().items() if k in ("compute", "d2h", "e2e")}
-        if world > 1:
+        if shm is not None:
             if pinned:
                 C.host_unregister(base)
-            del frame
+            del frame, full
             barrier()
             shm.close()
             if rank == 0:
@@ -465,6 +481,7 @@ def main():
 
     # ---- e2e scope (pinned host stripe -> H2D -> filter -> D2H -> pinned host) ----
     if a.e2e_steps > 0 and dev:
+        ramp()
         eng = dp.engine
         eng.alloc_host_io()
         if rows > 0:

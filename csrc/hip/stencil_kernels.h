@@ -182,21 +182,32 @@ __device__ __forceinline__ void load_luts(const KArgs& a, uint8_t* lds) {
 }
 
 // Legacy skip border (kernel.cu:83 interior-only bounds): bytes of pixels in the
-// skip region keep the prologue value.
+// skip region keep the prologue value.  The column part of the region is fixed
+// per lane, so skip_cols builds the lane's byte mask once per band (bits set:
+// the stencil output is kept); the row part is one scalar test per row, and the
+// merge is 4 bit-selects per row (was 16 compare/selects per row, and the
+// per-row scalar bounds spilled SGPRs in every SKIP instance).
 template <int C>
-__device__ __forceinline__ void apply_skip(const KArgs& a, int cb, int gy, int R, const uint32_t (&center)[4],
-                                           uint32_t (&o)[4]) {
-  const bool row_skip = gy <= R || gy >= a.Hg - R;
+__device__ __forceinline__ void skip_cols(const KArgs& a, int cb, int R, uint32_t (&keep)[4]) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    uint32_t w = o[q];
+    uint32_t m = 0;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int x = (cb + 4 * q + e) / C;
-      const uint32_t m = 0xFFu << (8 * e);
-      w = (row_skip || x <= R || x >= a.W - R) ? ((w & ~m) | (center[q] & m)) : w;
+      m |= (x > R && x < a.W - R) ? (0xFFu << (8 * e)) : 0u;
     }
-    o[q] = w;
+    keep[q] = m;
+  }
+}
+
+__device__ __forceinline__ void apply_skip(const KArgs& a, int gy, int R, const uint32_t (&keep)[4],
+                                           const uint32_t (&center)[4], uint32_t (&o)[4]) {
+  const bool row_skip = gy <= R || gy >= a.Hg - R;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t m = row_skip ? 0u : keep[q];
+    o[q] = (o[q] & m) | (center[q] & ~m);
   }
 }
 
@@ -477,6 +488,17 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : (SKIP && EXP ? 3 : 4))) void 
   const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
   const uint32_t last_row = in_row_off(a, ye - 1 + R);
   uint4* xb = xbuf[EXP ? t.wave : 0];
+  // @skip: the prologue bytes of the last 4 input rows (slot (r - ys) mod 4),
+  // so an output row's centre bytes come from registers, not a second load
+  constexpr int kRing = SKIP ? 4 : 1;
+  static_assert(!SKIP || R < kRing, "skip centre ring too short");
+  uint32_t cen[kRing][4];
+  uint32_t keep[SKIP ? 4 : 1];
+  if constexpr (SKIP) skip_cols<C>(a, cb, R, keep);
+  auto keep_centre = [&](const uint32_t (&u)[8], uint32_t (&c)[4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) c[q] = __builtin_amdgcn_perm(u[2 * q + 1], u[2 * q], 0x06040200u);
+  };
 
   VState<F> sa, sb;
 #pragma unroll
@@ -490,6 +512,9 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : (SKIP && EXP ? 3 : 4))) void 
     RawChunk<PRO> rr;
     load_raw<PRO>(rin, in_row_off(a, ys - R + i), lane_in, rr);
     cook_pairs<PRO>(a, rr, luts, u);
+    if constexpr (SKIP) {
+      if (i >= R) keep_centre(u, cen[(i - R) % kRing]);
+    }
     if constexpr (F::SOBEL) {
       if (i & 1) vpush_sobel<F>(u, sb, sa, vdummy, vdummy);
       else vpush_sobel<F>(u, sa, sb, vdummy, vdummy);
@@ -509,10 +534,13 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : (SKIP && EXP ? 3 : 4))) void 
   for (int i = 0; i < kPF; ++i) load_raw<PRO>(rin, ys + i < ye ? in_row_off(a, ys + i + R) : last_row, lane_in, nx[i]);
 
   const bool inner = rows_inside(a, ys - R, ye - 1 + R);
-  auto row_step = [&](int y, const VState<F>& prev, VState<F>& next, RawChunk<PRO>& nb, bool valid) {
+  // (i: the step's index in its unrolled group; the group starts at a multiple
+  // of kRing rows past ys, so ring slots are compile-time)
+  auto row_step = [&](int y, int i, const VState<F>& prev, VState<F>& next, RawChunk<PRO>& nb, bool valid) {
     uint32_t u[8], vv[8], dd[8];
     cook_pairs<PRO>(a, nb, luts, u);
     load_raw<PRO>(rin, ahead_row_off(a, inner, y, kPF, ye, R, last_row), lane_in, nb);
+    if constexpr (SKIP) keep_centre(u, cen[(i + R) % kRing]);  // input row y + R
     if constexpr (F::SOBEL) {
       vpush_sobel<F>(u, prev, next, vv, dd);
     } else {
@@ -609,28 +637,26 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : (SKIP && EXP ? 3 : 4))) void 
 #pragma unroll
       for (int q = 0; q < 4; ++q) o[q] = pack4(ob[4 * q], ob[4 * q + 1], ob[4 * q + 2], ob[4 * q + 3]);
     }
-    if constexpr (SKIP) {
-      uint32_t center[4];
-      load_chunk<PRO>(a, rin, in_row_off(a, y), lane_in, luts + 256, center);
-      apply_skip<C>(a, cb, a.row0 + y, R, center, o);
-    }
+    if constexpr (SKIP) apply_skip(a, a.row0 + y, R, keep, cen[i % kRing], o);
     if (a.has_epi) lut16(luts + 512, o);
     // rows past the band (tail of the 4-row group) are computed but not stored
     store_out<EXP, SAUX>(o, rout, valid, a.out_org + (uint32_t)((int64_t)y * a.out_pitch), lout, xb, lane);
   };
 
-  // rows go in groups of kPF with no branch around any step, ping-ponging the
+  // rows go in groups of kG with no branch around any step, ping-ponging the
   // filter state so no register copies are needed
   constexpr bool live_in_b = ((K - 1) & 1) != 0;
-  for (int y = ys; y < ye; y += kPF) {
+  constexpr int kG = kPF > kRing ? kPF : kRing;  // multiple of both
+  static_assert(kG % kPF == 0 && kG % kRing == 0, "row group must cover the prefetch and ring periods");
+  for (int y = ys; y < ye; y += kG) {
 #pragma unroll
-    for (int i = 0; i < kPF; i += 2) {
+    for (int i = 0; i < kG; i += 2) {
       if (live_in_b) {
-        row_step(y + i, sb, sa, nx[i], y + i < ye);
-        row_step(y + i + 1, sa, sb, nx[i + 1], y + i + 1 < ye);
+        row_step(y + i, i, sb, sa, nx[i % kPF], y + i < ye);
+        row_step(y + i + 1, i + 1, sa, sb, nx[(i + 1) % kPF], y + i + 1 < ye);
       } else {
-        row_step(y + i, sa, sb, nx[i], y + i < ye);
-        row_step(y + i + 1, sb, sa, nx[i + 1], y + i + 1 < ye);
+        row_step(y + i, i, sa, sb, nx[i % kPF], y + i < ye);
+        row_step(y + i + 1, i + 1, sb, sa, nx[(i + 1) % kPF], y + i + 1 < ye);
       }
     }
   }
@@ -683,6 +709,8 @@ __global__ __launch_bounds__(kNT, (F::K >= 5 ? 3 : 4)) void k_direct(KArgs a) {
   __shared__ __attribute__((aligned(16))) uint4 xbuf[EXP ? kWaves : 1][EXP ? 3 * kW : 1];
   uint4* xb = xbuf[EXP ? t.wave : 0];
 
+  uint32_t keep[SKIP ? 4 : 1];
+  if constexpr (SKIP) skip_cols<C>(a, cb, R, keep);
   uint32_t ring[K][NE];  // slot of input row r: (r - (ys - R)) mod K
   auto push = [&](const RawChunk<PRO>& raw, uint32_t (&slot)[NE]) __attribute__((always_inline)) {
     uint32_t u[8];
@@ -734,7 +762,7 @@ __global__ __launch_bounds__(kNT, (F::K >= 5 ? 3 : 4)) void k_direct(KArgs a) {
         const uint32_t(&cr)[NE] = ring[(o + R) % K];
 #pragma unroll
         for (int q = 0; q < 4; ++q) center[q] = __builtin_amdgcn_perm(cr[NX + 2 * q + 1], cr[NX + 2 * q], 0x06040200u);
-        apply_skip<C>(a, cb, a.row0 + yy, R, center, o4);
+        apply_skip(a, a.row0 + yy, R, keep, center, o4);
       }
       if (a.has_epi) lut16(luts + 512, o4);
       store_out<EXP, SAUX>(o4, rout, yy < ye, a.out_org + (uint32_t)((int64_t)yy * a.out_pitch), lout, xb, lane);
