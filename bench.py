@@ -398,7 +398,8 @@ def main():
         if world > 1 and dev and pinfo["passes"] and len(pinfo["passes"]) == 1:
             link = C.probe_link_rate(ctx.comm, ctx.local_rank, 64 << 20, 3)  # bytes/ms per link, one way
             rows_per_ms = rows / step_ms["median"] if step_ms else 1.0
-            hbm = step_bytes / copy_ms if copy_ms else 1.0
+            # bytes / ms the root's HBM sustains: the faster of a copy and this filter
+            hbm = step_bytes / min(copy_ms, step_ms["median"]) if copy_ms and step_ms else 1.0
             rows_per_ms, link, hbm = from_root([rows_per_ms, link, hbm])
             plan = C.plan_dist_split(H, world, W * pinfo["cin"], W * pinfo["cout"], rows_per_ms, rows_per_ms,
                                      link, hbm, 8, R)

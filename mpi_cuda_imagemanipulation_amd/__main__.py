@@ -46,6 +46,10 @@ def main(argv=None) -> int:
     r.add_argument("--dist-chunks", type=int, default=0,
                    help="> 1 ranks, one iteration, single-pass chains: ship / filter / gather the "
                         "stripes in this many overlapped row chunks (bit-identical)")
+    r.add_argument("--row-weights", default=None,
+                   help="comma list, one share per rank (weighted split, e.g. a larger root share for "
+                        "--dist-chunks); default: even rows")
+    r.add_argument("--verbose", "-v", action="store_true", help="rank-prefixed progress log on stderr")
     c = sub.add_parser("convert", help="convert between image formats")
     c.add_argument("src")
     c.add_argument("dst")
@@ -64,6 +68,11 @@ def main(argv=None) -> int:
     else:
         pipe = models.Pipeline(a.chain or "gaussian5", border=a.border or "reflect101")
     pipe.dist_chunks = a.dist_chunks
+    weights = [float(v) for v in a.row_weights.split(",")] if a.row_weights else None
+    if a.verbose:
+        import os
+
+        os.environ["STRIPE_LOG"] = "INFO"
     if a.backend in ("rccl", "gloo"):
         return _run_per_process(a, pipe)
     img = utils.read_image(a.input)
@@ -73,7 +82,9 @@ def main(argv=None) -> int:
 
         backend = "local" if torch.cuda.is_available() else "host"
     t0 = time.perf_counter()
-    out = pipe.run_distributed(img, a.ranks, backend=backend, iterations=a.iterations)
+    log = utils.get_logger("cli", 0)
+    log.info("run %s on %s, %d ranks (%s)", pipe.spec.chain, img.shape, a.ranks, backend)
+    out = pipe.run_distributed(img, a.ranks, backend=backend, iterations=a.iterations, row_weights=weights)
     ms = (time.perf_counter() - t0) * 1e3
     utils.write_image(a.output, out)
     print(json.dumps({"cmd": "run", "input": a.input, "output": a.output, "shape": list(img.shape),
@@ -90,6 +101,7 @@ def _run_per_process(a, pipe) -> int:
     from . import parallel, utils
 
     ctx = parallel.init(a.backend)
+    log = utils.get_logger("cli", ctx.rank)
     img = utils.read_image(a.input) if ctx.rank == 0 else None
     meta = [None if img is None else tuple(img.shape)]
     if ctx.world > 1:
@@ -97,7 +109,9 @@ def _run_per_process(a, pipe) -> int:
     shape = meta[0]
     H, W = shape[:2]
     Cc = 1 if len(shape) == 2 else shape[2]
-    dp = parallel.DistributedPipeline(ctx, pipe, W, H, Cc, root_buffers=True)
+    weights = [float(v) for v in a.row_weights.split(",")] if a.row_weights else None
+    dp = parallel.DistributedPipeline(ctx, pipe, W, H, Cc, root_buffers=True, row_weights=weights)
+    log.info("stripe rows %s of %dx%dx%d, chain %s", dp.stripe, W, H, Cc, pipe.spec.chain)
     dp.load_root(img)
     if ctx.world > 1:
         dist.barrier()
@@ -110,6 +124,7 @@ def _run_per_process(a, pipe) -> int:
         dp.gather()
     dp.synchronize()
     ms = (time.perf_counter() - t0) * 1e3
+    log.info("dist step %.3f ms", ms)
     if ctx.rank == 0:
         out = dp.result_root()
         utils.write_image(a.output, np.ascontiguousarray(out))

@@ -22,6 +22,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from .._native import C
+from ..utils.log import get_logger
 
 try:
     import torch
@@ -92,6 +93,8 @@ def init(backend: str = "auto") -> DistContext:
     if backend == "auto":
         backend = "rccl" if (torch is not None and torch.cuda.is_available()) else "gloo"
     device = backend == "rccl"
+    log = get_logger("parallel", rank)
+    log.info("init: rank %d of %d, local rank %d, backend %s", rank, world, local_rank, backend)
     if device:
         torch.cuda.set_device(local_rank)
     comm = None
@@ -111,6 +114,7 @@ def init(backend: str = "auto") -> DistContext:
             comm = C.make_rccl_comm(uid[0], rank, world, local_rank)
         else:
             comm = GlooComm().native(rank, world)
+    log.info("communicator ready (%s)", "rccl" if device else ("gloo" if world > 1 else "none"))
     return DistContext(rank, world, local_rank, device, comm)
 
 
@@ -168,4 +172,29 @@ def run_local_group(pipeline, image: np.ndarray, ranks: int, backend: str = "hos
     return pipeline.run_distributed(image, ranks, backend, iterations)
 
 
-__all__ = ["DistContext", "GlooComm", "init", "DistributedPipeline", "plan_rows", "run_local_group"]
+def plan_rows_weighted(H: int, weights, min_rows: int = 1):
+    """[(row0, rows)] per rank for per-rank shares `weights` and the number of active ranks."""
+    return C.plan_rows_weighted(H, [float(w) for w in weights], min_rows)
+
+
+def dist_split(H: int, world: int, row_in_bytes: int, row_out_bytes: int, root_rows_per_ms: float,
+               link_bytes_per_ms: float, hbm_bytes_per_ms: float, chunks: int = 8, min_rows: int = 1,
+               peer_rows_per_ms: float | None = None) -> dict:
+    """Link-aware split of the root-resident dist step (the root filters its
+    share in place, every peer's share crosses its own link): weights, rows and
+    the modelled times (root, peer, root-HBM floor, predicted, even split)."""
+    return C.plan_dist_split(H, world, row_in_bytes, row_out_bytes, root_rows_per_ms,
+                             peer_rows_per_ms or root_rows_per_ms, link_bytes_per_ms, hbm_bytes_per_ms, chunks,
+                             min_rows)
+
+
+def probe_link_rate(ctx: DistContext, nbytes: int = 64 << 20, reps: int = 3) -> float:
+    """Bytes per ms per root<->peer link, one direction, all links busy both ways
+    (every rank must call it; 0 on one rank)."""
+    if ctx.comm is None or ctx.world == 1:
+        return 0.0
+    return C.probe_link_rate(ctx.comm, ctx.local_rank if ctx.device else -1, nbytes, reps)
+
+
+__all__ = ["DistContext", "GlooComm", "init", "DistributedPipeline", "plan_rows", "plan_rows_weighted", "dist_split",
+           "probe_link_rate", "run_local_group"]
