@@ -45,15 +45,8 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u2 __attribute__((ext_vector_type(2)));
 
-constexpr int kSepNJ = 8;                // 16-byte column tiles per wave strip
-constexpr int kSepSB = 16 * kSepNJ;      // output bytes per strip
-constexpr int kSepWB = 256;              // staged input bytes per row
-constexpr int kSepRow = 544;             // LDS bytes per staged row: 512 + 32 makes the
-                                         // b128 fragment reads conflict-free (bank/4 = 2m+g)
-constexpr int kSepTile = 32 * kSepRow;   // one 32-row X pair per wave
-constexpr int kSepLoads = 32 * kSepWB / 8 / 64;  // 8-byte loads per lane per pair
 constexpr int kSepWaves = 4;
-constexpr int kSepEntries = 16;          // weight fragments per lane: Bh[4][2], Bv[2][2][2]
+constexpr int kSepEntries = 12;          // weight fragments per lane: Bh[2][2], Bv[2][2][2]
 
 struct SepArgs {
   KArgs a;
@@ -99,22 +92,49 @@ __device__ __forceinline__ uint32_t bytes_to_h2(uint32_t d, uint32_t sel) {
   return __builtin_bit_cast(uint32_t, h);
 }
 
-template <int KSH>
-__global__ __launch_bounds__(kSepWaves * 64, 2) void k_blur_sep(SepArgs sa) {
+// Planar kernel.  A wave owns a strip of NX x-tiles of 16 pixels (all C
+// channels) and a band of rows.  Each 32-row X pair is staged into LDS as C
+// f16 channel PLANES (RGB is de-interleaved while staging: 3 gathers + 6
+// biased byte->f16 perms per 4 pixels), so the horizontal Toeplitz product of
+// one channel needs a 64-pixel window per 16 outputs: 2 k-steps instead of the
+// 4 k-steps a 128-byte interleaved window takes (RGB: 8 horizontal MFMAs per
+// 16 output bytes instead of 16, 20 in all instead of 28).  The vertical
+// product is unchanged; for RGB a lane ends with 4 consecutive pixels of one
+// output row in each channel accumulator, i.e. 12 contiguous interleaved
+// bytes: one dwordx3 store.
+template <int C>
+struct PlGeom {
+  static constexpr int NX = C == 3 ? 2 : 8;          // 16-pixel x-tiles per strip
+  static constexpr int PX = 16 * NX;                 // output pixels per strip
+  static constexpr int WPX = PX + 48;                // staged pixels per row: [sx - 16, sx + PX + 32)
+  static constexpr int UB = C == 3 ? 12 : 16;        // bytes per staging load (4 RGB / 16 gray pixels)
+  static constexpr int UPX = UB / C;                 // pixels per staging load
+  static constexpr int U = WPX / UPX;                // loads per staged row
+  static constexpr int LPL = (32 * U + 63) / 64;     // loads per lane per 32-row pair
+  static constexpr int STRIDE = (2 * WPX + 16) | 16;  // plane row bytes: an odd multiple of 16
+                                                     // (16 rows x b128 reads hit 16 distinct bank quads)
+  static constexpr int PLANE = 32 * STRIDE;
+  static constexpr int TILE = C * PLANE;             // LDS bytes per wave
+  static_assert(WPX % UPX == 0, "staged row must be whole loads");
+  static_assert(STRIDE % 32 == 16 && STRIDE >= 2 * WPX, "plane stride");
+};
+
+// EDGE: the row width is not a multiple of 4 pixels (the last group of a row
+// is partial: byte stores); otherwise every group is whole or past the row.
+template <int C, bool EDGE>
+__global__ __launch_bounds__(kSepWaves * 64, 2) void k_blur_pl(SepArgs sa) {
+  using G = PlGeom<C>;
+  constexpr int NX = G::NX;
   const KArgs& a = sa.a;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  // task = (strip, band of a.band rows); consecutive waves take horizontally
-  // adjacent strips (their 256-byte windows overlap by half; measured ~2 %
-  // faster than strip-major order)
   const int task = xcd_remap((int)blockIdx.x, (int)gridDim.x, a.nxcd) * kSepWaves + wave;
   if (task >= sa.nstrips * a.nbands) return;  // wave-uniform
-  uint8_t* wl = lds + wave * kSepTile;
+  uint8_t* wl = lds + wave * G::TILE;
   const int strip = task % sa.nstrips, by = task / sa.nstrips;
-  // bands and 32-row groups sit on a grid of global rows (multiples of 32), so
+  // bands and 32-row groups sit on a grid of global rows (multiples of 32):
   // every output row is summed in the same order whatever the launch's row
-  // ranges (interior/boundary split, rank count): results are independent of
-  // the partition, bit for bit
+  // ranges, so results are independent of the partition, bit for bit
   int base, ys, ye;
   if (by < a.nb0) {
     base = sa.a0 + by * a.band;
@@ -127,10 +147,10 @@ __global__ __launch_bounds__(kSepWaves * 64, 2) void k_blur_sep(SepArgs sa) {
   }
   const int R = sa.R;
 
-  // ---- weights (per-lane MFMA fragments, see prepare_sep_consts) ----
-  half8 bh[KSH][2], bv[2][2][2];
+  // ---- weights: Bh[s][hl] (horizontal, 2 k-steps), Bv[q][s][hl] (vertical) ----
+  half8 bh[2][2], bv[2][2][2];
 #pragma unroll
-  for (int s = 0; s < KSH; ++s)
+  for (int s = 0; s < 2; ++s)
 #pragma unroll
     for (int hl = 0; hl < 2; ++hl) bh[s][hl] = __builtin_bit_cast(half8, sa.tw[(s * 2 + hl) * 64 + lane]);
 #pragma unroll
@@ -139,124 +159,213 @@ __global__ __launch_bounds__(kSepWaves * 64, 2) void k_blur_sep(SepArgs sa) {
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int hl = 0; hl < 2; ++hl)
-        bv[q][s][hl] = __builtin_bit_cast(half8, sa.tw[(8 + q * 4 + s * 2 + hl) * 64 + lane]);
+        bv[q][s][hl] = __builtin_bit_cast(half8, sa.tw[(4 + q * 4 + s * 2 + hl) * 64 + lane]);
 
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);
   const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
-
-  const int lo_ok = max(-R, -a.row0);      // rows addressable without remapping
+  const int lo_ok = max(-R, -a.row0);  // rows addressable without remapping
   const int hi_ok = min(a.rows - 1 + R, a.Hg - 1 - a.row0);
-  // staging map: load q (0..15) of a lane covers pair row 2q + (lane >> 5),
-  // bytes 8*(lane & 31)..+7 of the 256-byte window
-  const int hi_row = lane >> 5, chunk = lane & 31;
+  const int sx = strip * G::PX;  // first output pixel of the strip
   const int m = lane & 15, g = lane >> 4;
-  const uint8_t* frag_base = wl + m * kSepRow + 16 * g;
 
-  const int sx = strip * kSepSB;           // first output byte of the strip
-  const int x_in = sx - sa.L + 8 * chunk;  // byte offset of the lane's chunk in a row
+  // staging map: load i of a lane is unit u = lane + 64 i -> pair row u / U,
+  // pixels UPX * (u % U) .. of the staged window (window pixel 0 = sx - 16).
+  // The (row, unit) pattern repeats every P loads (64 P = a multiple of U),
+  // so only P (row, column) pairs live in registers.
+  constexpr int P = [] {
+    for (int p = 1; p < G::LPL; ++p)
+      if (64 * p % G::U == 0) return p;
+    return G::LPL;
+  }();
+  constexpr int RSTEP = 64 * P / G::U;  // pair rows advanced every P loads
+  static_assert(P == G::LPL || 64 * P % G::U == 0, "staging period");
+  int srow[P];
+  int scol[P];  // first staged pixel of the unit, relative to the window start
+#pragma unroll
+  for (int i = 0; i < P; ++i) {
+    const int u = lane + 64 * i;
+    srow[i] = u / G::U;
+    scol[i] = G::UPX * (u % G::U);
+  }
+  auto unit_ok = [&](int i) __attribute__((always_inline)) { return srow[i % P] + RSTEP * (i / P) < 32; };
+  typedef uint32_t u3 __attribute__((ext_vector_type(3)));
+  typedef std::conditional_t<C == 3, u3, u4> unit_t;
+  unit_t pf[G::LPL];
   const int yh0 = base - 16;               // input row of X row 0
-  const int ngroups = (ye - base + 31) >> 5;  // 32-row output groups
-  const int npairs = ngroups + 1;          // 32-row X pairs (tiles 2k, 2k+1)
-
-  u2 pf[kSepLoads];
+  const int ngroups = (ye - base + 31) >> 5;
   auto prefetch = [&](int k) __attribute__((always_inline)) {
     const int yt = yh0 + 32 * k;
-    if (yt >= lo_ok && yt + 31 <= hi_ok) {
-      const uint32_t base = a.in_org + (uint32_t)((int64_t)(yt + hi_row) * a.in_pitch) + (uint32_t)x_in;
+    const bool inner = yt >= lo_ok && yt + 31 <= hi_ok;
 #pragma unroll
-      for (int q = 0; q < kSepLoads; ++q)
-        pf[q] = __builtin_amdgcn_raw_buffer_load_b64(rin, base + (uint32_t)(2 * q * a.in_pitch), 0, 0);
-    } else {
+    for (int i = 0; i < G::LPL; ++i) {
+      // rows beyond the stripe + halo feed only zero weights: clamp, then border-map
+      const int y = yt + srow[i % P] + RSTEP * (i / P);
+      const uint32_t roff = inner ? a.in_org + (uint32_t)((int64_t)y * a.in_pitch)
+                                  : in_row_off(a, min(max(y, -R), a.rows - 1 + R));
+      const uint32_t off = unit_ok(i) ? roff + (uint32_t)((sx - 16 + scol[i % P]) * C) : kOOB;
+      if constexpr (C == 3) pf[i] = __builtin_amdgcn_raw_buffer_load_b96(rin, off, 0, 0);
+      else pf[i] = __builtin_amdgcn_raw_buffer_load_b128(rin, off, 0, 0);
+    }
+  };
+  auto stage = [&]() __attribute__((always_inline)) {
 #pragma unroll
-      for (int q = 0; q < kSepLoads; ++q) {
-        // rows beyond the stripe + halo feed only zero weights: clamp, then border-map
-        const int y = min(max(yt + 2 * q + hi_row, -R), a.rows - 1 + R);
-        pf[q] = __builtin_amdgcn_raw_buffer_load_b64(rin, in_row_off(a, y) + (uint32_t)x_in, 0, 0);
+    for (int i = 0; i < G::LPL; ++i) {
+      if (!unit_ok(i)) continue;  // idle lanes of the last load (lane-divergent, LDS only)
+      const int dst = (srow[i % P] + RSTEP * (i / P)) * G::STRIDE + 2 * scol[i % P];
+      if constexpr (C == 3) {
+        // bytes R0 G0 B0 R1 | G1 B1 R2 G2 | B2 R3 G3 B3 -> three planes of 4 f16
+        const uint32_t d0 = pf[i].x, d1 = pf[i].y, d2 = pf[i].z;
+        const uint32_t p01 = __builtin_amdgcn_perm(d1, d0, 0x04010300u);  // R0 R1 G0 G1
+        const uint32_t p12 = __builtin_amdgcn_perm(d2, d1, 0x06030502u);  // R2 R3 G2 G3
+        const uint32_t pb = __builtin_amdgcn_perm(d2, d1, 0x07040401u);   // B1 B2 -- B3 (byte 2 unused)
+        const uint32_t r01 = bytes_to_h2(p01, 0x04010400u), g01 = bytes_to_h2(p01, 0x04030402u);
+        const uint32_t r23 = bytes_to_h2(p12, 0x04010400u), g23 = bytes_to_h2(p12, 0x04030402u);
+        const uint32_t b01 = bytes_to_h2(__builtin_amdgcn_perm(d0, pb, 0x00000006u), 0x04010400u);  // B0 B1
+        const uint32_t b23 = bytes_to_h2(pb, 0x04030401u);                                         // B2 B3
+        *reinterpret_cast<u2*>(wl + dst) = u2{r01, r23};
+        *reinterpret_cast<u2*>(wl + G::PLANE + dst) = u2{g01, g23};
+        *reinterpret_cast<u2*>(wl + 2 * G::PLANE + dst) = u2{b01, b23};
+      } else {
+        const u4 d = pf[i];
+        u4 lo, hi;
+        lo.x = bytes_to_h2(d.x, 0x04010400u);
+        lo.y = bytes_to_h2(d.x, 0x04030402u);
+        lo.z = bytes_to_h2(d.y, 0x04010400u);
+        lo.w = bytes_to_h2(d.y, 0x04030402u);
+        hi.x = bytes_to_h2(d.z, 0x04010400u);
+        hi.y = bytes_to_h2(d.z, 0x04030402u);
+        hi.z = bytes_to_h2(d.w, 0x04010400u);
+        hi.w = bytes_to_h2(d.w, 0x04030402u);
+        *reinterpret_cast<u4*>(wl + dst) = lo;
+        *reinterpret_cast<u4*>(wl + dst + 16) = hi;
       }
     }
   };
 
-  const int xo = sx + 4 * g;  // first output byte of the lane's dword (+16 j)
-  // column tiles past the row end (last strip only): their stores get the
-  // range-check-failing bit (offsets stay < 2^31 - 2^16, checked on the host)
-  uint32_t colbad[kSepNJ];
+  // output columns: a lane's 4 pixels 4g .. 4g + 3 of x-tile i
+  uint32_t colok[NX];  // 0: whole group in the row; kOOB: none; else partial (byte stores)
+  int npx[NX];
 #pragma unroll
-  for (int j = 0; j < kSepNJ; ++j) colbad[j] = xo + 16 * j < a.E ? 0u : kOOB;
-
-  f4 acc[2][kSepNJ];  // running vertical sums of the current output group
-  // One 32-row X pair: FIN = it is k-step 1 of group k - 1 (finish + store),
-  // START = it is k-step 0 of group k.  Compile-time flags keep the MFMA
-  // stream branch-free so fragment reads and MFMAs can be interleaved.
+  for (int i = 0; i < NX; ++i) {
+    const int x = sx + 16 * i + 4 * g;
+    npx[i] = min(4, max(0, a.W - x));
+    colok[i] = npx[i] == 4 ? 0u : kOOB;
+  }
+  f4 acc[C][NX][2];  // running vertical sums of the current output group
   auto step = [&](auto fin_c, auto start_c, int k) __attribute__((always_inline)) {
     constexpr bool FIN = decltype(fin_c)::value, START = decltype(start_c)::value;
-#pragma unroll
-    for (int q = 0; q < kSepLoads; ++q) {
-      u4 v;
-      v.x = bytes_to_h2(pf[q].x, 0x04010400u);
-      v.y = bytes_to_h2(pf[q].x, 0x04030402u);
-      v.z = bytes_to_h2(pf[q].y, 0x04010400u);
-      v.w = bytes_to_h2(pf[q].y, 0x04030402u);
-      *reinterpret_cast<u4*>(wl + (2 * q + hi_row) * kSepRow + 16 * chunk) = v;
-    }
+    stage();
     sep_lds_sync();
     if (START) prefetch(k + 1);  // pair k + 1 exists iff group k does
     const int yg = base + 32 * (k - 1);  // first row of the group being finished
-    // per output-row-half byte offset of (row, xo), or kOOB for rows outside
-    // [ys, ye): one v_or per store instead of a predicate + exec mask
     uint32_t rowoff[2];
     if constexpr (FIN) {
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int y = yg + 16 * q + m;
-        rowoff[q] = (y >= ys && y < ye) ? a.out_org + (uint32_t)((int64_t)y * a.out_pitch) + (uint32_t)xo : kOOB;
+        rowoff[q] = (y >= ys && y < ye) ? a.out_org + (uint32_t)((int64_t)y * a.out_pitch) : kOOB;
       }
     }
+    // Tiles t = C i + c (x-tile i, channel c), software-pipelined: the LDS
+    // fragments of tile t + 2 are read and the horizontal MFMAs of tile t + 1
+    // issued before tile t's split and vertical MFMAs, so neither the LDS
+    // latency nor the MFMA -> VALU dependency of the split stalls the wave.
+    constexpr int T = NX * C;
+    auto hread = [&](int t, half8 (&f)[2][2]) __attribute__((always_inline)) {
+      const int i = t / C, c = t % C;
+      const uint8_t* fb = wl + c * G::PLANE + m * G::STRIDE + 2 * (16 * i + 8 * g);
 #pragma unroll
-    for (int j = 0; j < kSepNJ; ++j) {
-      // horizontal: X tiles 2k (rows 0..15 of the pair) and 2k+1 (16..31), column j
-      f4 x0 = {0.f, 0.f, 0.f, 0.f}, x1 = {0.f, 0.f, 0.f, 0.f};
-      half8 f0[KSH], f1[KSH];
-#pragma unroll
-      for (int s = 0; s < KSH; ++s) {
-        f0[s] = *reinterpret_cast<const half8*>(frag_base + 32 * (j + 2 * s));
-        f1[s] = *reinterpret_cast<const half8*>(frag_base + 16 * kSepRow + 32 * (j + 2 * s));
+      for (int s = 0; s < 2; ++s) {
+        f[0][s] = *reinterpret_cast<const half8*>(fb + 64 * s);
+        f[1][s] = *reinterpret_cast<const half8*>(fb + 16 * G::STRIDE + 64 * s);
       }
-      __builtin_amdgcn_sched_barrier(0);
+    };
+    // horizontal: X tiles of rows 0..15 and 16..31 of the pair
+    auto hmfma = [&](const half8 (&f)[2][2], f4 (&x)[2]) __attribute__((always_inline)) {
+      x[0] = f4{0.f, 0.f, 0.f, 0.f};
+      x[1] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < KSH; ++s) {
-        x0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(f0[s], bh[s][0], x0, 0, 0, 0);
-        x1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(f1[s], bh[s][0], x1, 0, 0, 0);
-        x0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(f0[s], bh[s][1], x0, 0, 0, 0);
-        x1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(f1[s], bh[s][1], x1, 0, 0, 0);
-      }
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int hl = 0; hl < 2; ++hl)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) x[h] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f[h][s], bh[s][hl], x[h], 0, 0, 0);
+    };
+    // finished output bytes of the current x-tile, packed as the channels
+    // complete: RGB interleave R0 G0 B0 R1 | G1 B1 R2 G2 | B2 R3 G3 B3 (byte e = 3 px + c)
+    uint32_t wo[2][C];
+    auto vert = [&](int t, const f4 (&x)[2]) __attribute__((always_inline)) {
+      const int i = t / C, c = t % C;
       // accumulator layout -> A operand of the vertical product (k = X row, permuted)
       uint32_t h[4], l[4];
-      split_h2(x0[0], x0[1], h[0], l[0]);
-      split_h2(x0[2], x0[3], h[1], l[1]);
-      split_h2(x1[0], x1[1], h[2], l[2]);
-      split_h2(x1[2], x1[3], h[3], l[3]);
+      split_h2(x[0][0], x[0][1], h[0], l[0]);
+      split_h2(x[0][2], x[0][3], h[1], l[1]);
+      split_h2(x[1][0], x[1][1], h[2], l[2]);
+      split_h2(x[1][2], x[1][3], h[3], l[3]);
       const u4 uh = {h[0], h[1], h[2], h[3]}, ul = {l[0], l[1], l[2], l[3]};
       const half8 ah = __builtin_bit_cast(half8, uh), al = __builtin_bit_cast(half8, ul);
+      f4 o4[2], n4[2];
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        if constexpr (FIN) {
-          f4 o4 = acc[q][j];
-          o4 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bv[q][1][0], o4, 0, 0, 0);
-          o4 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bv[q][1][1], o4, 0, 0, 0);
-          o4 = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bv[q][1][0], o4, 0, 0, 0);
-          const uint32_t o = pack_u8x4(o4);
-          __builtin_amdgcn_raw_buffer_store_b32(o, rout, (rowoff[q] | colbad[j]) + 16 * j, 0, 0);
+        o4[q] = acc[c][i][q];
+        n4[q] = f4{0.f, 0.f, 0.f, 0.f};
+      }
+      // four independent 3-MFMA chains, interleaved
+#pragma unroll
+      for (int st = 0; st < 3; ++st)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const half8 av = st == 2 ? al : ah;
+          if constexpr (FIN) o4[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, bv[q][1][st == 1], o4[q], 0, 0, 0);
+          if constexpr (START) n4[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, bv[q][0][st == 1], n4[q], 0, 0, 0);
         }
-        if constexpr (START) {
-          f4 n4 = {0.f, 0.f, 0.f, 0.f};
-          n4 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bv[q][0][0], n4, 0, 0, 0);
-          n4 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bv[q][0][1], n4, 0, 0, 0);
-          n4 = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bv[q][0][0], n4, 0, 0, 0);
-          acc[q][j] = n4;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        if constexpr (START) acc[c][i][q] = n4[q];
+        if constexpr (FIN) {
+          if (c == 0) {
+#pragma unroll
+            for (int w = 0; w < C; ++w) wo[q][w] = 0;
+          }
+#pragma unroll
+          for (int px = 0; px < 4; ++px) {
+            const int e = C * px + c;
+            wo[q][e >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(o4[q][px], e & 3, wo[q][e >> 2]);
+          }
         }
       }
+      if constexpr (FIN) {
+        if (c != C - 1) return;
+        // lane: pixels 4g .. 4g + 3 of x-tile i in output row yg + 16 q + m
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const uint32_t off = rowoff[q] + (uint32_t)((sx + 16 * i + 4 * g) * C);
+          if (!EDGE || npx[i] == 4 || npx[i] == 0 || rowoff[q] == kOOB) {
+            if constexpr (C == 3)
+              __builtin_amdgcn_raw_buffer_store_b96(u3{wo[q][0], wo[q][1], wo[q][2]}, rout, off | colok[i], 0, 0);
+            else
+              __builtin_amdgcn_raw_buffer_store_b32(wo[q][0], rout, off | colok[i], 0, 0);
+          } else {  // the row's last, partial group (W % 4 != 0): bytes < C W only
+#pragma unroll
+            for (int e = 0; e < 4 * C; ++e)
+              __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(wo[q][e >> 2] >> (8 * (e & 3))), rout,
+                                                   e < C * npx[i] ? off + (uint32_t)e : kOOB, 0, 0);
+          }
+        }
+      }
+    };
+    half8 F[2][2][2];
+    f4 X[2][2];
+    hread(0, F[0]);
+    if (T > 1) hread(1, F[1]);
+    hmfma(F[0], X[0]);
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      if (t + 1 < T) hmfma(F[(t + 1) & 1], X[(t + 1) & 1]);
+      if (t + 2 < T) hread(t + 2, F[t & 1]);
+      vert(t, X[t & 1]);
     }
-    sep_lds_sync();  // fragment reads done before the next pair overwrites the tile
+    sep_lds_sync();  // fragment reads done before the next pair overwrites the planes
   };
   using T_ = std::integral_constant<bool, true>;
   using F_ = std::integral_constant<bool, false>;
@@ -268,33 +377,22 @@ __global__ __launch_bounds__(kSepWaves * 64, 2) void k_blur_sep(SepArgs sa) {
 
 }  // namespace dev
 
-namespace {
-
-inline void sep_geometry(int R, int C, int* L, int* ksh) {
-  *L = (int)align_up(R * C, 16);
-  *ksh = (int)div_up(*L + 16 + R * C, 32);
-}
-
-}  // namespace
-
 bool sep_supported(const Pass& p) {
-  if (p.sep_h.empty() || p.sep_v.size() != p.sep_h.size() || (p.cmid != 1 && p.cmid != 3)) return false;
-  int L, ksh;
-  sep_geometry(p.R, p.cmid, &L, &ksh);
-  return L <= kMarginBytes && ksh >= 2 && ksh <= 4 && 16 * (dev::kSepNJ + 2 * ksh) <= dev::kSepWB && p.R <= 16;
+  // planar kernel: 64-pixel horizontal window per 16 outputs (R <= 16) and the
+  // 48-byte left reach of the staged window within the buffers' x-margin
+  return !p.sep_h.empty() && p.sep_v.size() == p.sep_h.size() && (p.cmid == 1 || p.cmid == 3) && p.R <= 16 &&
+         16 * p.cmid <= kMarginBytes;
 }
 
 // Per-lane weight fragments.  Lane l (g = l >> 4, n = l & 15), element j:
-//  Bh[s][hl]: window byte k = 32 s + 8 g + j, output byte n:
-//             tap t = (k - L - n + R C) / C when divisible, 0 <= t < K.
+//  Bh[s][hl]: window pixel k = 32 s + 8 g + j (window pixel 0 = x-tile start
+//             - 16), output pixel n: tap t = k - 16 - n + R when 0 <= t < K.
 //  Bv[q][s][hl]: X row hr = 32 s + 16 (j >> 2) + 4 g + (j & 3) (the accumulator
 //             order of the A operand), output row 16 q + n of the 32-row group:
 //             tap t = hr - 16 - 16 q - n + R.
 void prepare_sep_consts(const Pass& p, PassConsts* pc, hipStream_t s) {
-  const int K = p.K, R = p.R, C = p.cmid;
-  int L, ksh;
-  sep_geometry(R, C, &L, &ksh);
-  STRIPE_CHECK(sep_supported(p), "separable blur geometry unsupported (K=" << K << ", C=" << C << ")");
+  const int K = p.K, R = p.R;
+  STRIPE_CHECK(sep_supported(p), "separable blur geometry unsupported (K=" << K << ", C=" << p.cmid << ")");
   std::vector<_Float16> host((size_t)dev::kSepEntries * 64 * 8, (_Float16)0.f);
   auto put = [&](int e, int lane, int j, float w, int hl) {
     const _Float16 whi = (_Float16)w;
@@ -304,11 +402,9 @@ void prepare_sep_consts(const Pass& p, PassConsts* pc, hipStream_t s) {
   for (int lane = 0; lane < 64; ++lane) {
     const int g = lane >> 4, n = lane & 15;
     for (int j = 0; j < 8; ++j) {
-      for (int sidx = 0; sidx < 4; ++sidx) {
-        const int k = 32 * sidx + 8 * g + j;
-        const int d = k - L - n + R * C;
-        float w = 0.f;
-        if (sidx < ksh && d >= 0 && d % C == 0 && d / C < K) w = p.sep_h[(size_t)(d / C)];
+      for (int sidx = 0; sidx < 2; ++sidx) {
+        const int t = 32 * sidx + 8 * g + j - 16 - n + R;
+        const float w = (t >= 0 && t < K) ? p.sep_h[(size_t)t] : 0.f;
         for (int hl = 0; hl < 2; ++hl) put(sidx * 2 + hl, lane, j, w, hl);
       }
       for (int q = 0; q < 2; ++q)
@@ -316,7 +412,7 @@ void prepare_sep_consts(const Pass& p, PassConsts* pc, hipStream_t s) {
           const int hr = 32 * sidx + 16 * (j >> 2) + 4 * g + (j & 3);
           const int t = hr - 16 - 16 * q - n + R;
           const float w = (t >= 0 && t < K) ? p.sep_v[(size_t)t] : 0.f;
-          for (int hl = 0; hl < 2; ++hl) put(8 + q * 4 + sidx * 2 + hl, lane, j, w, hl);
+          for (int hl = 0; hl < 2; ++hl) put(4 + q * 4 + sidx * 2 + hl, lane, j, w, hl);
         }
     }
   }
@@ -369,12 +465,11 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
   a.in_zero = (uint32_t)L.in_zero;
   a.out_bytes = (uint32_t)L.out_bytes;
   a.out_org = (uint32_t)L.out_org;
-  int Lb, ksh;
-  sep_geometry(p.R, p.cmid, &Lb, &ksh);
   sa.tw = reinterpret_cast<const dev::u4*>(pc.conv);
   sa.R = p.R;
-  sa.L = Lb;
-  sa.nstrips = (int)div_up(a.E, dev::kSepSB);
+  sa.L = 16 * p.cmid;
+  const int spx = p.cmid == 3 ? dev::PlGeom<3>::PX : dev::PlGeom<1>::PX;
+  sa.nstrips = (int)div_up(L.W, spx);
 
   const int n0 = std::max(0, L.ry[1] - L.ry[0]);
   const int n1 = L.nrange > 1 ? std::max(0, L.ry[3] - L.ry[2]) : 0;
@@ -415,9 +510,11 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
     a.nb0 = (int)div_up(a.ry1 - sa.a0, band);
     a.nbands = a.nb0 + (n1 ? (int)div_up(a.ry3 - sa.a2, band) : 0);
     const dim3 grid((unsigned)div_up((int64_t)sa.nstrips * a.nbands, dev::kSepWaves));
-    const size_t lds = (size_t)dev::kSepWaves * dev::kSepTile;
-    // the kernel is channel-agnostic: the tap stride lives in the weight fragments
-    void (*fn)(dev::SepArgs) = ksh == 2 ? dev::k_blur_sep<2> : ksh == 3 ? dev::k_blur_sep<3> : dev::k_blur_sep<4>;
+    const size_t lds =
+        (size_t)dev::kSepWaves * (p.cmid == 3 ? dev::PlGeom<3>::TILE : dev::PlGeom<1>::TILE);
+    const bool edge = L.W % 4 != 0;
+    void (*fn)(dev::SepArgs) = p.cmid == 3 ? (edge ? dev::k_blur_pl<3, true> : dev::k_blur_pl<3, false>)
+                                           : (edge ? dev::k_blur_pl<1, true> : dev::k_blur_pl<1, false>);
     fn<<<grid, dev::kSepWaves * 64, lds, s>>>(sa);
     HIP_CHECK(hipGetLastError());
   }

@@ -26,7 +26,7 @@ def report():
 
 def test_every_kernel_family_reported(report):
     names = " ".join(report)
-    for fam in ["k_pointwise", "k_fill_margins", "k_synth", "k_copy_rows", "k_sep", "k_direct", "k_blur_sep",
+    for fam in ["k_pointwise", "k_fill_margins", "k_synth", "k_copy_rows", "k_sep", "k_direct", "k_blur_pl",
                 "k_conv_mfma"]:
         assert fam in names, fam
 
@@ -45,7 +45,7 @@ def test_hot_kernels_have_occupancy(report):
         occ = v.get("Occupancy [waves/SIMD]", 0)
         if "k_sep" in k or "k_direct" in k:
             assert occ >= 3, (k, occ)
-        elif "k_blur_sep" in k:
+        elif "k_blur_pl" in k:
             assert occ >= 2, (k, occ)
 
 
@@ -63,7 +63,7 @@ def test_hot_families_no_sgpr_spills(report):
     # Round 2 had 220 of 440 stencil instances spilling (every @skip variant,
     # the reference pipeline's among them): the skip region's per-row scalar
     # bounds; round 3 hoists the column mask out of the row loop.
-    hot = ("k_sep", "k_direct", "k_pointwise", "k_blur_sep", "k_conv_mfma")
+    hot = ("k_sep", "k_direct", "k_pointwise", "k_blur_pl", "k_conv_mfma")
     bad = {k: v["SGPRs Spill"] for k, v in report.items()
            if any(f in k for f in hot) and v.get("SGPRs Spill", 0) != 0}
     assert not bad, json.dumps(bad, indent=1)[:2000]
