@@ -111,12 +111,16 @@ struct PlGeom {
   static constexpr int UPX = UB / C;                 // pixels per staging load
   static constexpr int U = WPX / UPX;                // loads per staged row
   static constexpr int LPL = (32 * U + 63) / 64;     // loads per lane per 32-row pair
-  static constexpr int STRIDE = (2 * WPX + 16) | 16;  // plane row bytes: an odd multiple of 16
-                                                     // (16 rows x b128 reads hit 16 distinct bank quads)
+  // plane row bytes: 16 q with q = 2 mod 4.  ds_read_b128 serves a wave in
+  // the lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31} (+32), and the
+  // fragment of lane (m, g) starts at quad q m + g: with q = 2 mod 4 every
+  // group hits 16 distinct 4-bank quads (an odd q leaves 3 quads doubled:
+  // 44 % of the LDS cycles were bank conflicts with q = 11)
+  static constexpr int STRIDE = 16 * ((2 * WPX + 15) / 16 + (((2 - (2 * WPX + 15) / 16) % 4) + 4) % 4);
   static constexpr int PLANE = 32 * STRIDE;
   static constexpr int TILE = C * PLANE;             // LDS bytes per wave
   static_assert(WPX % UPX == 0, "staged row must be whole loads");
-  static_assert(STRIDE % 32 == 16 && STRIDE >= 2 * WPX, "plane stride");
+  static_assert(STRIDE % 64 == 32 && STRIDE >= 2 * WPX, "plane stride");
 };
 
 // EDGE: the row width is not a multiple of 4 pixels (the last group of a row
@@ -479,17 +483,17 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
     a.ry2 = n1 ? L.ry[2] : 0;
     a.ry3 = n1 ? L.ry[3] : 0;
     // band = gpb 32-row groups.  A task costs gpb + 1 pair steps (one warm-up
-    // pair per band).  A SIMD's resident waves share its MFMA and VALU pipes,
-    // so the kernel takes about ceil(tasks / SIMDs) x (gpb + 1) pair times
-    // (measured: a 16384x2048 RGB stripe at 8 groups = 3 tasks per SIMD x 9,
-    // 0.090 ms; at 13 groups = 2 x 14, 0.0975 ms): pick gpb minimising that.
+    // pair per band), and the launch runs in rounds of one task per resident
+    // wave slot (2 waves per SIMD): pick gpb minimising rounds x (gpb + 1).
+    // (Counting SIMDs instead of wave slots left a 16384x2048 RGB stripe at
+    // 3072 tasks on 2048 slots: a half-empty second round.)
     // L.band (rows, >= 32) overrides for tuning.
     const int64_t g0 = div_up(n0 + 31, 32), g1 = n1 ? div_up(n1 + 31, 32) : 0;  // groups incl. grid offset
-    const int64_t simds = resident_simds();
+    const int64_t slots = 2 * resident_simds();
     int64_t gpb = 1, best = -1;
-    for (int64_t c = 1; c <= 16; ++c) {
+    for (int64_t c = 1; c <= 64; ++c) {
       const int64_t tasks = (int64_t)sa.nstrips * (div_up(g0, c) + div_up(g1, c));
-      const int64_t cost = div_up(tasks, simds) * (c + 1);
+      const int64_t cost = div_up(tasks, slots) * (c + 1);
       if (best < 0 || cost < best) {
         best = cost;
         gpb = c;
