@@ -33,6 +33,10 @@
 #include "dev_common.h"
 #include "stripe/kernels.h"
 
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <type_traits>
 #include <vector>
 
 namespace stripe {
@@ -251,6 +255,217 @@ void k_conv_mfma(ConvArgs ca) {
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// i8 weight-digit kernel (default).  The same banded-Toeplitz implicit GEMM on
+// v_mfma_i32_16x16x64_i8: the input enters as x - 128 (exact in i8), and every
+// weight as a 24-bit fixed-point integer W = w * 2^S split into three signed
+// base-256 digits (W = d0 + 256 d1 + 65536 d2), one i32 accumulator per digit.
+// The epilogue forms sum(x W) exactly in f64 and rounds (sum) * 2^-S half to
+// even, so the only error left is the weights' 24-bit quantisation (|dw| <=
+// 2^-24 max|w|, about 2^-22 relative of the f16 hi+lo split's per weight).
+// K = 64 per MFMA holds FOUR kernel rows' 48-pixel windows in 3 k-steps, so a
+// 16x16 tile costs 3 digits x 3 k-steps = 9 MFMAs per 4 kernel rows (K = 31:
+// 72 per tile) against 2 x 3 = 6 per 2 rows (96) on f16, at the same 16 cycles
+// per MFMA; the planes are i8 (half the LDS).
+// Lane map of the 16 i8 elements of lane (m = l & 15, g = l >> 4) in k-step s:
+// 16 consecutive pixels of kernel row r = (4 s + g) / 3 at window pixel
+// 16 ((4 s + g) mod 3) -- any map works as long as A and B use the same one
+// (the sum over k pairs element j of lane (m, g) with element j of lane (n, g);
+// tools/mfma_i8_probe.hip), and 16-pixel segments never straddle a 48-pixel row.
+constexpr int kQPS = 96;  // i8 plane row bytes (>= kCWin)
+
+template <int C>
+constexpr int convq_mt() { return C == 3 ? 2 : 4; }
+
+template <int C, int MT>
+__host__ __device__ constexpr int convq_rows_staged(int nq) {
+  return (16 * MT + 4 * nq + (C == 3 ? 3 : 9) - 1) / (C == 3 ? 3 : 9) * (C == 3 ? 3 : 9);
+}
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+struct ConvI8Args {
+  KArgs a;
+  const i32x4* tw;  // B fragments: [quad][kstep 3][digit 3][lane 64]
+  int K, R, nq;     // kernel size, radius, 4-row quads (even)
+  double scale, bias;
+};
+
+constexpr int kBQuad = 9 * 1024;  // bytes of one quad's B fragments
+
+template <int C, int MT>
+__global__ __launch_bounds__(256, 2) void k_conv_i8(ConvI8Args ca) {
+  const KArgs& a = ca.a;
+  const int R = ca.R, nq = ca.nq;
+  extern __shared__ __attribute__((aligned(16))) uint8_t qplane[];  // [C][rows_in][kQPS]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int x0 = blockIdx.x * kCTN;
+  const int yb = a.ry0 + blockIdx.y * (16 * MT);
+  if (yb >= a.ry1) return;
+  const int rows_in = convq_rows_staged<C, MT>(nq);
+  const int pstride = rows_in * kQPS;
+
+  // ---- stage pixels [x0 - 16, x0 + 80) of rows yb - R .. as x - 128 ----
+  // The window starts 16 pixels left of the tile (not R): its first byte is
+  // then 16-byte aligned for RGB and gray alike (3 (x0 - 16) = 192 k - 48), so
+  // RGB goes in as 12-byte units (4 pixels) de-interleaved by byte permutes
+  // (6 perms + 3 dword stores per unit instead of 12 byte stores) and gray as
+  // 16-byte rows pieces; the taps shift by 16 - R in the B fragments.
+  {
+    const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);
+    constexpr int UB = C == 3 ? 12 : 16;              // bytes per unit
+    constexpr int U = kCWin * C / UB;                  // units per staged row: 24 (RGB) / 6 (gray)
+    constexpr int kMaxRows = convq_rows_staged<C, MT>(10);  // K <= 33
+    constexpr int kG = (kMaxRows * U + 255) / 256;     // unit loads per thread
+    const int nunits = rows_in * U;
+    const bool inner = rows_inside(a, yb - R, a.ry1 - 1 + R);
+    const uint32_t colb = (uint32_t)((x0 - 16) * C);
+    typedef uint32_t u3 __attribute__((ext_vector_type(3)));
+    typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+    typedef std::conditional_t<C == 3, u3, u4v> unit_t;
+    unit_t d[kG];
+#pragma unroll
+    for (int i = 0; i < kG; ++i) {
+      const int u = tid + 256 * i;
+      const int r = u / U, k = u % U;
+      // rows past the last needed input row feed only unstored outputs / zero
+      // weights: clamp so no read leaves the stripe + halo
+      const int y = min(yb - R + r, a.ry1 - 1 + R);
+      const uint32_t roff = inner ? a.in_org + (uint32_t)((int64_t)y * a.in_pitch) : in_row_off(a, y);
+      const uint32_t off = u < nunits ? roff + colb + (uint32_t)(UB * k) : kOOB;
+      if constexpr (C == 3) d[i] = __builtin_amdgcn_raw_buffer_load_b96(rin, off, 0, 0);
+      else d[i] = __builtin_amdgcn_raw_buffer_load_b128(rin, off, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < kG; ++i) {
+      const int u = tid + 256 * i;
+      if (u >= nunits) break;  // lane-divergent only in the last load
+      const int r = u / U, k = u % U;
+      if constexpr (C == 3) {
+        // R0 G0 B0 R1 | G1 B1 R2 G2 | B2 R3 G3 B3 -> R0..R3, G0..G3, B0..B3 (x - 128)
+        const uint32_t d0 = d[i].x ^ 0x80808080u, d1 = d[i].y ^ 0x80808080u, d2 = d[i].z ^ 0x80808080u;
+        const uint32_t p01 = __builtin_amdgcn_perm(d1, d0, 0x04010300u);  // R0 R1 G0 G1
+        const uint32_t p12 = __builtin_amdgcn_perm(d2, d1, 0x06030502u);  // R2 R3 G2 G3
+        const uint32_t rr = __builtin_amdgcn_perm(p12, p01, 0x05040100u);
+        const uint32_t gg = __builtin_amdgcn_perm(p12, p01, 0x07060302u);
+        const uint32_t pb = __builtin_amdgcn_perm(d2, d1, 0x07040401u);   // B1 B2 -- B3
+        const uint32_t bb = __builtin_amdgcn_perm(pb, d0, 0x07050402u);   // B0 B1 B2 B3
+        uint8_t* row = qplane + r * kQPS + 4 * k;
+        *reinterpret_cast<uint32_t*>(row) = rr;
+        *reinterpret_cast<uint32_t*>(row + pstride) = gg;
+        *reinterpret_cast<uint32_t*>(row + 2 * pstride) = bb;
+      } else {
+        *reinterpret_cast<u4v*>(qplane + r * kQPS + 16 * k) = d[i] ^ 0x80808080u;
+      }
+    }
+  }
+  __syncthreads();
+
+  // per-lane A offsets of the three k-steps of a quad (see the lane map above)
+  const int m = lane & 15, g = lane >> 4;
+  int aoff[3];
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    const int e = 4 * s + g;
+    aoff[s] = (m + e / 3) * kQPS + 16 * (e % 3) + 16 * wave;
+  }
+
+  i32x4 acc[3][C][MT];
+#pragma unroll
+  for (int d = 0; d < 3; ++d)
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) acc[d][c][mt] = i32x4{0, 0, 0, 0};
+
+  // k-step stream t = 3 q + s: B(t) (3 digits) through a 3-slot register ring
+  // two steps ahead, A(t + 1) read from the planes while step t multiplies
+  const __amdgpu_buffer_rsrc_t rtw = make_rsrc(ca.tw, (uint32_t)nq * (uint32_t)kBQuad);
+  const uint32_t tl = 16u * (uint32_t)lane;
+  const int nsteps = 3 * nq;
+  i32x4 bq[3][3];
+  auto load_b = [&](int t, int slot) __attribute__((always_inline)) {
+    const uint32_t off = (uint32_t)min(t, nsteps - 1) * 3072u + tl;  // past the end: re-read (unused)
+#pragma unroll
+    for (int dg = 0; dg < 3; ++dg)
+      bq[slot][dg] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(rtw, off + 1024u * dg, 0, 0));
+  };
+  i32x4 af[2][C][MT];
+  auto read_a = [&](int q, int s, int buf) __attribute__((always_inline)) {
+    const uint8_t* pl = qplane + 4 * q * kQPS + aoff[s];
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+        af[buf][c][mt] = *reinterpret_cast<const i32x4*>(pl + c * pstride + 16 * mt * kQPS);
+  };
+  load_b(0, 0);
+  load_b(1, 1);
+  read_a(0, 0, 0);
+  // 6 steps = 2 quads per body (nq is even: the host pads a zero-weight quad)
+  for (int q0 = 0; q0 < nsteps; q0 += 6) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const int t = q0 + i;
+      load_b(t + 2, (i + 2) % 3);
+      read_a(min((q0 / 3) + (i + 1) / 3, nq - 1), (i + 1) % 3, (i + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int dg = 0; dg < 3; ++dg)
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+            acc[dg][c][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[i & 1][c][mt], bq[i % 3][dg], acc[dg][c][mt], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  __syncthreads();  // every wave's last fragment read before the planes are reused
+
+  // ---- epilogue: sum(x W) exactly in f64, * 2^-S, round half even, saturate;
+  // the tile leaves through LDS as 16-byte row chunks ----
+  constexpr int kOS = kCTN * C + 16;
+  uint8_t* otile = qplane;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const double v = __builtin_fma((double)acc[2][c][mt][r], 65536.0,
+                                       __builtin_fma((double)acc[1][c][mt][r], 256.0, (double)acc[0][c][mt][r]));
+        const double o = __builtin_rint(__builtin_fma(v, ca.scale, ca.bias));
+        otile[(16 * mt + 4 * g + r) * kOS + (16 * wave + m) * C + c] = (uint8_t)__builtin_fmin(__builtin_fmax(o, 0.0), 255.0);
+      }
+  __syncthreads();
+  const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
+  constexpr int NCO = kCTN * C / 16;
+  const int E = a.W * C;
+#pragma unroll
+  for (int k = 0; k < (16 * MT * NCO + 255) / 256; ++k) {
+    const int q = tid + 256 * k;
+    if (q >= 16 * MT * NCO) break;
+    const int row = q / NCO, ch = q % NCO;
+    const int y = yb + row;
+    const int b = x0 * C + 16 * ch;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = *reinterpret_cast<const u32x4*>(otile + row * kOS + 16 * ch);
+    const uint32_t roff = a.out_org + (uint32_t)((int64_t)y * a.out_pitch) + (uint32_t)b;
+    if (y < a.ry1) {
+      if (b + 16 <= E) {
+        __builtin_amdgcn_raw_buffer_store_b128(v, rout, roff, 0, 0);
+      } else if (b < E) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v[i >> 2] >> (8 * (i & 3))), rout,
+                                               b + i < E ? roff + (uint32_t)i : kOOB, 0, 0);
+      }
+    }
+  }
+}
+
 }  // namespace dev
 
 // Kernel-row pairs of a K x K window, padded to an even count (a zero-weight
@@ -263,8 +478,84 @@ static int conv_pairs(int K) {
 // B fragments: pair p, k-step s, part hl, lane l (g = l >> 4, n = l & 15),
 // element j: k = 32 s + 8 g + j -> (kernel row 2p + (k >= 48), window pixel
 // k mod 48); B[k][n] = w[ky][px - n] for 0 <= px - n < K, else 0.
+// STRIPE_CONV_F16=1: the f16 hi+lo kernel (k_conv_mfma) instead of the i8
+// weight-digit kernel (A/B runs)
+static bool conv_f16() {
+  static const bool v = [] {
+    const char* e = std::getenv("STRIPE_CONV_F16");
+    return e && std::atoi(e) != 0;
+  }();
+  return v;
+}
+
+// 4-row quads of a K x K window, padded to an even count (zero-weight quad).
+static int conv_quads(int K) {
+  const int nq = (K + 3) / 4;
+  return nq + (nq & 1);
+}
+
+// i8 digits: S = the largest shift with max|W| <= 2^23 - 2^15 - 1 (so the top
+// digit of the balanced base-256 split stays in [-128, 127]); fragments of
+// quad q, k-step s, digit d, lane l (g = l >> 4, n = l & 15), element j:
+// kernel row 4 q + (4 s + g) / 3, window pixel px = 16 ((4 s + g) mod 3) + j,
+// B[k][n] = digit d of W[ky][px - n - (16 - R)] (the window starts 16 pixels
+// left of the tile).
+static void prepare_conv_i8(const Pass& p, PassConsts* pc, hipStream_t s) {
+  const int K = p.K;
+  STRIPE_CHECK(K >= 1 && K <= 33, "conv K=" << K << " exceeds the 48-pixel Toeplitz window");
+  double maxw = 0;
+  for (float w : p.conv_w) maxw = std::max(maxw, std::fabs((double)w));
+  int S = 0;
+  if (maxw > 0) S = (int)std::floor(std::log2((double)((1 << 23) - (1 << 15) - 1) / maxw));
+  std::vector<int64_t> W((size_t)K * K);
+  int64_t wsum = 0;
+  for (size_t i = 0; i < W.size(); ++i) {
+    W[i] = std::llround(std::ldexp((double)p.conv_w[i], S));
+    STRIPE_CHECK(std::llabs(W[i]) <= (1 << 23) - (1 << 15), "weight digit range");
+    wsum += W[i];
+  }
+  auto digit = [](int64_t w, int d) {
+    int64_t v = w;
+    int8_t dg = 0;
+    for (int i = 0; i <= d; ++i) {
+      dg = (int8_t)(uint8_t)(v & 0xFF);  // balanced: the low byte as a signed value
+      v = (v - dg) / 256;
+    }
+    return dg;
+  };
+  const int nq = conv_quads(K);
+  std::vector<int8_t> host((size_t)nq * 9 * 64 * 16, 0);
+  for (int q = 0; q < nq; ++q)
+    for (int st = 0; st < 3; ++st)
+      for (int d = 0; d < 3; ++d)
+        for (int l = 0; l < 64; ++l)
+          for (int j = 0; j < 16; ++j) {
+            const int e = 4 * st + (l >> 4);
+            // window pixel 0 = tile pixel -16 (staging alignment): tap = px - n - (16 - R)
+            const int ky = 4 * q + e / 3, px = 16 * (e % 3) + j, tap = px - (l & 15) - (16 - p.R);
+            int8_t v = 0;
+            if (ky < K && tap >= 0 && tap < K) v = digit(W[(size_t)ky * K + tap], d);
+            host[((((size_t)q * 3 + st) * 3 + d) * 64 + l) * 16 + j] = v;
+          }
+  // the split is exact: d0 + 256 d1 + 65536 d2 == W for every weight
+  for (int64_t w : W) STRIPE_CHECK(digit(w, 0) + 256 * (int64_t)digit(w, 1) + 65536 * (int64_t)digit(w, 2) == w, "digits");
+  pc->conv_mode = 1;
+  pc->conv_scale = std::ldexp(1.0, -S);
+  pc->conv_bias = 128.0 * (double)wsum * pc->conv_scale;
+  pc->conv_bytes = host.size();
+  HIP_CHECK(hipMalloc(&pc->conv, pc->conv_bytes));
+  HIP_CHECK(hipMemcpyAsync(pc->conv, host.data(), pc->conv_bytes, hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+}
+
 void prepare_conv_consts(const Pass& p, PassConsts* pc, hipStream_t s) {
   if (sep_supported(p)) return prepare_sep_consts(p, pc, s);
+  // MFMAs per 16x16 tile: i8 3 digits x 3 k-steps per 4-row quad, f16 2 parts x
+  // 3 k-steps per row pair (both padded to an even count); ties go to f16
+  // (K = 9: 1.26 vs 1.41 ms on 16K RGB, the i8 kernel's epilogue and 3
+  // accumulator sets cost more where the MFMA count does not drop)
+  const bool i8 = 9 * conv_quads(p.K) < 6 * conv_pairs(p.K);
+  if (!conv_f16() && i8) return prepare_conv_i8(p, pc, s);
   const int K = p.K;
   STRIPE_CHECK(K >= 1 && K <= 33, "conv K=" << K << " exceeds the 48-pixel Toeplitz window");
   const int np = conv_pairs(K);
@@ -315,6 +606,50 @@ void launch_conv_mfma(const Pass& p, const PassConsts& pc, const PassLaunch& L, 
                "conv launch needs the allocation view (< 2 GiB buffers)");
   STRIPE_CHECK((L.rebased || (L.in_org >= kMarginBytes && L.out_org >= kMarginBytes)) && L.in_zero >= kMarginBytes,
                "bad origin offsets");
+  if (pc.conv_mode == 1) {
+    dev::ConvI8Args ci{};
+    dev::KArgs& a = ci.a;
+    a.in = L.in;
+    a.out = L.out;
+    a.zero_row = L.zero_row;
+    a.in_pitch = L.in_pitch;
+    a.out_pitch = L.out_pitch;
+    a.W = L.W;
+    a.E = L.W * p.cmid;
+    a.rows = L.rows;
+    a.row0 = L.row0;
+    a.Hg = L.Hg;
+    a.border = (int)p.border;
+    a.in_base = L.in_base;
+    a.in_bytes = (uint32_t)L.in_bytes;
+    a.in_org = (uint32_t)L.in_org;
+    a.in_zero = (uint32_t)L.in_zero;
+    a.out_base = L.out_base;
+    a.out_bytes = (uint32_t)L.out_bytes;
+    a.out_org = (uint32_t)L.out_org;
+    ci.tw = reinterpret_cast<const dev::i32x4*>(pc.conv);
+    ci.K = p.K;
+    ci.R = p.R;
+    ci.nq = conv_quads(p.K);
+    ci.scale = pc.conv_scale;
+    ci.bias = pc.conv_bias;
+    const int mt = p.cmid == 3 ? dev::convq_mt<3>() : dev::convq_mt<1>();
+    const int rows_in = p.cmid == 3 ? dev::convq_rows_staged<3, dev::convq_mt<3>()>(ci.nq)
+                                    : dev::convq_rows_staged<1, dev::convq_mt<1>()>(ci.nq);
+    const size_t lds = std::max((size_t)p.cmid * rows_in * dev::kQPS,  // planes
+                                (size_t)16 * mt * (dev::kCTN * p.cmid + 16));  // output tile
+    for (int r = 0; r < L.nrange; ++r) {
+      const int y0 = L.ry[2 * r], y1 = L.ry[2 * r + 1];
+      if (y1 <= y0) continue;
+      a.ry0 = y0;
+      a.ry1 = y1;
+      const dim3 grid((unsigned)div_up(L.W, dev::kCTN), (unsigned)div_up(y1 - y0, 16 * mt));
+      if (p.cmid == 3) dev::k_conv_i8<3, dev::convq_mt<3>()><<<grid, 256, lds, s>>>(ci);
+      else dev::k_conv_i8<1, dev::convq_mt<1>()><<<grid, 256, lds, s>>>(ci);
+      HIP_CHECK(hipGetLastError());
+    }
+    return;
+  }
   dev::ConvArgs ca{};
   dev::KArgs& a = ca.a;
   a.in = L.in;

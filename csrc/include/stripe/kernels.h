@@ -31,6 +31,9 @@ struct PassConsts {
   uint8_t* luts = nullptr;   // kLutBytes, layout above
   void* conv = nullptr;      // conv pass: packed MFMA operand tables
   size_t conv_bytes = 0;
+  int conv_mode = 0;         // general conv: 0 f16 hi+lo row pairs, 1 i8 weight digits (k_conv_i8)
+  double conv_scale = 0;     // i8 digits: weights = W_int * conv_scale (a power of two)
+  double conv_bias = 0;      // i8 digits: 128 * sum(W_int) * conv_scale (the x - 128 shift)
 };
 
 struct PassLaunch {
