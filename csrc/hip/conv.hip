@@ -261,9 +261,10 @@ void k_conv_mfma(ConvArgs ca) {
 // v_mfma_i32_16x16x64_i8: the input enters as x - 128 (exact in i8), and every
 // weight as a 24-bit fixed-point integer W = w * 2^S split into three signed
 // base-256 digits (W = d0 + 256 d1 + 65536 d2), one i32 accumulator per digit.
-// The epilogue forms sum(x W) exactly in f64 and rounds (sum) * 2^-S half to
-// even, so the only error left is the weights' 24-bit quantisation (|dw| <=
-// 2^-24 max|w|, about 2^-22 relative of the f16 hi+lo split's per weight).
+// The epilogue combines the digit sums (exact integers) with power-of-two
+// scales in three f32 FMAs and rounds half to even: the error left is the
+// weights' 24-bit quantisation (|dw| <= 2^-24 max|w|) and ~2^-15 of f32
+// rounding, so an output differs from the f64 golden only within ~1e-4 of a tie.
 // K = 64 per MFMA holds FOUR kernel rows' 48-pixel windows in 3 k-steps, so a
 // 16x16 tile costs 3 digits x 3 k-steps = 9 MFMAs per 4 kernel rows (K = 31:
 // 72 per tile) against 2 x 3 = 6 per 2 rows (96) on f16, at the same 16 cycles
@@ -428,16 +429,22 @@ __global__ __launch_bounds__(256, 2) void k_conv_i8(ConvI8Args ca) {
   // the tile leaves through LDS as 16-byte row chunks ----
   constexpr int kOS = kCTN * C + 16;
   uint8_t* otile = qplane;
+  const float s0 = (float)ca.scale, s1 = (float)(ca.scale * 256.0), s2 = (float)(ca.scale * 65536.0);
+  const float bias = (float)ca.bias;
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
       for (int c = 0; c < C; ++c) {
-        const double v = __builtin_fma((double)acc[2][c][mt][r], 65536.0,
-                                       __builtin_fma((double)acc[1][c][mt][r], 256.0, (double)acc[0][c][mt][r]));
-        const double o = __builtin_rint(__builtin_fma(v, ca.scale, ca.bias));
-        otile[(16 * mt + 4 * g + r) * kOS + (16 * wave + m) * C + c] = (uint8_t)__builtin_fmin(__builtin_fmax(o, 0.0), 255.0);
+        // digit sums are exact in f32 (|D| <= 961 * 128 * 128 < 2^24) and the
+        // scales are powers of two; the three f32 FMAs round the result to
+        // ~2^-15 (an output changes only within ~1e-4 of a tie), and
+        // v_cvt_pk_u8_f32 rounds half to even and saturates
+        const float v = __builtin_fmaf((float)acc[2][c][mt][r], s2,
+                                       __builtin_fmaf((float)acc[1][c][mt][r], s1,
+                                                      __builtin_fmaf((float)acc[0][c][mt][r], s0, bias)));
+        otile[(16 * mt + 4 * g + r) * kOS + (16 * wave + m) * C + c] = (uint8_t)__builtin_amdgcn_cvt_pk_u8_f32(v, 0, 0u);
       }
   __syncthreads();
   const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);

@@ -15,3 +15,5 @@ done
 timeout -k 10 300 python3 tools/kbench.py --chains "$CONV9|" --shape 16384x16384x3 --iters 10 >> $O/kb_i8.jsonl 2>/dev/null
 STRIPE_CONV_F16=1 timeout -k 10 300 python3 tools/kbench.py --chains "$CONV9|" --shape 16384x16384x3 --iters 10 >> $O/kb_f16.jsonl 2>/dev/null
 echo i8; cut -c1-60,200-300 $O/kb_i8.jsonl; echo f16; cut -c1-60,200-300 $O/kb_f16.jsonl
+bash scripts/profile.sh "$CONV|" 16384x2048x3 gpurun_out/r3prof_conv > /dev/null 2>&1 && echo conv prof done
+grep -A9 "k_conv_i8" gpurun_out/r3prof_conv/summary.txt | grep -v "^--" | head -60
