@@ -250,6 +250,7 @@ int cmd_run(const Args& a) {
   const std::string backend = a.get("backend", cfg.backend == BackendKind::Host ? "host" : "local");
   const int iters = a.geti("iterations", 1);
   if (a.has("verbose")) {
+    set_log_level(LogLevel::Info);
     std::cerr << compile_chain(parse_chain(cfg.chain), cfg.C, cfg.border, cfg.fuse).describe();
     std::cerr << plan_rows(cfg.H, N, 1, cfg.legacy_partition).describe() << "\n";
   }

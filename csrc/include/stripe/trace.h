@@ -10,6 +10,7 @@
 //     (STRIPE_COMM_TIMEOUT_S, default 600 s) after which the group aborts.
 #pragma once
 
+#include <sstream>
 #include <string>
 
 namespace stripe {
@@ -37,4 +38,24 @@ void fault_point(const char* stage, int rank);
 
 double comm_timeout_s();
 
+// Leveled, rank-prefixed log lines on stderr (SURVEY §5 metrics / logging; the
+// reference prints with std::cout from rank 0 only, kernel.cu:186-188,230-232).
+// Level from STRIPE_LOG = error | warning | info | debug (default warning, the
+// same variable the Python logger reads); `stripe --verbose` sets info.
+enum class LogLevel : int { Error = 0, Warning = 1, Info = 2, Debug = 3 };
+LogLevel log_level();
+void set_log_level(LogLevel l);
+void log_line(LogLevel l, int rank, const std::string& msg);  // "[r<rank> hh:mm:ss.mmm L] msg"
+
 }  // namespace stripe
+
+// STRIPE_LOG(Info, rank, "stripe rows " << n): the message is only formatted
+// when the level is enabled
+#define STRIPE_LOG(level, rank, expr)                                           \
+  do {                                                                          \
+    if ((int)::stripe::LogLevel::level <= (int)::stripe::log_level()) {         \
+      std::ostringstream _ls;                                                   \
+      _ls << expr;                                                              \
+      ::stripe::log_line(::stripe::LogLevel::level, (rank), _ls.str());         \
+    }                                                                           \
+  } while (0)

@@ -155,6 +155,11 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
   }
   cur_c_ = cfg_.C;
   if (device()) HIP_CHECK(hipDeviceSynchronize());
+  STRIPE_LOG(Info, rank_, "engine: " << (device() ? "device " + std::to_string(cfg_.device) : std::string("host"))
+                                     << ", " << cfg_.W << "x" << cfg_.H << "x" << cfg_.C << " '" << cfg_.chain
+                                     << "', " << plan_.passes.size() << " pass(es), stripe rows [" << stripe().row0
+                                     << ", " << stripe().row0 + stripe().rows << ") of " << part_.active
+                                     << " active ranks, halo " << halo_ << " rows, depth " << depth_);
 }
 
 Engine::~Engine() {
@@ -827,6 +832,8 @@ void Engine::autotune_bands() {
     }
     prt_[i].band = best_band;
     prt_[i].wgs = best_wgs;
+    STRIPE_LOG(Info, rank_, "autotune pass " << i << ": band " << best_band << " rows, occupancy cap " << best_wgs
+                                             << " (" << best * 1e3f << " us per launch)");
   }
 }
 
@@ -1622,6 +1629,11 @@ Image run_group(const EngineConfig& cfg, const std::vector<Comm*>& comms, const 
         out = std::move(o);
         if (times) *times = t;
       }
+    } catch (const std::exception& ex) {
+      STRIPE_LOG(Error, r, "rank failed: " << ex.what() << " (aborting the group)");
+      std::lock_guard<std::mutex> lk(mu);
+      if (!err) err = std::current_exception();
+      for (Comm* c : comms) c->abort("rank " + std::to_string(r) + " failed");
     } catch (...) {
       std::lock_guard<std::mutex> lk(mu);
       if (!err) err = std::current_exception();

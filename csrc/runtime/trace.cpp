@@ -7,9 +7,14 @@
 
 #include <rocprofiler-sdk-roctx/roctx.h>
 
+#include <atomic>
+#include <cctype>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
+#include <mutex>
 #include <sstream>
 
 #include "stripe/common.h"
@@ -71,6 +76,47 @@ void fault_point(const char* stage, int rank) {
     }
     fail(msg.str());
   }
+}
+
+namespace {
+std::atomic<int> g_log_level{-1};
+std::mutex g_log_mu;
+
+int parse_level() {
+  const char* e = std::getenv("STRIPE_LOG");
+  if (!e) return (int)LogLevel::Warning;
+  std::string v(e);
+  for (auto& ch : v) ch = (char)std::tolower((unsigned char)ch);
+  if (v == "error" || v == "critical") return (int)LogLevel::Error;
+  if (v == "info") return (int)LogLevel::Info;
+  if (v == "debug") return (int)LogLevel::Debug;
+  return (int)LogLevel::Warning;
+}
+}  // namespace
+
+LogLevel log_level() {
+  int l = g_log_level.load(std::memory_order_relaxed);
+  if (l < 0) {
+    l = parse_level();
+    g_log_level.store(l);
+  }
+  return (LogLevel)l;
+}
+
+void set_log_level(LogLevel l) { g_log_level.store((int)l); }
+
+void log_line(LogLevel l, int rank, const std::string& msg) {
+  static const char tag[] = {'E', 'W', 'I', 'D'};
+  const auto now = std::chrono::system_clock::now();
+  const std::time_t t = std::chrono::system_clock::to_time_t(now);
+  const int ms = (int)(std::chrono::duration_cast<std::chrono::milliseconds>(now.time_since_epoch()).count() % 1000);
+  std::tm tmv{};
+  localtime_r(&t, &tmv);
+  char ts[32];
+  std::strftime(ts, sizeof ts, "%H:%M:%S", &tmv);
+  std::lock_guard<std::mutex> lk(g_log_mu);
+  std::fprintf(stderr, "[r%d %s.%03d %c] %s\n", rank, ts, ms, tag[(int)l & 3], msg.c_str());
+  std::fflush(stderr);
 }
 
 double comm_timeout_s() {
