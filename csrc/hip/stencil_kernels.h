@@ -135,17 +135,20 @@ __device__ __forceinline__ void gray_ref_pairs(const KArgs& a, const uint32_t (&
   const uint8_t* tr = luts + 768;
   const uint8_t* tg = luts + 1024;
   const uint8_t* tb = luts + 1280;
+  // all 48 term lookups first, then the sums, then (one uniform branch) the
+  // 16 post-LUT lookups: two LDS round trips per row.  (With the post-LUT
+  // test inside the per-pixel loop hipcc emitted 16 basic blocks of "3
+  // lookups, wait, add, branch, lookup": 32 dependent LDS waits per row.)
+  uint32_t g[16];
 #pragma unroll
-  for (int pp = 0; pp < 8; ++pp) {
-    uint32_t g2[2];
+  for (int px = 0; px < 16; ++px)
+    g[px] = (uint32_t)tr[byte_at(d, 3 * px)] + (uint32_t)tg[byte_at(d, 3 * px + 1)] + (uint32_t)tb[byte_at(d, 3 * px + 2)];
+  if (a.has_post) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int b0 = 3 * (2 * pp + h);
-      g2[h] = (uint32_t)tr[byte_at(d, b0)] + (uint32_t)tg[byte_at(d, b0 + 1)] + (uint32_t)tb[byte_at(d, b0 + 2)];
-      if (a.has_post) g2[h] = luts[256 + g2[h]];
-    }
-    u[pp] = g2[0] | (g2[1] << 16);
+    for (int px = 0; px < 16; ++px) g[px] = luts[256 + g[px]];
   }
+#pragma unroll
+  for (int pp = 0; pp < 8; ++pp) u[pp] = g[2 * pp] | (g[2 * pp + 1] << 16);
 }
 
 // Prologue: the 16 output-channel bytes of a raw chunk.

@@ -183,8 +183,9 @@ class Engine {
   // stripe: the chain (halo exchange included), its output rows downloaded in
   // `chunks` row chunks as they are filtered, into `dst` (packed rows of this
   // rank's stripe; pinned or registered host memory, e.g. this rank's slice of
-  // a frame shared with rank 0).  The input is left as it was (the step can
-  // be repeated on the same frame).
+  // a frame shared with rank 0).  Single-pass chains leave the input as it
+  // was (the step can be repeated on the same frame); multi-pass chains
+  // consume it like run(1) (their ping-pong passes overwrite it).
   void run_to_host(void* dst, int chunks = 8);
 
   // ---- end-to-end (host -> device -> host) ----

@@ -1411,9 +1411,8 @@ void Engine::run_to_host(void* dst, int chunks) {
   HIP_CHECK(hipStreamWaitEvent(s_compute_, ev_[2], 0));
   stage_begin(Stage::E2E, s_compute_);
   const Pass& p0 = plan_.passes[0];
-  const bool single = plan_.passes.size() == 1 &&
-                      (p0.kind == PassKind::Separable || p0.kind == PassKind::Direct || p0.kind == PassKind::Pointwise);
-  if (!single) {  // multi-pass chains: the chain, then the download in chunks
+  const bool single = plan_.passes.size() == 1;  // any kind: launch_pass takes row ranges
+  if (!single) {  // multi-pass chains: the chain, then the download
     run(1);
     const int ob = out_buf_;
     HIP_CHECK(hipEventRecord(ev_cmp_[0], s_compute_));
@@ -1445,10 +1444,11 @@ void Engine::run_to_host(void* dst, int chunks) {
   stage_end(Stage::D2H, s_d2h_);
   stage_end(Stage::E2E, s_d2h_);
   join_d2h();
-  // the input stays current: the next step filters the same frame
-  cur_ = in_buf;
-  cur_c_ = plan_.cin;
-  run_in_buf_ = in_buf;
+  if (single) {  // the input stays current: the next step filters the same frame
+    cur_ = in_buf;
+    cur_c_ = plan_.cin;
+    run_in_buf_ = in_buf;
+  }
 }
 
 void Engine::store_root(void* full, bool dst_device) {

@@ -92,7 +92,8 @@ def test_mfma_conv_blur(m, rng, K, C, shape):
         got = _run(m, img, f"blur:{K}", border)
         ref = m._C.golden_apply(img, f"blur:{K}", border, True)
         d = np.abs(got.astype(int) - ref.astype(int))
-        assert d.max() <= 1 and (d == 0).mean() > 0.995, (K, C, shape, border, d.max(), (d == 0).mean())
+        # ties only: round 3 measured <= 1 in 2000 (tests/test_oracle_conv.py checks where)
+        assert d.max() <= 1 and (d != 0).sum() <= max(2, d.size // 2000), (K, C, shape, border, d.max(), (d != 0).sum())
 
 
 @pytest.mark.parametrize("C", [1, 3])
@@ -107,7 +108,7 @@ def test_mfma_sepconv_asymmetric(m, rng, C, K):
     got = m.ops.sep_conv2d(torch.from_numpy(img).cuda(), h, v).cpu().numpy()
     ref = m.ops.sep_conv2d(img, h, v)
     d = np.abs(got.astype(int) - ref.astype(int))
-    assert d.max() <= 1 and (d == 0).mean() > 0.99, (d.max(), (d == 0).mean())
+    assert d.max() <= 1 and (d != 0).sum() <= max(2, d.size // 2000), (d.max(), (d != 0).sum())
 
 
 def test_mfma_sep_matches_general_conv(m, rng):
@@ -136,7 +137,7 @@ def test_mfma_general_conv(m, rng, K, C, shape):
         got = m.ops.conv2d(torch.from_numpy(img).cuda(), w, border).cpu().numpy()
         ref = m.ops.conv2d(img, w, border)
         d = np.abs(got.astype(int) - ref.astype(int))
-        assert d.max() <= 1 and (d == 0).mean() > 0.99, (K, C, shape, border, d.max(), (d == 0).mean())
+        assert d.max() <= 1 and (d != 0).sum() <= max(2, d.size // 2000), (K, C, shape, border, d.max(), (d != 0).sum())
 
 
 def test_mfma_conv_asymmetric_weights(m, rng):

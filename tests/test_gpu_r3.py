@@ -34,7 +34,9 @@ def test_run_to_host_matches_golden(m, chain, chunks):
     shape = (H, W, info["cout"]) if info["cout"] > 1 else (H, W)
     host = torch.empty(int(np.prod(shape)), dtype=torch.uint8, pin_memory=True)
     ref = m._C.golden_apply(m._C.synth_rows(4, W, Cc, 0, H), chain, "reflect101", True)
-    for _ in range(2):  # the step leaves its input in place: the same frame twice
+    for _ in range(2):  # single-pass chains leave the input in place; multi-pass ones consume it
+        if len(info["passes"]) > 1:
+            e.load_synthetic(4)
         host.zero_()
         e.run_to_host_ptr(host.data_ptr(), chunks)
         e.synchronize()
