@@ -301,204 +301,228 @@ def main():
     max_rows = max(r for _, r in part)
     ws_max = max_rows * W * (pinfo["cin"] + pinfo["cout"])  # the same on every rank
 
-    # ---- resident scope, Infinity-Cache cold: rotate over enough stripe
-    # copies that each step's input was last touched > 256 MiB ago ----
     scopes = {"resident": {"mpx_s": round(mpx, 1), "ms": round(ms_per_step, 5), "verified": verify}}
-    cold_steps = a.steps if a.cold_steps < 0 else a.cold_steps
-    nrot = int(math.ceil(2 * MALL_BYTES / max(1, ws_max))) + 1
-    if cold_steps > 0 and ws_max <= MALL_BYTES and iterable and nrot <= 8:
-        engines = [dp] + [parallel.DistributedPipeline(ctx, pipe, W, H, Cc) for _ in range(nrot - 1)]
-        for e in engines[1:]:
-            e.engine.set_tuning(dp.engine.bands, dp.engine.caps)
-        for e in engines:
-            e.load_synthetic(a.seed)
-        ramp()
-        for i in range(2 * nrot):  # warm: every copy once
-            engines[i % nrot].run(1)
-        for e in engines:
-            e.synchronize()
-        sync()
-        barrier()
-        t0 = time.perf_counter()
-        for i in range(cold_steps):
-            engines[i % nrot].run(1)
-        for e in engines:
-            e.synchronize()
-        sync()
-        barrier()
-        cms = max_over_ranks((time.perf_counter() - t0) * 1e3) / cold_steps
-        scopes["resident_cold"] = {"mpx_s": round(W * H / (cms * 1e-3) / 1e6, 1), "ms": round(cms, 5),
-                                   "stripe_copies": nrot, "halo_every_step": True}
-        del engines
-    elif cold_steps > 0 and ws_max > MALL_BYTES:
-        scopes["resident_cold"] = {"same_as": "resident",
-                                   "note": f"per-GPU working set {ws_max} B exceeds the 256 MiB Infinity Cache"}
 
-    # ---- dist scopes (root frame -> scatter -> filter -> gather -> root) ----
-    dist_chunks = 0
-    if a.dist_steps > 0:
-        dd = parallel.DistributedPipeline(ctx, pipe, W, H, Cc, root_buffers=True)
-        dd.engine.set_tuning(dp.engine.bands, dp.engine.caps)
-        if rank == 0:
-            dd.engine.load_root_synthetic(a.seed)
-        dd.synchronize()
+    def guarded(name, fn):
+        """run one extra scope; an exception is reported in the record (after every
+        rank agrees the scope failed) instead of ending the run without the
+        headline line"""
+        ok, err = True, None
+        try:
+            fn()
+        except Exception as e:  # noqa: BLE001
+            ok, err = False, f"{type(e).__name__}: {e}"
+            log.error("scope %s failed: %s", name, err)
+        if not all_ok(ok):
+            scopes.setdefault(name, {})["error"] = err or "failed on another rank"
 
-        def verify_root(d, cuts):
-            if rank != 0:
-                return all_ok(True)
-            full = d.engine.store_root()
-            return all_ok(check_frame_rows(lambda lo, hi: full[lo:hi], cuts))
-
-        def time_dist(d, step):
+    def scope_cold():
+        # ---- resident scope, Infinity-Cache cold: rotate over enough stripe
+        # copies that each step's input was last touched > 256 MiB ago ----
+        cold_steps = a.steps if a.cold_steps < 0 else a.cold_steps
+        nrot = int(math.ceil(2 * MALL_BYTES / max(1, ws_max))) + 1
+        if cold_steps > 0 and ws_max <= MALL_BYTES and iterable and nrot <= 8:
+            engines = [dp] + [parallel.DistributedPipeline(ctx, pipe, W, H, Cc) for _ in range(nrot - 1)]
+            for e in engines[1:]:
+                e.engine.set_tuning(dp.engine.bands, dp.engine.caps)
+            for e in engines:
+                e.load_synthetic(a.seed)
             ramp()
-            for _ in range(2):
-                step()
-            d.synchronize()
+            for i in range(2 * nrot):  # warm: every copy once
+                engines[i % nrot].run(1)
+            for e in engines:
+                e.synchronize()
             sync()
             barrier()
             t0 = time.perf_counter()
-            for _ in range(a.dist_steps):
-                step()
-            d.synchronize()
+            for i in range(cold_steps):
+                engines[i % nrot].run(1)
+            for e in engines:
+                e.synchronize()
             sync()
             barrier()
-            dms = max_over_ranks((time.perf_counter() - t0) * 1e3) / a.dist_steps
-            return dms
+            cms = max_over_ranks((time.perf_counter() - t0) * 1e3) / cold_steps
+            scopes["resident_cold"] = {"mpx_s": round(W * H / (cms * 1e-3) / 1e6, 1), "ms": round(cms, 5),
+                                       "stripe_copies": nrot, "halo_every_step": True}
+            del engines
+        elif cold_steps > 0 and ws_max > MALL_BYTES:
+            scopes["resident_cold"] = {"same_as": "resident",
+                                       "note": f"per-GPU working set {ws_max} B exceeds the 256 MiB Infinity Cache"}
 
-        def seq_step():
-            dd.scatter()
-            dd.run(1)
-            dd.gather()
+    def scope_dist():
+        # ---- dist scopes (root frame -> scatter -> filter -> gather -> root) ----
+        dist_chunks = 0
+        if a.dist_steps > 0:
+            dd = parallel.DistributedPipeline(ctx, pipe, W, H, Cc, root_buffers=True)
+            dd.engine.set_tuning(dp.engine.bands, dp.engine.caps)
+            if rank == 0:
+                dd.engine.load_root_synthetic(a.seed)
+            dd.synchronize()
 
-        cuts = [r0 for r0, r in part[1:active]]
-        seq_step()
-        dd.synchronize()
-        ok = verify_root(dd, cuts) if not a.no_verify else None
-        dms = time_dist(dd, seq_step)
-        scopes["dist_sequential"] = {"mpx_s": round(W * H / (dms * 1e-3) / 1e6, 1), "ms": round(dms, 5),
-                                     "verified": ok}
-        stages["dist_sequential"] = {k: round(v, 4) for k, v in dd.stage_times().items()
-                                     if k in ("scatter", "compute", "halo", "gather")}
-        # (device ranks only: host comms run each grouped call synchronously)
-        dist_chunks = dd.engine.dist_chunks(8) if dev else 0
-        direct = dev and world == 1 and dd.engine.dist_direct
-        if dist_chunks > 0 or direct:
-            name = "dist_direct" if direct else "dist_pipelined"
-            dd.engine.run_dist(8)
+            def verify_root(d, cuts):
+                if rank != 0:
+                    return all_ok(True)
+                full = d.engine.store_root()
+                return all_ok(check_frame_rows(lambda lo, hi: full[lo:hi], cuts))
+
+            def time_dist(d, step):
+                ramp()
+                for _ in range(2):
+                    step()
+                d.synchronize()
+                sync()
+                barrier()
+                t0 = time.perf_counter()
+                for _ in range(a.dist_steps):
+                    step()
+                d.synchronize()
+                sync()
+                barrier()
+                dms = max_over_ranks((time.perf_counter() - t0) * 1e3) / a.dist_steps
+                return dms
+
+            def seq_step():
+                dd.scatter()
+                dd.run(1)
+                dd.gather()
+
+            cuts = [r0 for r0, r in part[1:active]]
+            seq_step()
             dd.synchronize()
             ok = verify_root(dd, cuts) if not a.no_verify else None
-            dms = time_dist(dd, lambda: dd.engine.run_dist(8))
-            scopes[name] = {"mpx_s": round(W * H / (dms * 1e-3) / 1e6, 1), "ms": round(dms, 5), "verified": ok,
-                            "chunks": dist_chunks, "rows": [r for _, r in part]}
-            stages[name] = {k: round(v, 4) for k, v in dd.stage_times().items()
-                            if k in ("scatter", "compute", "gather")}
-        del dd
-        # link-aware weighted split: the root keeps the share that balances its
-        # in-place filter against each peer link's transfer time
-        if world > 1 and dev and pinfo["passes"] and len(pinfo["passes"]) == 1:
-            link = C.probe_link_rate(ctx.comm, ctx.local_rank, 64 << 20, 3)  # bytes/ms per link, one way
-            rows_per_ms = rows / step_ms["median"] if step_ms else 1.0
-            # bytes / ms the root's HBM sustains: the faster of a copy and this filter
-            hbm = step_bytes / min(copy_ms, step_ms["median"]) if copy_ms and step_ms else 1.0
-            rows_per_ms, link, hbm = from_root([rows_per_ms, link, hbm])
-            plan = C.plan_dist_split(H, world, W * pinfo["cin"], W * pinfo["cout"], rows_per_ms, rows_per_ms,
-                                     link, hbm, 8, R)
-            dw = parallel.DistributedPipeline(ctx, pipe, W, H, Cc, root_buffers=True, row_weights=plan["weights"])
-            if dw.engine.dist_chunks(8) > 0:
-                dw.engine.set_tuning(dp.engine.bands, dp.engine.caps)
+            dms = time_dist(dd, seq_step)
+            scopes["dist_sequential"] = {"mpx_s": round(W * H / (dms * 1e-3) / 1e6, 1), "ms": round(dms, 5),
+                                         "verified": ok}
+            stages["dist_sequential"] = {k: round(v, 4) for k, v in dd.stage_times().items()
+                                         if k in ("scatter", "compute", "halo", "gather")}
+            # (device ranks only: host comms run each grouped call synchronously)
+            dist_chunks = dd.engine.dist_chunks(8) if dev else 0
+            direct = dev and world == 1 and dd.engine.dist_direct
+            if dist_chunks > 0 or direct:
+                name = "dist_direct" if direct else "dist_pipelined"
+                dd.engine.run_dist(8)
+                dd.synchronize()
+                ok = verify_root(dd, cuts) if not a.no_verify else None
+                dms = time_dist(dd, lambda: dd.engine.run_dist(8))
+                scopes[name] = {"mpx_s": round(W * H / (dms * 1e-3) / 1e6, 1), "ms": round(dms, 5), "verified": ok,
+                                "chunks": dist_chunks, "rows": [r for _, r in part]}
+                stages[name] = {k: round(v, 4) for k, v in dd.stage_times().items()
+                                if k in ("scatter", "compute", "gather")}
+            del dd
+            # link-aware weighted split: the root keeps the share that balances its
+            # in-place filter against each peer link's transfer time
+            if world > 1 and dev and pinfo["passes"] and len(pinfo["passes"]) == 1:
+                link = C.probe_link_rate(ctx.comm, ctx.local_rank, 64 << 20, 3)  # bytes/ms per link, one way
+                rows_per_ms = rows / step_ms["median"] if step_ms else 1.0
+                # bytes / ms the root's HBM sustains: the faster of a copy and this filter
+                hbm = step_bytes / min(copy_ms, step_ms["median"]) if copy_ms and step_ms else 1.0
+                rows_per_ms, link, hbm = from_root([rows_per_ms, link, hbm])
+                plan = C.plan_dist_split(H, world, W * pinfo["cin"], W * pinfo["cout"], rows_per_ms, rows_per_ms,
+                                         link, hbm, 8, R)
+                dw = parallel.DistributedPipeline(ctx, pipe, W, H, Cc, root_buffers=True, row_weights=plan["weights"])
+                if dw.engine.dist_chunks(8) > 0:
+                    dw.engine.set_tuning(dp.engine.bands, dp.engine.caps)
+                    if rank == 0:
+                        dw.engine.load_root_synthetic(a.seed)
+                    dw.engine.run_dist(8)
+                    dw.synchronize()
+                    wcuts = list(np.cumsum(plan["rows"])[:-1])
+                    ok = verify_root(dw, [int(c) for c in wcuts]) if not a.no_verify else None
+                    dms = time_dist(dw, lambda: dw.engine.run_dist(8))
+                    scopes["dist_weighted"] = {
+                        "mpx_s": round(W * H / (dms * 1e-3) / 1e6, 1), "ms": round(dms, 5), "verified": ok,
+                        "rows": plan["rows"], "link_gb_s": round(link * 1e3 / 1e9, 2),
+                        "model": {k: round(plan[k], 5) for k in ("root_ms", "peer_ms", "floor_ms", "predicted_ms",
+                                                                 "even_ms")}}
+                    stages["dist_weighted"] = {k: round(v, 4) for k, v in dw.stage_times().items()
+                                               if k in ("scatter", "compute", "gather")}
+                del dw
+
+    def scope_ref():
+        # ---- reference window: filter + D2H + gather into rank 0's host memory
+        # (kernel.cu:190-226).  Every rank downloads its stripe, chunk by chunk as
+        # it is filtered, into its slice of one host frame shared with rank 0
+        # (POSIX shared memory, page-locked in every process: each GPU's own PCIe
+        # link carries its stripe, and no host copy follows). ----
+        if a.ref_steps > 0 and dev:
+            from multiprocessing import shared_memory
+
+            nbytes = H * W * pinfo["cout"]
+            shm = None
+            if world > 1 or a.ref_shm:
+                names = [f"stripe_refwin_{os.getpid()}" if rank == 0 else None]
+                dist.broadcast_object_list(names, src=0)
                 if rank == 0:
-                    dw.engine.load_root_synthetic(a.seed)
-                dw.engine.run_dist(8)
-                dw.synchronize()
-                wcuts = list(np.cumsum(plan["rows"])[:-1])
-                ok = verify_root(dw, [int(c) for c in wcuts]) if not a.no_verify else None
-                dms = time_dist(dw, lambda: dw.engine.run_dist(8))
-                scopes["dist_weighted"] = {
-                    "mpx_s": round(W * H / (dms * 1e-3) / 1e6, 1), "ms": round(dms, 5), "verified": ok,
-                    "rows": plan["rows"], "link_gb_s": round(link * 1e3 / 1e9, 2),
-                    "model": {k: round(plan[k], 5) for k in ("root_ms", "peer_ms", "floor_ms", "predicted_ms",
-                                                             "even_ms")}}
-                stages["dist_weighted"] = {k: round(v, 4) for k, v in dw.stage_times().items()
-                                           if k in ("scatter", "compute", "gather")}
-            del dw
-
-    # ---- reference window: filter + D2H + gather into rank 0's host memory
-    # (kernel.cu:190-226).  Every rank downloads its stripe, chunk by chunk as
-    # it is filtered, into its slice of one host frame shared with rank 0
-    # (POSIX shared memory, page-locked in every process: each GPU's own PCIe
-    # link carries its stripe, and no host copy follows). ----
-    if a.ref_steps > 0 and dev:
-        from multiprocessing import shared_memory
-
-        nbytes = H * W * pinfo["cout"]
-        shm = None
-        if world > 1 or a.ref_shm:
-            names = [f"stripe_refwin_{os.getpid()}" if rank == 0 else None]
-            dist.broadcast_object_list(names, src=0)
-            if rank == 0:
-                shm = shared_memory.SharedMemory(name=names[0], create=True, size=nbytes)
-            barrier()
-            if rank != 0:
-                shm = shared_memory.SharedMemory(name=names[0])
-            frame = np.ndarray((nbytes,), dtype=np.uint8, buffer=shm.buf)
-        else:
-            frame_t = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)  # keeps the pages alive
-            frame = frame_t.numpy()
-        base = frame.ctypes.data
-        pinned = shm is None or C.host_register(base, nbytes)
-        mine = base + row0 * W * pinfo["cout"]
-        dp.load_synthetic(a.seed)
-        dp.synchronize()
-        dp.engine.run_to_host_ptr(mine, 8)
-        dp.synchronize()
-        barrier()
-        ok = None
-        full = None
-        if not a.no_verify:
-            full = frame.reshape(H, W, -1) if pinfo["cout"] > 1 else frame.reshape(H, W)
-            ok = all_ok(rank != 0 or check_frame_rows(lambda lo, hi: full[lo:hi], [r0 for r0, _ in part[1:active]]))
-        ramp()
-        dp.engine.run_to_host_ptr(mine, 8)
-        dp.synchronize()
-        sync()
-        barrier()
-        t0 = time.perf_counter()
-        for _ in range(a.ref_steps):
+                    shm = shared_memory.SharedMemory(name=names[0], create=True, size=nbytes)
+                barrier()
+                if rank != 0:
+                    shm = shared_memory.SharedMemory(name=names[0])
+                frame = np.ndarray((nbytes,), dtype=np.uint8, buffer=shm.buf)
+            else:
+                frame_t = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)  # keeps the pages alive
+                frame = frame_t.numpy()
+            base = frame.ctypes.data
+            pinned = shm is None or C.host_register(base, nbytes)
+            mine = base + row0 * W * pinfo["cout"]
+            dp.load_synthetic(a.seed)
+            dp.synchronize()
             dp.engine.run_to_host_ptr(mine, 8)
             dp.synchronize()
-            barrier()  # rank 0's window ends when every stripe is in its memory
-        rms = max_over_ranks((time.perf_counter() - t0) * 1e3) / a.ref_steps
-        scopes["ref_window"] = {"mpx_s": round(W * H / (rms * 1e-3) / 1e6, 1), "ms": round(rms, 5), "verified": ok,
-                                "host_frame": "shared memory" if shm is not None else "pinned", "pinned": bool(pinned)}
-        stages["ref_window"] = {k: round(v, 4) for k, v in dp.stage_times().items() if k in ("compute", "d2h", "e2e")}
-        if shm is not None:
-            if pinned:
-                C.host_unregister(base)
-            del frame, full
             barrier()
-            shm.close()
-            if rank == 0:
-                shm.unlink()
+            ok = None
+            full = None
+            if not a.no_verify:
+                full = frame.reshape(H, W, -1) if pinfo["cout"] > 1 else frame.reshape(H, W)
+                ok = all_ok(rank != 0 or check_frame_rows(lambda lo, hi: full[lo:hi], [r0 for r0, _ in part[1:active]]))
+            ramp()
+            dp.engine.run_to_host_ptr(mine, 8)
+            dp.synchronize()
+            sync()
+            barrier()
+            t0 = time.perf_counter()
+            for _ in range(a.ref_steps):
+                dp.engine.run_to_host_ptr(mine, 8)
+                dp.synchronize()
+                barrier()  # rank 0's window ends when every stripe is in its memory
+            rms = max_over_ranks((time.perf_counter() - t0) * 1e3) / a.ref_steps
+            scopes["ref_window"] = {"mpx_s": round(W * H / (rms * 1e-3) / 1e6, 1), "ms": round(rms, 5), "verified": ok,
+                                    "host_frame": "shared memory" if shm is not None else "pinned", "pinned": bool(pinned)}
+            stages["ref_window"] = {k: round(v, 4) for k, v in dp.stage_times().items() if k in ("compute", "d2h", "e2e")}
+            if shm is not None:
+                if pinned:
+                    C.host_unregister(base)
+                del frame, full
+                barrier()
+                shm.close()
+                if rank == 0:
+                    shm.unlink()
 
-    # ---- e2e scope (pinned host stripe -> H2D -> filter -> D2H -> pinned host) ----
-    if a.e2e_steps > 0 and dev:
-        ramp()
-        eng = dp.engine
-        eng.alloc_host_io()
-        if rows > 0:
-            eng.host_input()[...] = C.synth_rows(a.seed, W, Cc, row0, rows)
-        eng.run_e2e(8)
-        eng.synchronize()
-        barrier()
-        t0 = time.perf_counter()
-        for _ in range(a.e2e_steps):
+    def scope_e2e():
+        # ---- e2e scope (pinned host stripe -> H2D -> filter -> D2H -> pinned host) ----
+        if a.e2e_steps > 0 and dev:
+            ramp()
+            eng = dp.engine
+            eng.alloc_host_io()
+            if rows > 0:
+                eng.host_input()[...] = C.synth_rows(a.seed, W, Cc, row0, rows)
             eng.run_e2e(8)
-        eng.synchronize()
-        barrier()
-        ems = max_over_ranks((time.perf_counter() - t0) * 1e3) / a.e2e_steps
-        scopes["e2e"] = {"mpx_s": round(W * H / (ems * 1e-3) / 1e6, 1), "ms": round(ems, 5)}
-        stages["e2e"] = {k: round(v, 4) for k, v in dp.stage_times().items()
-                         if k in ("h2d", "compute", "halo", "d2h", "e2e")}
+            eng.synchronize()
+            barrier()
+            t0 = time.perf_counter()
+            for _ in range(a.e2e_steps):
+                eng.run_e2e(8)
+            eng.synchronize()
+            barrier()
+            ems = max_over_ranks((time.perf_counter() - t0) * 1e3) / a.e2e_steps
+            scopes["e2e"] = {"mpx_s": round(W * H / (ems * 1e-3) / 1e6, 1), "ms": round(ems, 5)}
+            stages["e2e"] = {k: round(v, 4) for k, v in dp.stage_times().items()
+                             if k in ("h2d", "compute", "halo", "d2h", "e2e")}
+
+    for name, fn, on in (("resident_cold", scope_cold, True), ("dist", scope_dist, a.dist_steps > 0),
+                         ("ref_window", scope_ref, a.ref_steps > 0 and dev),
+                         ("e2e", scope_e2e, a.e2e_steps > 0 and dev)):
+        if on:
+            guarded(name, fn)
 
     if rank == 0:
         med = step_ms["median"] if step_ms else None
