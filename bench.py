@@ -451,7 +451,8 @@ def main():
             shm = None
             if world > 1 or a.ref_shm:
                 names = [f"stripe_refwin_{os.getpid()}" if rank == 0 else None]
-                dist.broadcast_object_list(names, src=0)
+                if world > 1:
+                    dist.broadcast_object_list(names, src=0)
                 if rank == 0:
                     shm = shared_memory.SharedMemory(name=names[0], create=True, size=nbytes)
                 barrier()
