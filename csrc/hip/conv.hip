@@ -277,7 +277,9 @@ void k_conv_mfma(ConvArgs ca) {
 constexpr int kQPS = 96;  // i8 plane row bytes (>= kCWin)
 
 template <int C>
-constexpr int convq_mt() { return C == 3 ? 2 : 4; }
+// m-tiles (16 output rows) per wave: measured 16K conv:31, RGB 2 / 3: 2.059 /
+// 2.037 ms (4 spills), gray 4 / 6 / 8: 0.771 / 0.683 / 0.717 ms
+constexpr int convq_mt() { return C == 3 ? 3 : 6; }
 
 template <int C, int MT>
 __host__ __device__ constexpr int convq_rows_staged(int nq) {
@@ -640,9 +642,24 @@ void launch_conv_mfma(const Pass& p, const PassConsts& pc, const PassLaunch& L, 
     ci.nq = conv_quads(p.K);
     ci.scale = pc.conv_scale;
     ci.bias = pc.conv_bias;
-    const int mt = p.cmid == 3 ? dev::convq_mt<3>() : dev::convq_mt<1>();
-    const int rows_in = p.cmid == 3 ? dev::convq_rows_staged<3, dev::convq_mt<3>()>(ci.nq)
-                                    : dev::convq_rows_staged<1, dev::convq_mt<1>()>(ci.nq);
+    // m-tiles per wave (STRIPE_CONV_MT overrides for A/B runs)
+    static const int env_mt = [] {
+      const char* e = std::getenv("STRIPE_CONV_MT");
+      return e ? std::atoi(e) : 0;
+    }();
+    int mt = p.cmid == 3 ? dev::convq_mt<3>() : dev::convq_mt<1>();
+    if (env_mt > 0) mt = env_mt;
+    using KFn = void (*)(dev::ConvI8Args);
+    KFn fn = nullptr;
+    int rows_in = 0;
+#define STRIPE_CONVQ(CC, MM)                                         \
+    if (p.cmid == CC && mt == MM) {                                  \
+      fn = dev::k_conv_i8<CC, MM>;                                   \
+      rows_in = dev::convq_rows_staged<CC, MM>(ci.nq);               \
+    }
+    STRIPE_CONVQ(3, 2) STRIPE_CONVQ(3, 3) STRIPE_CONVQ(1, 4) STRIPE_CONVQ(1, 6) STRIPE_CONVQ(1, 8)
+#undef STRIPE_CONVQ
+    STRIPE_CHECK(fn != nullptr, "no i8 conv kernel for " << p.cmid << " channels x " << mt << " m-tiles");
     const size_t lds = std::max((size_t)p.cmid * rows_in * dev::kQPS,  // planes
                                 (size_t)16 * mt * (dev::kCTN * p.cmid + 16));  // output tile
     for (int r = 0; r < L.nrange; ++r) {
@@ -651,8 +668,7 @@ void launch_conv_mfma(const Pass& p, const PassConsts& pc, const PassLaunch& L, 
       a.ry0 = y0;
       a.ry1 = y1;
       const dim3 grid((unsigned)div_up(L.W, dev::kCTN), (unsigned)div_up(y1 - y0, 16 * mt));
-      if (p.cmid == 3) dev::k_conv_i8<3, dev::convq_mt<3>()><<<grid, 256, lds, s>>>(ci);
-      else dev::k_conv_i8<1, dev::convq_mt<1>()><<<grid, 256, lds, s>>>(ci);
+      fn<<<grid, 256, lds, s>>>(ci);
       HIP_CHECK(hipGetLastError());
     }
     return;
