@@ -278,8 +278,9 @@ constexpr int kQPS = 96;  // i8 plane row bytes (>= kCWin)
 
 template <int C>
 // m-tiles (16 output rows) per wave: measured 16K conv:31, RGB 2 / 3: 2.059 /
-// 2.037 ms (4 spills), gray 4 / 6 / 8: 0.771 / 0.683 / 0.717 ms
-constexpr int convq_mt() { return C == 3 ? 3 : 6; }
+// 2.037 ms on one box, 2.145-2.165 / 2.186-2.191 on another (4 spills: the
+// 3-occupancy MT = 2 stays), gray 4 / 6 / 8: 0.771 / 0.683 / 0.717 ms
+constexpr int convq_mt() { return C == 3 ? 2 : 6; }
 
 template <int C, int MT>
 __host__ __device__ constexpr int convq_rows_staged(int nq) {
