@@ -102,9 +102,9 @@ __device__ __forceinline__ uint32_t bytes_to_h2(uint32_t d, uint32_t sel) {
 // product is unchanged; for RGB a lane ends with 4 consecutive pixels of one
 // output row in each channel accumulator, i.e. 12 contiguous interleaved
 // bytes: one dwordx3 store.
-template <int C>
+template <int C, int NX_>
 struct PlGeom {
-  static constexpr int NX = C == 3 ? 2 : 8;          // 16-pixel x-tiles per strip
+  static constexpr int NX = NX_;                     // 16-pixel x-tiles per strip
   static constexpr int PX = 16 * NX;                 // output pixels per strip
   static constexpr int WPX = PX + 48;                // staged pixels per row: [sx - 16, sx + PX + 32)
   static constexpr int UB = C == 3 ? 12 : 16;        // bytes per staging load (4 RGB / 16 gray pixels)
@@ -125,9 +125,10 @@ struct PlGeom {
 
 // EDGE: the row width is not a multiple of 4 pixels (the last group of a row
 // is partial: byte stores); otherwise every group is whole or past the row.
-template <int C, bool EDGE>
-__global__ __launch_bounds__(kSepWaves * 64, 2) void k_blur_pl(SepArgs sa) {
-  using G = PlGeom<C>;
+// NX x-tiles per strip, PFD 32-row pairs prefetched ahead, OCC waves per SIMD.
+template <int C, bool EDGE, int NX_, int PFD, int OCC>
+__global__ __launch_bounds__(kSepWaves * 64, OCC) void k_blur_pl(SepArgs sa) {
+  using G = PlGeom<C, NX_>;
   constexpr int NX = G::NX;
   const KArgs& a = sa.a;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -194,10 +195,11 @@ __global__ __launch_bounds__(kSepWaves * 64, 2) void k_blur_pl(SepArgs sa) {
   auto unit_ok = [&](int i) __attribute__((always_inline)) { return srow[i % P] + RSTEP * (i / P) < 32; };
   typedef uint32_t u3 __attribute__((ext_vector_type(3)));
   typedef std::conditional_t<C == 3, u3, u4> unit_t;
-  unit_t pf[G::LPL];
+  unit_t pf[PFD][G::LPL];
   const int yh0 = base - 16;               // input row of X row 0
   const int ngroups = (ye - base + 31) >> 5;
-  auto prefetch = [&](int k) __attribute__((always_inline)) {
+  auto prefetch = [&](int k, auto buf_c) __attribute__((always_inline)) {
+    constexpr int B = decltype(buf_c)::value;
     const int yt = yh0 + 32 * k;
     const bool inner = yt >= lo_ok && yt + 31 <= hi_ok;
 #pragma unroll
@@ -207,18 +209,19 @@ __global__ __launch_bounds__(kSepWaves * 64, 2) void k_blur_pl(SepArgs sa) {
       const uint32_t roff = inner ? a.in_org + (uint32_t)((int64_t)y * a.in_pitch)
                                   : in_row_off(a, min(max(y, -R), a.rows - 1 + R));
       const uint32_t off = unit_ok(i) ? roff + (uint32_t)((sx - 16 + scol[i % P]) * C) : kOOB;
-      if constexpr (C == 3) pf[i] = __builtin_amdgcn_raw_buffer_load_b96(rin, off, 0, 0);
-      else pf[i] = __builtin_amdgcn_raw_buffer_load_b128(rin, off, 0, 0);
+      if constexpr (C == 3) pf[B][i] = __builtin_amdgcn_raw_buffer_load_b96(rin, off, 0, 0);
+      else pf[B][i] = __builtin_amdgcn_raw_buffer_load_b128(rin, off, 0, 0);
     }
   };
-  auto stage = [&]() __attribute__((always_inline)) {
+  auto stage = [&](auto buf_c) __attribute__((always_inline)) {
+    constexpr int B = decltype(buf_c)::value;
 #pragma unroll
     for (int i = 0; i < G::LPL; ++i) {
       if (!unit_ok(i)) continue;  // idle lanes of the last load (lane-divergent, LDS only)
       const int dst = (srow[i % P] + RSTEP * (i / P)) * G::STRIDE + 2 * scol[i % P];
       if constexpr (C == 3) {
         // bytes R0 G0 B0 R1 | G1 B1 R2 G2 | B2 R3 G3 B3 -> three planes of 4 f16
-        const uint32_t d0 = pf[i].x, d1 = pf[i].y, d2 = pf[i].z;
+        const uint32_t d0 = pf[B][i].x, d1 = pf[B][i].y, d2 = pf[B][i].z;
         const uint32_t p01 = __builtin_amdgcn_perm(d1, d0, 0x04010300u);  // R0 R1 G0 G1
         const uint32_t p12 = __builtin_amdgcn_perm(d2, d1, 0x06030502u);  // R2 R3 G2 G3
         const uint32_t pb = __builtin_amdgcn_perm(d2, d1, 0x07040401u);   // B1 B2 -- B3 (byte 2 unused)
@@ -230,7 +233,7 @@ __global__ __launch_bounds__(kSepWaves * 64, 2) void k_blur_pl(SepArgs sa) {
         *reinterpret_cast<u2*>(wl + G::PLANE + dst) = u2{g01, g23};
         *reinterpret_cast<u2*>(wl + 2 * G::PLANE + dst) = u2{b01, b23};
       } else {
-        const u4 d = pf[i];
+        const u4 d = pf[B][i];
         u4 lo, hi;
         lo.x = bytes_to_h2(d.x, 0x04010400u);
         lo.y = bytes_to_h2(d.x, 0x04030402u);
@@ -256,11 +259,12 @@ __global__ __launch_bounds__(kSepWaves * 64, 2) void k_blur_pl(SepArgs sa) {
     colok[i] = npx[i] == 4 ? 0u : kOOB;
   }
   f4 acc[C][NX][2];  // running vertical sums of the current output group
-  auto step = [&](auto fin_c, auto start_c, int k) __attribute__((always_inline)) {
+  auto step = [&](auto fin_c, auto start_c, auto buf_c, int k) __attribute__((always_inline)) {
     constexpr bool FIN = decltype(fin_c)::value, START = decltype(start_c)::value;
-    stage();
+    stage(buf_c);
     sep_lds_sync();
-    if (START) prefetch(k + 1);  // pair k + 1 exists iff group k does
+    // pair k + PFD exists iff group k + PFD - 1 does (pairs 0 .. ngroups)
+    if (START && k + PFD <= ngroups) prefetch(k + PFD, buf_c);
     const int yg = base + 32 * (k - 1);  // first row of the group being finished
     uint32_t rowoff[2];
     if constexpr (FIN) {
@@ -373,10 +377,29 @@ __global__ __launch_bounds__(kSepWaves * 64, 2) void k_blur_pl(SepArgs sa) {
   };
   using T_ = std::integral_constant<bool, true>;
   using F_ = std::integral_constant<bool, false>;
-  prefetch(0);
-  step(F_{}, T_{}, 0);
-  for (int k = 1; k < ngroups; ++k) step(T_{}, T_{}, k);
-  step(T_{}, F_{}, ngroups);
+  using B0 = std::integral_constant<int, 0>;
+  using B1 = std::integral_constant<int, PFD - 1>;  // the other prefetch buffer (PFD 2)
+  prefetch(0, B0{});
+  if constexpr (PFD == 1) {
+    step(F_{}, T_{}, B0{}, 0);
+    for (int k = 1; k < ngroups; ++k) step(T_{}, T_{}, B0{}, k);
+    step(T_{}, F_{}, B0{}, ngroups);
+  } else {
+    prefetch(1, B1{});  // pair 1 exists: ngroups >= 1
+    // pair k sits in buffer k & 1 (static: the loop runs pairs of steps)
+    step(F_{}, T_{}, B0{}, 0);
+    int k = 1;
+    for (; k + 1 < ngroups; k += 2) {
+      step(T_{}, T_{}, B1{}, k);
+      step(T_{}, T_{}, B0{}, k + 1);
+    }
+    if (k < ngroups) {  // odd k
+      step(T_{}, T_{}, B1{}, k);
+      ++k;
+    }
+    if (k & 1) step(T_{}, F_{}, B1{}, k);
+    else step(T_{}, F_{}, B0{}, k);
+  }
 }
 
 }  // namespace dev
@@ -472,8 +495,25 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
   sa.tw = reinterpret_cast<const dev::u4*>(pc.conv);
   sa.R = p.R;
   sa.L = 16 * p.cmid;
-  const int spx = p.cmid == 3 ? dev::PlGeom<3>::PX : dev::PlGeom<1>::PX;
-  sa.nstrips = (int)div_up(L.W, spx);
+  // kernel configuration: x-tiles per strip, pairs prefetched ahead, waves per
+  // SIMD.  Measured on 16K frames (profiles/r3/blur/kbench.txt): RGB is best at
+  // 2 tiles / 1 pair / 2 waves (0.566 ms; 4 or 6 tiles at 1 wave with 2 pairs in
+  // flight: 0.586 / 0.649 ms); gray at 16 tiles / 2 pairs / 1 wave (0.213 ms
+  // against 0.234 ms at 8 / 1 / 2).  The W % 4 != 0 variant of the wide gray
+  // strip spills SGPRs (so does an 8-tile one), so edge frames take 4 tiles.
+  struct Cfg {
+    int nx, occ;
+    void (*fn)(dev::SepArgs);
+    size_t tile;
+  };
+#define STRIPE_BLUR_CFG(CC, EDGE, NX, PFD, OCC) \
+  Cfg { NX, OCC, dev::k_blur_pl<CC, EDGE, NX, PFD, OCC>, (size_t)dev::PlGeom<CC, NX>::TILE }
+  static const Cfg cfgs[2][2] = {{STRIPE_BLUR_CFG(1, false, 16, 2, 1), STRIPE_BLUR_CFG(1, true, 4, 1, 2)},
+                                 {STRIPE_BLUR_CFG(3, false, 2, 1, 2), STRIPE_BLUR_CFG(3, true, 2, 1, 2)}};
+#undef STRIPE_BLUR_CFG
+  const bool edge = L.W % 4 != 0;
+  const Cfg& cf = cfgs[p.cmid == 3][edge];
+  sa.nstrips = (int)div_up(L.W, 16 * cf.nx);
 
   const int n0 = std::max(0, L.ry[1] - L.ry[0]);
   const int n1 = L.nrange > 1 ? std::max(0, L.ry[3] - L.ry[2]) : 0;
@@ -489,7 +529,7 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
     // 3072 tasks on 2048 slots: a half-empty second round.)
     // L.band (rows, >= 32) overrides for tuning.
     const int64_t g0 = div_up(n0 + 31, 32), g1 = n1 ? div_up(n1 + 31, 32) : 0;  // groups incl. grid offset
-    const int64_t slots = 2 * resident_simds();
+    const int64_t slots = (int64_t)cf.occ * resident_simds();
     int64_t gpb = 1, best = -1;
     for (int64_t c = 1; c <= 64; ++c) {
       const int64_t tasks = (int64_t)sa.nstrips * (div_up(g0, c) + div_up(g1, c));
@@ -514,12 +554,8 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
     a.nb0 = (int)div_up(a.ry1 - sa.a0, band);
     a.nbands = a.nb0 + (n1 ? (int)div_up(a.ry3 - sa.a2, band) : 0);
     const dim3 grid((unsigned)div_up((int64_t)sa.nstrips * a.nbands, dev::kSepWaves));
-    const size_t lds =
-        (size_t)dev::kSepWaves * (p.cmid == 3 ? dev::PlGeom<3>::TILE : dev::PlGeom<1>::TILE);
-    const bool edge = L.W % 4 != 0;
-    void (*fn)(dev::SepArgs) = p.cmid == 3 ? (edge ? dev::k_blur_pl<3, true> : dev::k_blur_pl<3, false>)
-                                           : (edge ? dev::k_blur_pl<1, true> : dev::k_blur_pl<1, false>);
-    fn<<<grid, dev::kSepWaves * 64, lds, s>>>(sa);
+    const size_t lds = (size_t)dev::kSepWaves * cf.tile;
+    cf.fn<<<grid, dev::kSepWaves * 64, lds, s>>>(sa);
     HIP_CHECK(hipGetLastError());
   }
   if (p.out_margin_px > 0)

@@ -40,13 +40,14 @@ def test_no_scratch_no_vgpr_spills(report):
 
 def test_hot_kernels_have_occupancy(report):
     # streaming stencils need >= 4 waves/SIMD to keep rows in flight; the MFMA
-    # blur runs 2 waves/SIMD by design (one computes while the other loads)
+    # blur runs 2 waves/SIMD (one computes while the other loads) or, for the
+    # wide gray strip, 1 wave/SIMD with two 32-row pairs prefetched (PFD = 2)
     for k, v in report.items():
         occ = v.get("Occupancy [waves/SIMD]", 0)
         if "k_sep" in k or "k_direct" in k:
             assert occ >= 3, (k, occ)
         elif "k_blur_pl" in k:
-            assert occ >= 2, (k, occ)
+            assert occ >= (1 if k.endswith("Li2ELi1EEEvNS0_7SepArgsE") else 2), (k, occ)
 
 
 def test_headline_kernel_clean(report):
