@@ -132,7 +132,7 @@ __global__ __launch_bounds__(kSepWaves * 64, OCC) void k_blur_pl(SepArgs sa) {
   constexpr int NX = G::NX;
   const KArgs& a = sa.a;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int task = xcd_remap((int)blockIdx.x, (int)gridDim.x, a.nxcd) * kSepWaves + wave;
   if (task >= sa.nstrips * a.nbands) return;  // wave-uniform
   uint8_t* wl = lds + wave * G::TILE;
@@ -198,19 +198,33 @@ __global__ __launch_bounds__(kSepWaves * 64, OCC) void k_blur_pl(SepArgs sa) {
   unit_t pf[PFD][G::LPL];
   const int yh0 = base - 16;               // input row of X row 0
   const int ngroups = (ye - base + 31) >> 5;
-  auto prefetch = [&](int k, auto buf_c) __attribute__((always_inline)) {
-    constexpr int B = decltype(buf_c)::value;
-    const int yt = yh0 + 32 * k;
-    const bool inner = yt >= lo_ok && yt + 31 <= hi_ok;
+  // lane part of an interior load's offset: row srow * pitch + window bytes
+  uint32_t loff[P];
 #pragma unroll
-    for (int i = 0; i < G::LPL; ++i) {
-      // rows beyond the stripe + halo feed only zero weights: clamp, then border-map
-      const int y = yt + srow[i % P] + RSTEP * (i / P);
-      const uint32_t roff = inner ? a.in_org + (uint32_t)((int64_t)y * a.in_pitch)
-                                  : in_row_off(a, min(max(y, -R), a.rows - 1 + R));
-      const uint32_t off = unit_ok(i) ? roff + (uint32_t)((sx - 16 + scol[i % P]) * C) : kOOB;
-      if constexpr (C == 3) pf[B][i] = __builtin_amdgcn_raw_buffer_load_b96(rin, off, 0, 0);
-      else pf[B][i] = __builtin_amdgcn_raw_buffer_load_b128(rin, off, 0, 0);
+  for (int i = 0; i < P; ++i) loff[i] = (uint32_t)(srow[i] * a.in_pitch + (sx - 16 + scol[i]) * C);
+  auto load = [&](int i, uint32_t off, auto buf_c) __attribute__((always_inline)) {
+    constexpr int B = decltype(buf_c)::value;
+    if constexpr (C == 3) pf[B][i] = __builtin_amdgcn_raw_buffer_load_b96(rin, off, 0, 0);
+    else pf[B][i] = __builtin_amdgcn_raw_buffer_load_b128(rin, off, 0, 0);
+  };
+  auto prefetch = [&](int k, auto buf_c) __attribute__((always_inline)) {
+    const int yt = yh0 + 32 * k;
+    if (__builtin_expect(yt >= lo_ok && yt + 31 <= hi_ok, 1)) {
+      // interior pair (wave-uniform branch): one add per load
+      const uint32_t sb = a.in_org + (uint32_t)((int64_t)yt * a.in_pitch);
+#pragma unroll
+      for (int i = 0; i < G::LPL; ++i) {
+        const uint32_t off = sb + (uint32_t)(RSTEP * (i / P) * a.in_pitch) + loff[i % P];
+        load(i, unit_ok(i) ? off : kOOB, buf_c);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < G::LPL; ++i) {
+        // rows beyond the stripe + halo feed only zero weights: clamp, then border-map
+        const int y = yt + srow[i % P] + RSTEP * (i / P);
+        const uint32_t roff = in_row_off(a, min(max(y, -R), a.rows - 1 + R));
+        load(i, unit_ok(i) ? roff + (uint32_t)((sx - 16 + scol[i % P]) * C) : kOOB, buf_c);
+      }
     }
   };
   auto stage = [&](auto buf_c) __attribute__((always_inline)) {
