@@ -156,12 +156,13 @@ Plan compile_chain(const std::vector<Op>& ops, int cin, Border default_border, b
       p.K = op.K;
       p.R = op.K / 2;
       p.conv_w = op.weights;
+      p.conv_digits = op.conv_digits;
       p.sep_h = op.sep_h;
       p.sep_v = op.sep_v;
       p.cin = p.cmid = p.cout = c;
       p.desc = "conv" + std::to_string(op.K) + "x" + std::to_string(op.K) +
                (p.sep_h.empty() ? (op.K <= 5 || (op.K == 7 && c == 1) ? "(direct) " : "(mfma) ") : "(mfma-separable) ") +
-               std::to_string(c) + "ch border=" + border_name(p.border);
+               std::to_string(c) + "ch border=" + border_name(p.border) + (op.conv_digits == 2 ? " lsb" : "");
     } else {
       const StencilInfo& si = stencil_info(op.sid);
       p.kind = si.separable ? PassKind::Separable : PassKind::Direct;

@@ -239,8 +239,13 @@ std::vector<Op> parse_chain(const std::string& spec_in) {
       c.border = op.border;
       op = c;
     } else if (name == "conv") {
-      // conv:K:w00;w01;...  (K*K weights, row-major, correlation)
-      STRIPE_CHECK(parts.size() == 3, "conv syntax: conv:K:w0;w1;...;w(K*K-1)");
+      // conv:K:w00;w01;...[:exact|:lsb]  (K*K weights, row-major, correlation)
+      STRIPE_CHECK(parts.size() == 3 || parts.size() == 4, "conv syntax: conv:K:w0;w1;...;w(K*K-1)[:exact|:lsb]");
+      if (parts.size() == 4) {
+        const std::string prec = trim(parts[3]);
+        STRIPE_CHECK(prec == "exact" || prec == "lsb", "conv precision must be exact or lsb, got '" << prec << "'");
+        op.conv_digits = prec == "lsb" ? 2 : 3;
+      }
       op.kind = OpKind::Conv;
       op.K = (int)parse_num(parts[1], tok);
       STRIPE_CHECK(op.K >= 1 && op.K % 2 == 1 && op.K / 2 <= kMaxRadius, "conv K must be odd <= 33");

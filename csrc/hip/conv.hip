@@ -32,6 +32,7 @@
 // kernel.cu:64-94); this is SURVEY config 5's im2col -> MFMA path.
 #include "dev_common.h"
 #include "stripe/kernels.h"
+#include "stripe/trace.h"
 
 #include <algorithm>
 #include <cmath>
@@ -291,14 +292,15 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 struct ConvI8Args {
   KArgs a;
-  const i32x4* tw;  // B fragments: [quad][kstep 3][digit 3][lane 64]
+  const i32x4* tw;  // B fragments: [quad][kstep 3][digit ND][lane 64]
   int K, R, nq;     // kernel size, radius, 4-row quads (even)
   double scale, bias;
 };
 
-constexpr int kBQuad = 9 * 1024;  // bytes of one quad's B fragments
-
-template <int C, int MT>
+// ND weight digits: 3 (24-bit weights, the exact default) or 2 (16-bit,
+// "conv:K:w..:lsb": every output within 1 LSB of the f64 result, 2/3 of the
+// MFMAs and accumulators)
+template <int C, int MT, int ND>
 __global__ __launch_bounds__(256, 2) void k_conv_i8(ConvI8Args ca) {
   const KArgs& a = ca.a;
   const int R = ca.R, nq = ca.nq;
@@ -376,9 +378,9 @@ __global__ __launch_bounds__(256, 2) void k_conv_i8(ConvI8Args ca) {
     aoff[s] = (m + e / 3) * kQPS + 16 * (e % 3) + 16 * wave;
   }
 
-  i32x4 acc[3][C][MT];
+  i32x4 acc[ND][C][MT];
 #pragma unroll
-  for (int d = 0; d < 3; ++d)
+  for (int d = 0; d < ND; ++d)
 #pragma unroll
     for (int c = 0; c < C; ++c)
 #pragma unroll
@@ -386,14 +388,14 @@ __global__ __launch_bounds__(256, 2) void k_conv_i8(ConvI8Args ca) {
 
   // k-step stream t = 3 q + s: B(t) (3 digits) through a 3-slot register ring
   // two steps ahead, A(t + 1) read from the planes while step t multiplies
-  const __amdgpu_buffer_rsrc_t rtw = make_rsrc(ca.tw, (uint32_t)nq * (uint32_t)kBQuad);
+  const __amdgpu_buffer_rsrc_t rtw = make_rsrc(ca.tw, (uint32_t)nq * 3u * ND * 1024u);
   const uint32_t tl = 16u * (uint32_t)lane;
   const int nsteps = 3 * nq;
-  i32x4 bq[3][3];
+  i32x4 bq[3][ND];
   auto load_b = [&](int t, int slot) __attribute__((always_inline)) {
-    const uint32_t off = (uint32_t)min(t, nsteps - 1) * 3072u + tl;  // past the end: re-read (unused)
+    const uint32_t off = (uint32_t)min(t, nsteps - 1) * (ND * 1024u) + tl;  // past the end: re-read (unused)
 #pragma unroll
-    for (int dg = 0; dg < 3; ++dg)
+    for (int dg = 0; dg < ND; ++dg)
       bq[slot][dg] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(rtw, off + 1024u * dg, 0, 0));
   };
   i32x4 af[2][C][MT];
@@ -417,7 +419,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_i8(ConvI8Args ca) {
       read_a(min((q0 / 3) + (i + 1) / 3, nq - 1), (i + 1) % 3, (i + 1) & 1);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int dg = 0; dg < 3; ++dg)
+      for (int dg = 0; dg < ND; ++dg)
 #pragma unroll
         for (int c = 0; c < C; ++c)
 #pragma unroll
@@ -444,9 +446,8 @@ __global__ __launch_bounds__(256, 2) void k_conv_i8(ConvI8Args ca) {
         // scales are powers of two; the three f32 FMAs round the result to
         // ~2^-15 (an output changes only within ~1e-4 of a tie), and
         // v_cvt_pk_u8_f32 rounds half to even and saturates
-        const float v = __builtin_fmaf((float)acc[2][c][mt][r], s2,
-                                       __builtin_fmaf((float)acc[1][c][mt][r], s1,
-                                                      __builtin_fmaf((float)acc[0][c][mt][r], s0, bias)));
+        const float lo2 = __builtin_fmaf((float)acc[1][c][mt][r], s1, __builtin_fmaf((float)acc[0][c][mt][r], s0, bias));
+        const float v = ND == 3 ? __builtin_fmaf((float)acc[ND - 1][c][mt][r], s2, lo2) : lo2;
         otile[(16 * mt + 4 * g + r) * kOS + (16 * wave + m) * C + c] = (uint8_t)__builtin_amdgcn_cvt_pk_u8_f32(v, 0, 0u);
       }
   __syncthreads();
@@ -510,18 +511,44 @@ static int conv_quads(int K) {
 // kernel row 4 q + (4 s + g) / 3, window pixel px = 16 ((4 s + g) mod 3) + j,
 // B[k][n] = digit d of W[ky][px - n - (16 - R)] (the window starts 16 pixels
 // left of the tile).
+// Fixed-point exponent S of an ND-digit weight set (max|W| <= 2^(8 ND - 1) - 2^(8 ND - 9) - 1).
+static int conv_shift(const std::vector<float>& w, int ND) {
+  const int64_t wmax = ND == 3 ? (1 << 23) - (1 << 15) : (1 << 15) - (1 << 7);
+  double maxw = 0;
+  for (float x : w) maxw = std::max(maxw, std::fabs((double)x));
+  return maxw > 0 ? (int)std::floor(std::log2((double)(wmax - 1) / maxw)) : 0;
+}
+
+// Largest output error (in LSB) of ND-digit weights: |x - 128| <= 128 times
+// the summed quantisation residuals (the digit sums themselves are exact).
+static double conv_quant_bound(const std::vector<float>& w, int ND) {
+  const int S = conv_shift(w, ND);
+  double r = 0;
+  for (float x : w) {
+    const double v = std::ldexp((double)x, S);
+    r += std::fabs(v - (double)std::llround(v));
+  }
+  return 128.0 * std::ldexp(r, -S);
+}
+
 static void prepare_conv_i8(const Pass& p, PassConsts* pc, hipStream_t s) {
   const int K = p.K;
   STRIPE_CHECK(K >= 1 && K <= 33, "conv K=" << K << " exceeds the 48-pixel Toeplitz window");
-  double maxw = 0;
-  for (float w : p.conv_w) maxw = std::max(maxw, std::fabs((double)w));
-  int S = 0;
-  if (maxw > 0) S = (int)std::floor(std::log2((double)((1 << 23) - (1 << 15) - 1) / maxw));
+  // lsb mode keeps its promise (every output within 1 LSB: quantisation error
+  // < 0.45 LSB before the final rounding) or falls back to the exact digits
+  int ND = p.conv_digits == 2 ? 2 : 3;
+  if (ND == 2 && conv_quant_bound(p.conv_w, 2) >= 0.45) {
+    STRIPE_LOG(Info, -1, "conv" << K << " lsb: 16-bit weights could miss by " << conv_quant_bound(p.conv_w, 2)
+                                << " LSB, using 24-bit digits");
+    ND = 3;
+  }
+  const int64_t wmax = ND == 3 ? (1 << 23) - (1 << 15) : (1 << 15) - (1 << 7);
+  const int S = conv_shift(p.conv_w, ND);
   std::vector<int64_t> W((size_t)K * K);
   int64_t wsum = 0;
   for (size_t i = 0; i < W.size(); ++i) {
     W[i] = std::llround(std::ldexp((double)p.conv_w[i], S));
-    STRIPE_CHECK(std::llabs(W[i]) <= (1 << 23) - (1 << 15), "weight digit range");
+    STRIPE_CHECK(std::llabs(W[i]) <= wmax, "weight digit range");
     wsum += W[i];
   }
   auto digit = [](int64_t w, int d) {
@@ -534,10 +561,10 @@ static void prepare_conv_i8(const Pass& p, PassConsts* pc, hipStream_t s) {
     return dg;
   };
   const int nq = conv_quads(K);
-  std::vector<int8_t> host((size_t)nq * 9 * 64 * 16, 0);
+  std::vector<int8_t> host((size_t)nq * 3 * ND * 64 * 16, 0);
   for (int q = 0; q < nq; ++q)
     for (int st = 0; st < 3; ++st)
-      for (int d = 0; d < 3; ++d)
+      for (int d = 0; d < ND; ++d)
         for (int l = 0; l < 64; ++l)
           for (int j = 0; j < 16; ++j) {
             const int e = 4 * st + (l >> 4);
@@ -545,11 +572,13 @@ static void prepare_conv_i8(const Pass& p, PassConsts* pc, hipStream_t s) {
             const int ky = 4 * q + e / 3, px = 16 * (e % 3) + j, tap = px - (l & 15) - (16 - p.R);
             int8_t v = 0;
             if (ky < K && tap >= 0 && tap < K) v = digit(W[(size_t)ky * K + tap], d);
-            host[((((size_t)q * 3 + st) * 3 + d) * 64 + l) * 16 + j] = v;
+            host[((((size_t)q * 3 + st) * ND + d) * 64 + l) * 16 + j] = v;
           }
-  // the split is exact: d0 + 256 d1 + 65536 d2 == W for every weight
-  for (int64_t w : W) STRIPE_CHECK(digit(w, 0) + 256 * (int64_t)digit(w, 1) + 65536 * (int64_t)digit(w, 2) == w, "digits");
-  pc->conv_mode = 1;
+  // the split is exact: d0 + 256 d1 (+ 65536 d2) == W for every weight
+  for (int64_t w : W)
+    STRIPE_CHECK(digit(w, 0) + 256 * (int64_t)digit(w, 1) + (ND == 3 ? 65536 * (int64_t)digit(w, 2) : 0) == w,
+                 "digits");
+  pc->conv_mode = ND == 3 ? 1 : 2;
   pc->conv_scale = std::ldexp(1.0, -S);
   pc->conv_bias = 128.0 * (double)wsum * pc->conv_scale;
   pc->conv_bytes = host.size();
@@ -564,7 +593,8 @@ void prepare_conv_consts(const Pass& p, PassConsts* pc, hipStream_t s) {
   // 3 k-steps per row pair (both padded to an even count); ties go to f16
   // (K = 9: 1.26 vs 1.41 ms on 16K RGB, the i8 kernel's epilogue and 3
   // accumulator sets cost more where the MFMA count does not drop)
-  const bool i8 = 9 * conv_quads(p.K) < 6 * conv_pairs(p.K);
+  // (the 2-digit lsb mode: 6 per quad, never more than f16)
+  const bool i8 = p.conv_digits == 2 || 9 * conv_quads(p.K) < 6 * conv_pairs(p.K);
   if (!conv_f16() && i8) return prepare_conv_i8(p, pc, s);
   const int K = p.K;
   STRIPE_CHECK(K >= 1 && K <= 33, "conv K=" << K << " exceeds the 48-pixel Toeplitz window");
@@ -616,7 +646,8 @@ void launch_conv_mfma(const Pass& p, const PassConsts& pc, const PassLaunch& L, 
                "conv launch needs the allocation view (< 2 GiB buffers)");
   STRIPE_CHECK((L.rebased || (L.in_org >= kMarginBytes && L.out_org >= kMarginBytes)) && L.in_zero >= kMarginBytes,
                "bad origin offsets");
-  if (pc.conv_mode == 1) {
+  if (pc.conv_mode == 1 || pc.conv_mode == 2) {
+    const int nd = pc.conv_mode == 2 ? 2 : 3;
     dev::ConvI8Args ci{};
     dev::KArgs& a = ci.a;
     a.in = L.in;
@@ -653,14 +684,16 @@ void launch_conv_mfma(const Pass& p, const PassConsts& pc, const PassLaunch& L, 
     using KFn = void (*)(dev::ConvI8Args);
     KFn fn = nullptr;
     int rows_in = 0;
-#define STRIPE_CONVQ(CC, MM)                                         \
-    if (p.cmid == CC && mt == MM) {                                  \
-      fn = dev::k_conv_i8<CC, MM>;                                   \
+#define STRIPE_CONVQ(CC, MM, DD)                                     \
+    if (p.cmid == CC && mt == MM && nd == DD) {                      \
+      fn = dev::k_conv_i8<CC, MM, DD>;                               \
       rows_in = dev::convq_rows_staged<CC, MM>(ci.nq);               \
     }
-    STRIPE_CONVQ(3, 2) STRIPE_CONVQ(3, 3) STRIPE_CONVQ(1, 4) STRIPE_CONVQ(1, 6) STRIPE_CONVQ(1, 8)
+    STRIPE_CONVQ(3, 2, 3) STRIPE_CONVQ(3, 3, 3) STRIPE_CONVQ(1, 4, 3) STRIPE_CONVQ(1, 6, 3) STRIPE_CONVQ(1, 8, 3)
+    STRIPE_CONVQ(3, 2, 2) STRIPE_CONVQ(3, 3, 2) STRIPE_CONVQ(1, 6, 2)
 #undef STRIPE_CONVQ
-    STRIPE_CHECK(fn != nullptr, "no i8 conv kernel for " << p.cmid << " channels x " << mt << " m-tiles");
+    STRIPE_CHECK(fn != nullptr, "no i8 conv kernel for " << p.cmid << " channels x " << mt << " m-tiles x " << nd
+                                                          << " digits");
     const size_t lds = std::max((size_t)p.cmid * rows_in * dev::kQPS,  // planes
                                 (size_t)16 * mt * (dev::kCTN * p.cmid + 16));  // output tile
     for (int r = 0; r < L.nrange; ++r) {

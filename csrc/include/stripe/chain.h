@@ -50,6 +50,7 @@ struct Pass {
   int K = 1, R = 0;
   Border border = Border::Reflect101;
   std::vector<float> conv_w;  // Conv: K*K weights
+  int conv_digits = 3;        // Conv: weight digits of the i8 MFMA path (Op::conv_digits)
   std::vector<float> sep_h, sep_v;  // Conv: 1-D factors of a rank-one window (separable MFMA path)
   // x-margin contract for the output (what the next stencil consumer needs)
   int out_margin_px = 0;

@@ -73,6 +73,10 @@ struct Op {
   int K = 0;                  // conv window
   std::vector<float> weights; // conv: K*K f32 weights
   std::vector<float> sep_h, sep_v;  // conv: 1-D factors when weights[dy][dx] = sep_v[dy] * sep_h[dx]
+  // conv precision on the MFMA path: 3 = weights as 24-bit fixed point (an
+  // output differs from the f64 result only within ~1e-4 of a rounding tie),
+  // 2 = 16-bit ("conv:K:w..:lsb", every output within 1 LSB, 2/3 of the MFMAs)
+  int conv_digits = 3;
   std::string text;           // canonical spelling
   bool has_border = false;    // per-op border override ("gaussian5@replicate")
   Border border = Border::Reflect101;

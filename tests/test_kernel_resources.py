@@ -6,6 +6,7 @@ and writes build/kernel_resources.json.  No kernel may touch scratch memory
 (register spills to scratch are a silent 2-10x slowdown on a streaming kernel).
 """
 import json
+import re
 import os
 
 import pytest
@@ -47,7 +48,9 @@ def test_hot_kernels_have_occupancy(report):
         if "k_sep" in k or "k_direct" in k:
             assert occ >= 3, (k, occ)
         elif "k_blur_pl" in k:
-            assert occ >= (1 if k.endswith("Li2ELi1EEEvNS0_7SepArgsE") else 2), (k, occ)
+            # <C, EDGE, NX, PFD = 2, OCC = 1>: one wave per SIMD by design
+            one = re.search(r"ELi2ELi1EEEvNS0_7SepArgsE$", k) is not None
+            assert occ >= (1 if one else 2), (k, occ)
 
 
 def test_headline_kernel_clean(report):

@@ -124,3 +124,49 @@ def test_gpu_blur_vs_torch(m, rng, K, Cc, border):
     r = oracle.compare(got, sums, GPU_BAND)
     assert r["mismatch_outside_ties"] == 0 and r["max_diff"] <= 1, r
     assert r["mismatch"] <= max(2, r["n"] // 2000), r
+
+
+# ------------------------------------------------------------------ lsb mode
+# conv:K:w..:lsb: 16-bit weight digits on the i8 MFMA path (2/3 of the MFMAs);
+# every output within 1 LSB of the correctly rounded f64 result (the host
+# checks the quantisation bound per weight set and falls back to 24-bit
+# digits when it cannot promise that).
+def test_conv_lsb_spec(C, rng):
+    w = _weights(rng, 9)
+    info = C.plan_info(_conv_chain(w) + ":lsb", 3)
+    assert info["passes"][0]["desc"].endswith("lsb")
+    assert "lsb" not in C.plan_info(_conv_chain(w) + ":exact", 3)["passes"][0]["desc"]
+    with pytest.raises(Exception):
+        C.plan_info(_conv_chain(w) + ":fast", 3)
+    img = _img(rng, (23, 31), 3)
+    # the golden path is exact whatever the requested precision
+    assert (C.golden_apply(img, _conv_chain(w) + ":lsb", "reflect101", True) ==
+            C.golden_apply(img, _conv_chain(w), "reflect101", True)).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K", [9, 31, 33])
+@pytest.mark.parametrize("Cc", [1, 3])
+def test_gpu_conv_lsb_vs_torch(m, rng, K, Cc):
+    img = _img(rng, (150, 333), Cc)
+    w = _weights(rng, K)
+    got = _gpu(m, img, _conv_chain(w) + ":lsb", "reflect101")
+    sums = oracle.torch_sums(img, w, "reflect101", device="cuda")
+    r = oracle.compare(got, sums, GPU_BAND)
+    print(f"conv:{K} lsb C={Cc}: {r['mismatch']} of {r['n']} outputs off by one")
+    assert r["max_diff"] <= 1, r
+    assert r["mismatch"] <= r["n"] // 50, r  # measured rate recorded in profiles/r3/conv/
+
+
+@pytest.mark.gpu
+def test_gpu_conv_lsb_falls_back_when_unsafe(m, rng):
+    # one dominant tap: 16-bit digits of the small ones could miss by >= 0.45
+    # LSB, so the pass runs on 24-bit digits and stays exact except ties
+    K = 31
+    w = rng.uniform(-1, 1, (K, K)) * 1e-3
+    w[15, 15] = 1.5
+    w = oracle.f32_weights(w)
+    img = _img(rng, (90, 200), 3)
+    got = _gpu(m, img, _conv_chain(w) + ":lsb", "reflect101")
+    r = oracle.compare(got, oracle.torch_sums(img, w, "reflect101", device="cuda"), GPU_BAND)
+    assert r["mismatch_outside_ties"] == 0 and r["mismatch"] <= max(2, r["n"] // 2000), r
