@@ -80,8 +80,10 @@ def parse():
                     help="ref-window host frame in POSIX shared memory even on one rank (tests the multi-rank path)")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-autotune", action="store_true", help="skip the per-shape band / occupancy autotune")
-    ap.add_argument("--backend", default="rccl", choices=["rccl", "host"],
-                    help="rccl: GPU engine + RCCL (the benchmark); host: CPU golden engine + gloo (plumbing tests)")
+    ap.add_argument("--backend", default="rccl", choices=["rccl", "host", "gloo-gpu"],
+                    help="rccl: GPU engine + RCCL (the benchmark); host: CPU golden engine + gloo (plumbing "
+                         "tests); gloo-gpu: GPU engine, gloo transport through pinned host memory, processes may "
+                         "share GPUs (the multi-rank device path on a one-GPU box)")
     return ap.parse_args()
 
 
@@ -126,10 +128,10 @@ def main():
     from mpi_cuda_imagemanipulation_amd.models import Pipeline
     from mpi_cuda_imagemanipulation_amd.utils.log import get_logger
 
-    ctx = parallel.init("rccl" if a.backend == "rccl" else "gloo")
+    ctx = parallel.init({"rccl": "rccl", "host": "gloo", "gloo-gpu": "gloo-gpu"}[a.backend])
     log = get_logger("bench", ctx.rank)
     dev = ctx.device
-    tdev = "cuda" if dev else "cpu"
+    tdev = "cuda" if a.backend == "rccl" else "cpu"  # the process group's tensors
 
     def sync():
         if dev:
@@ -412,7 +414,7 @@ def main():
             # link-aware weighted split: the root keeps the share that balances its
             # in-place filter against each peer link's transfer time
             if world > 1 and dev and pinfo["passes"] and len(pinfo["passes"]) == 1:
-                link = C.probe_link_rate(ctx.comm, ctx.local_rank, 64 << 20, 3)  # bytes/ms per link, one way
+                link = C.probe_link_rate(ctx.comm, ctx.gpu, 64 << 20, 3)  # bytes/ms per link, one way
                 rows_per_ms = rows / step_ms["median"] if step_ms else 1.0
                 # bytes / ms the root's HBM sustains: the faster of a copy and this filter
                 hbm = step_bytes / min(copy_ms, step_ms["median"]) if copy_ms and step_ms else 1.0
@@ -563,7 +565,7 @@ def main():
             "halo_depth": dp.engine.halo_depth,
             "stripe_rows": [r for _, r in part],
             "stage_ms_rank0": stages,
-            "device": C.device_info(ctx.local_rank) if dev else {},
+            "device": C.device_info(ctx.gpu) if dev else {},
             "build": build_info(root),
             "host": socket.gethostname(),
             "torch": torch.__version__,

@@ -59,6 +59,9 @@ class LocalHub;
 std::shared_ptr<LocalHub> make_local_hub(int world, bool device, double timeout_s = 300.0);
 std::unique_ptr<Comm> make_local_comm(const std::shared_ptr<LocalHub>& hub, int rank);
 
+// ---- device buffers over a host-buffer communicator (processes sharing GPUs) ----
+std::unique_ptr<Comm> make_staged_comm(std::unique_ptr<Comm> host_comm, int device);
+
 // ---- Python / external callbacks (host buffers) ----
 struct CallbackOps {
   std::function<void()> group_start;

@@ -310,6 +310,14 @@ PYBIND11_MODULE(_C, m) {
     return c;
   });
 
+  // the callback comm's device-buffer face: takes over `host` (left empty)
+  m.def("make_staged_comm", [](PyComm* host, int device) {
+    STRIPE_CHECK(host && host->comm, "staged comm needs a host communicator");
+    auto c = std::make_unique<PyComm>();
+    c->comm = make_staged_comm(std::move(host->comm), device);
+    return c;
+  });
+
   // ---- engine ----
   py::class_<EngineConfig>(m, "EngineConfig")
       .def(py::init<>())

@@ -4,12 +4,14 @@
 // Semantics match a grouped ncclSend/ncclRecv: sends are posted immediately,
 // group_end() completes this rank's receives, then waits for its sends to be
 // consumed (so the sender may reuse its buffer afterwards).
+#include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
 #include <deque>
 #include <map>
 #include <mutex>
+#include <vector>
 
 #include "stripe/comm.h"
 #include "stripe/kernels.h"
@@ -221,7 +223,96 @@ class CallbackComm final : public Comm {
   CallbackOps ops_;
 };
 
+// Device-buffer face of a host-buffer communicator (gloo callbacks): N
+// processes sharing GPUs run the device engine with host transport -- the
+// reference's own deployment, every MPI rank on GPU 0 (kernel.cu:147), and the
+// multi-process device path exercised on a one-GPU box.  A send copies the
+// device buffer into pinned host memory on the caller's stream first; receives
+// land in pinned memory and are copied to the device on their streams once the
+// inner group has completed.  Calls outside a group form a group of one.
+class StagedComm final : public Comm {
+ public:
+  StagedComm(std::unique_ptr<Comm> inner, int device) : inner_(std::move(inner)), device_(device) {
+    STRIPE_CHECK(!inner_->device_buffers(), "staged comm wraps a host-buffer communicator");
+  }
+  ~StagedComm() override {
+    for (auto& b : pool_) (void)hipHostFree(b.p);
+  }
+  int rank() const override { return inner_->rank(); }
+  int size() const override { return inner_->size(); }
+  const char* backend() const override { return "staged"; }
+  bool device_buffers() const override { return true; }
+  void group_start() override {
+    STRIPE_CHECK(!in_group_, "nested group_start");
+    in_group_ = true;
+    used_ = 0;
+    inner_->group_start();
+  }
+  void send(const void* buf, size_t bytes, int peer, hipStream_t s) override {
+    const bool solo = !in_group_;
+    if (solo) group_start();
+    void* h = take(bytes);
+    HIP_CHECK(hipMemcpyAsync(h, buf, bytes, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    inner_->send(h, bytes, peer, nullptr);
+    if (solo) group_end();
+  }
+  void recv(void* buf, size_t bytes, int peer, hipStream_t s) override {
+    const bool solo = !in_group_;
+    if (solo) group_start();
+    void* h = take(bytes);
+    inner_->recv(h, bytes, peer, nullptr);
+    recvs_.push_back({buf, h, bytes, s});
+    if (solo) group_end();
+  }
+  void group_end() override {
+    STRIPE_CHECK(in_group_, "group_end without group_start");
+    in_group_ = false;
+    inner_->group_end();
+    for (auto& r : recvs_) HIP_CHECK(hipMemcpyAsync(r.dst, r.host, r.bytes, hipMemcpyHostToDevice, r.s));
+    // the pinned buffers are reused by the next group: copies done first
+    for (auto& r : recvs_) HIP_CHECK(hipStreamSynchronize(r.s));
+    recvs_.clear();
+  }
+  void barrier() override { inner_->barrier(); }
+  void abort(const std::string& why) override { inner_->abort(why); }
+
+ private:
+  struct Buf {
+    void* p;
+    size_t n;
+  };
+  struct Recv {
+    void* dst;
+    void* host;
+    size_t bytes;
+    hipStream_t s;
+  };
+  void* take(size_t bytes) {
+    if (used_ == pool_.size()) pool_.push_back({nullptr, 0});
+    Buf& b = pool_[used_++];
+    if (b.n < bytes) {
+      if (b.p) HIP_CHECK(hipHostFree(b.p));
+      b.p = nullptr;
+      HIP_CHECK(hipSetDevice(device_));
+      HIP_CHECK(hipHostMalloc(&b.p, std::max<size_t>(bytes, 1)));
+      b.n = bytes;
+    }
+    return b.p;
+  }
+  std::unique_ptr<Comm> inner_;
+  int device_;
+  bool in_group_ = false;
+  size_t used_ = 0;
+  std::vector<Buf> pool_;
+  std::vector<Recv> recvs_;
+};
+
 }  // namespace
+
+std::unique_ptr<Comm> make_staged_comm(std::unique_ptr<Comm> host_comm, int device) {
+  return std::make_unique<StagedComm>(std::move(host_comm), device);
+}
 
 std::shared_ptr<LocalHub> make_local_hub(int world, bool device, double timeout_s) {
   STRIPE_CHECK(world >= 1, "world must be >= 1");

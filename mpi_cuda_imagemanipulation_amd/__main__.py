@@ -38,9 +38,10 @@ def main(argv=None) -> int:
     r.add_argument("--chain", default=None)
     r.add_argument("--preset", default=None, choices=sorted(models.PRESETS))
     r.add_argument("--ranks", type=int, default=1)
-    r.add_argument("--backend", default="auto", choices=["auto", "local", "host", "rccl", "gloo"],
+    r.add_argument("--backend", default="auto", choices=["auto", "local", "host", "rccl", "gloo", "gloo-gpu"],
                    help="local: N logical ranks on this process's GPU; host: CPU golden engine; "
-                        "rccl / gloo: one process per rank under torchrun (RANK / WORLD_SIZE env)")
+                        "rccl / gloo / gloo-gpu: one process per rank under torchrun (RANK / WORLD_SIZE env; "
+                        "gloo-gpu: GPU engines sharing GPUs, gloo transport through pinned host memory)")
     r.add_argument("--border", default=None)
     r.add_argument("--iterations", type=int, default=1)
     r.add_argument("--dist-chunks", type=int, default=0,
@@ -73,7 +74,7 @@ def main(argv=None) -> int:
         import os
 
         os.environ["STRIPE_LOG"] = "INFO"
-    if a.backend in ("rccl", "gloo"):
+    if a.backend in ("rccl", "gloo", "gloo-gpu"):
         return _run_per_process(a, pipe)
     img = utils.read_image(a.input)
     backend = a.backend

@@ -37,8 +37,10 @@ class DistContext:
     rank: int
     world: int
     local_rank: int
-    device: bool          # True: GPU engine + RCCL; False: host engine + gloo
+    device: bool          # True: GPU engine (RCCL, or gloo staged through host); False: host engine + gloo
     comm: object          # native Comm handle (None when world == 1)
+    gpu: int = -1         # device index of this rank's engine (-1: host engine)
+    transport: str = ""   # rccl | gloo | gloo-gpu
 
 
 def plan_rows(H: int, world: int, min_rows: int = 1, legacy: bool = False):
@@ -85,37 +87,47 @@ class GlooComm:
 def init(backend: str = "auto") -> DistContext:
     """Initialise from torchrun-style env (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_*).
 
-    backend: 'rccl' (GPU engine, RCCL comm), 'gloo' (host engine), or 'auto'.
+    backend: 'rccl' (GPU engine, RCCL comm), 'gloo' (host engine),
+    'gloo-gpu' (GPU engine, gloo transport staged through pinned host memory:
+    processes may share GPUs -- rank r on GPU r mod count -- like the
+    reference's MPI ranks all on GPU 0, kernel.cu:147), or 'auto'.
     """
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
     if backend == "auto":
         backend = "rccl" if (torch is not None and torch.cuda.is_available()) else "gloo"
-    device = backend == "rccl"
+    if backend not in ("rccl", "gloo", "gloo-gpu"):
+        raise ValueError(f"unknown backend {backend!r} (rccl | gloo | gloo-gpu | auto)")
+    device = backend != "gloo"
+    gpu = -1
+    if device:
+        gpu = local_rank if backend == "rccl" else local_rank % max(1, torch.cuda.device_count())
     log = get_logger("parallel", rank)
     log.info("init: rank %d of %d, local rank %d, backend %s", rank, world, local_rank, backend)
     if device:
-        torch.cuda.set_device(local_rank)
+        torch.cuda.set_device(gpu)
     comm = None
     if device and world == 1:
         # a one-rank RCCL communicator: no traffic, but the same comm object,
         # bounded waits and barrier as the multi-rank path (exercised on 1-GPU boxes)
-        comm = C.make_rccl_comm(C.rccl_unique_id(), 0, 1, local_rank)
+        comm = C.make_rccl_comm(C.rccl_unique_id(), 0, 1, gpu)
     if world > 1:
         if not dist.is_initialized():
             # the process-group timeout follows the native collective bound
             # (STRIPE_COMM_TIMEOUT_S): a dead peer surfaces as an error, not a hang
-            dist.init_process_group("nccl" if device else "gloo", rank=rank, world_size=world,
+            dist.init_process_group("nccl" if backend == "rccl" else "gloo", rank=rank, world_size=world,
                                     timeout=datetime.timedelta(seconds=C.comm_timeout_s()))
-        if device:
+        if backend == "rccl":
             uid = [C.rccl_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
-            comm = C.make_rccl_comm(uid[0], rank, world, local_rank)
+            comm = C.make_rccl_comm(uid[0], rank, world, gpu)
+        elif backend == "gloo-gpu":
+            comm = C.make_staged_comm(GlooComm().native(rank, world), gpu)
         else:
             comm = GlooComm().native(rank, world)
-    log.info("communicator ready (%s)", "rccl" if device else ("gloo" if world > 1 else "none"))
-    return DistContext(rank, world, local_rank, device, comm)
+    log.info("communicator ready (%s)", backend if world > 1 else ("rccl" if device else "none"))
+    return DistContext(rank, world, local_rank, device, comm, gpu, backend)
 
 
 class DistributedPipeline:
@@ -125,7 +137,7 @@ class DistributedPipeline:
                  autotune: bool = False, row_weights=None):
         self.ctx = ctx
         cfg = pipeline.config(W, H, Cc, "device" if ctx.device else "host",
-                              device=ctx.local_rank if ctx.device else -1, autotune=autotune, row_weights=row_weights)
+                              device=ctx.gpu if ctx.device else -1, autotune=autotune, row_weights=row_weights)
         cfg.root_buffers = root_buffers
         self.engine = C.Engine(cfg, ctx.comm)
         self.W, self.H, self.C = W, H, Cc
@@ -193,7 +205,7 @@ def probe_link_rate(ctx: DistContext, nbytes: int = 64 << 20, reps: int = 3) -> 
     (every rank must call it; 0 on one rank)."""
     if ctx.comm is None or ctx.world == 1:
         return 0.0
-    return C.probe_link_rate(ctx.comm, ctx.local_rank if ctx.device else -1, nbytes, reps)
+    return C.probe_link_rate(ctx.comm, ctx.gpu if ctx.device else -1, nbytes, reps)
 
 
 __all__ = ["DistContext", "GlooComm", "init", "DistributedPipeline", "plan_rows", "plan_rows_weighted", "dist_split",

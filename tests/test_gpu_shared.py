@@ -1,0 +1,80 @@
+"""The multi-process DEVICE path on a one-GPU box (gloo-gpu backend).
+
+The driver's scaling runs use one process per GPU over RCCL; a one-GPU box
+cannot host that (RCCL refuses two ranks on one device), so the same
+per-process device flow -- DistributedPipeline, scatter / halo exchange /
+gather, the pipelined and weighted dist steps, the reference window into a
+shared-memory frame, the cache-cold scope, bench.py's verification -- runs here
+with N processes sharing GPU 0 and gloo moving the bytes through pinned host
+memory (StagedComm).  This is also the reference's own deployment: every MPI
+rank on GPU 0 (kernel.cu:147).
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _torchrun(n, args, tmp_path, timeout=300):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), *args]
+    env = dict(os.environ, OMP_NUM_THREADS="2", PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout, cwd=str(tmp_path))
+    assert r.returncode == 0, (r.stdout + r.stderr)[-6000:]
+    return [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_bench_gloo_gpu_processes(tmp_path, n):
+    recs = _torchrun(n, [os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--backend", "gloo-gpu",
+                         "--width", "2048", "--height", "1536", "--steps", "6", "--warmup", "2",
+                         "--dist-steps", "2", "--ref-steps", "2", "--e2e-steps", "2"], tmp_path)
+    assert len(recs) == 1
+    rec = recs[0]
+    assert rec["n_gpus"] == n and rec["value"] > 0 and rec["verified_vs_golden"] is True
+    assert sum(rec["stripe_rows"]) == 1536
+    for name, sc in rec["scopes"].items():
+        assert "error" not in sc, (name, sc)
+        if "verified" in sc:
+            assert sc["verified"] is True, (name, sc)
+
+
+@pytest.mark.parametrize("extra", [["--dist-chunks", "4"], ["--preset", "ref-gpu"],
+                                   ["--dist-chunks", "2", "--row-weights", "0.5,0.2,0.2,0.1"]])
+def test_cli_gloo_gpu_4_processes(tmp_path, C, extra):
+    import mpi_cuda_imagemanipulation_amd as m
+
+    img = m.utils.synthetic_image(11, 301, 203, 3)
+    src, out = tmp_path / "in.ppm", tmp_path / "out.ppm"
+    m.utils.write_image(str(src), img)
+    args = ["-m", "mpi_cuda_imagemanipulation_amd", "run", "--input", str(src), "--output", str(out),
+            "--backend", "gloo-gpu", *extra]
+    if "--preset" not in extra:
+        args += ["--chain", "gaussian5"]
+    recs = _torchrun(4, args, tmp_path)
+    assert len(recs) == 1 and recs[0]["ranks"] == 4
+    got = m.utils.read_image(str(out))
+    if "--preset" in extra:
+        import np_ref
+
+        rows = 203 // 4
+        for r in range(4):
+            s = img[r * rows:(r + 1) * rows]
+            e = np_ref.stencil(np_ref.contrast_ref(np_ref.gray_ref(s), 3.5), "emboss3", "skip")
+            assert (got[r * rows:(r + 1) * rows] == np_ref.expand(e)).all(), r
+    else:
+        assert (got == C.golden_apply(img, "gaussian5", "reflect101", True)).all()
