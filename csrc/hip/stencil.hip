@@ -138,6 +138,7 @@ void launch_stencil(const Pass& p, const PassConsts& pc, const PassLaunch& L, hi
   for (int c = 0; c < 3; ++c) {
     a.gmul[c] = gp.mult[c];
     a.gshift[c] = gp.shift[c];
+    STRIPE_CHECK(gp.mult[c] < (1u << 24), "gray multiplier exceeds 24 bits");
   }
   STRIPE_CHECK(p.cmid == 1 || p.cmid == 3, "stencil channels must be 1 or 3");
   STRIPE_CHECK(!(p.pro.gray && p.cin != 3), "gray prologue needs 3 input channels");

@@ -78,8 +78,9 @@ __device__ __forceinline__ WaveTask wave_task(const KArgs& a) {
 }
 
 enum { PRO_NONE = 0, PRO_LUT = 1, PRO_GRAY = 2, PRO_GRAYLUT = 3 };
-// PRO_GRAY: arithmetic gray (bt601 fixed point); PRO_GRAYLUT: gray:ref as three
-// per-channel table lookups (see cook_pairs).  Both read 48 RGB bytes per lane.
+// PRO_GRAY: arithmetic gray (bt601 fixed point); PRO_GRAYLUT: gray:ref (three
+// truncated per-channel terms, gray_ref_pairs) with its post LUT applied to the
+// u16 lanes directly.  Both read 48 RGB bytes per lane.
 constexpr bool is_gray(int pro) { return pro == PRO_GRAY || pro == PRO_GRAYLUT; }
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -119,12 +120,9 @@ __device__ __forceinline__ void load_raw(__amdgpu_buffer_rsrc_t rin, uint32_t ro
   }
 }
 
-// gray:ref (kernel.cu:40-42: per-channel truncated products, summed) as three
-// 256-entry LDS tables per pixel (luts + 768: R, G, B terms, built on the host
-// from the exact multiply-shift constants); the sum (<= 254) and the optional
-// post LUT land straight in the u16 fields the stencil arithmetic uses, so
-// there is no byte packing / unpacking.  ~9 VALU + 6-8 conflict-free LDS reads
-// per pixel pair instead of ~24 VALU for the arithmetic form.
+// gray:ref (kernel.cu:40-42: per-channel truncated products, summed); the
+// sum (<= 254) and the optional post LUT land straight in the u16 fields the
+// stencil arithmetic uses, so there is no byte packing / unpacking.
 template <int N>
 __device__ __forceinline__ uint32_t byte_at(const uint32_t (&d)[N], int j) {
   return (d[j >> 2] >> ((j & 3) * 8)) & 0xFFu;
@@ -132,17 +130,17 @@ __device__ __forceinline__ uint32_t byte_at(const uint32_t (&d)[N], int j) {
 
 __device__ __forceinline__ void gray_ref_pairs(const KArgs& a, const uint32_t (&d)[12], const uint8_t* luts,
                                                uint32_t (&u)[8]) {
-  const uint8_t* tr = luts + 768;
-  const uint8_t* tg = luts + 1024;
-  const uint8_t* tb = luts + 1280;
-  // all 48 term lookups first, then the sums, then (one uniform branch) the
-  // 16 post-LUT lookups: two LDS round trips per row.  (With the post-LUT
-  // test inside the per-pixel loop hipcc emitted 16 basic blocks of "3
-  // lookups, wait, add, branch, lookup": 32 dependent LDS waits per row.)
+  // the exact terms as 24-bit multiply + shift (find_trunc_magic): no LDS
+  // traffic for them.  As 48 table lookups per row they kept the LDS 65 % busy
+  // on the 16K RGB reference pipeline, half of it bank conflicts (random pixel
+  // bytes).  Then all 16 sums, then (one uniform branch) the 16 post-LUT
+  // lookups: one LDS round trip per row.
   uint32_t g[16];
+  const uint32_t m0 = a.gmul[0] & 0xFFFFFFu, m1 = a.gmul[1] & 0xFFFFFFu, m2 = a.gmul[2] & 0xFFFFFFu;
 #pragma unroll
   for (int px = 0; px < 16; ++px)
-    g[px] = (uint32_t)tr[byte_at(d, 3 * px)] + (uint32_t)tg[byte_at(d, 3 * px + 1)] + (uint32_t)tb[byte_at(d, 3 * px + 2)];
+    g[px] = ((byte_at(d, 3 * px) * m0) >> a.gshift[0]) + ((byte_at(d, 3 * px + 1) * m1) >> a.gshift[1]) +
+            ((byte_at(d, 3 * px + 2) * m2) >> a.gshift[2]);
   if (a.has_post) {
 #pragma unroll
     for (int px = 0; px < 16; ++px) g[px] = luts[256 + g[px]];
@@ -181,7 +179,7 @@ __device__ __forceinline__ void load_chunk(const KArgs& a, __amdgpu_buffer_rsrc_
 
 template <int PRO>
 __device__ __forceinline__ void load_luts(const KArgs& a, uint8_t* lds) {
-  for (int i = threadIdx.x; i < (PRO == PRO_GRAYLUT ? kLutBytes : 768); i += kNT) lds[i] = a.luts[i];
+  for (int i = threadIdx.x; i < 768; i += kNT) lds[i] = a.luts[i];
 }
 
 // Legacy skip border (kernel.cu:83 interior-only bounds): bytes of pixels in the
@@ -475,7 +473,7 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : (SKIP && EXP ? 3 : 4))) void 
   constexpr int CIN = is_gray(PRO) ? 3 : 1;  // input bytes per output byte
   using T = SepTraits<F>;
   __shared__ __attribute__((aligned(16))) uint4 xbuf[EXP ? kWaves : 1][EXP ? 3 * kW : 1];
-  __shared__ uint8_t luts[PRO == PRO_GRAYLUT ? kLutBytes : 768];
+  __shared__ uint8_t luts[768];
   if (PRO != PRO_NONE || a.has_epi) {
     load_luts<PRO>(a, luts);
     __syncthreads();
@@ -694,7 +692,7 @@ __global__ __launch_bounds__(kNT, (F::K >= 5 ? 3 : 4)) void k_direct(KArgs a) {
   constexpr int NX = (R * C + 1) / 2;  // neighbour dwords per side
   constexpr int NE = 8 + 2 * NX;       // extended row dwords
   constexpr int CIN = is_gray(PRO) ? 3 : 1;
-  __shared__ uint8_t luts[PRO == PRO_GRAYLUT ? kLutBytes : 768];
+  __shared__ uint8_t luts[768];
   if (PRO != PRO_NONE || a.has_epi) {
     load_luts<PRO>(a, luts);
     __syncthreads();

@@ -24,8 +24,9 @@ namespace stripe {
   } while (0)
 
 // Device-resident per-pass constants, built once by the engine.
-// Per-pass LUT block: [pre 256 | post 256 | epi 256 | gray:ref R, G, B terms 3 x 256].
-constexpr int kLutBytes = 1536;
+// Per-pass LUT block: [pre 256 | post 256 | epi 256] (the gray:ref terms are
+// computed by multiply-shift in the kernels).
+constexpr int kLutBytes = 768;
 
 struct PassConsts {
   uint8_t* luts = nullptr;   // kLutBytes, layout above

@@ -135,14 +135,10 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
   for (size_t i = 0; i < plan_.passes.size(); ++i) {
     const Pass& p = plan_.passes[i];
     std::vector<uint8_t> l(kLutBytes);
-    // per-channel gray:ref terms trunc(v * w_c) (kernel.cu:40-42): the stencil
-    // kernels' gray:ref prologue sums three table lookups per pixel
-    const GrayParams gp = gray_params(GrayMode::Ref);
     for (int v = 0; v < 256; ++v) {
       l[v] = p.pro.has_pre ? p.pro.pre[v] : (uint8_t)v;
       l[256 + v] = p.pro.has_post ? p.pro.post[v] : (uint8_t)v;
       l[512 + v] = p.has_epi ? p.epi[v] : (uint8_t)v;
-      for (int c = 0; c < 3; ++c) l[768 + 256 * c + v] = (uint8_t)(((uint32_t)v * gp.mult[c]) >> gp.shift[c]);
     }
     prt_[i].luts = Buffer(kLutBytes, device());
     if (device()) {
