@@ -1,7 +1,7 @@
 #!/bin/bash
 # DB blur kernel (STRIPE_BLUR_DB=1/2) and conv lsb mode: GPU tests, then timings
 set -o pipefail
-bash tools/r3_blur_db.sh || exit 1
+bash tools/ab/r3/r3_blur_db.sh || exit 1
 timeout -k 10 300 python -u -m pytest tests/test_oracle_conv.py -m gpu -q -s --timeout 120 --timeout-method thread -p no:cacheprovider -k "lsb" > gpurun_out/r3_lsb_tests.txt 2>&1 || { tail -30 gpurun_out/r3_lsb_tests.txt; exit 1; }
 grep -E "off by one|passed|failed" gpurun_out/r3_lsb_tests.txt
 W=$(python3 -c "print(';'.join(str(((7*i)%13-4)/400) for i in range(961)))")
