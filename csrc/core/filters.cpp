@@ -169,6 +169,16 @@ static Op make_conv_blur(int K, double sigma, const std::string& text) {
   return op;
 }
 
+// Trailing ":exact" / ":lsb" of a float conv token (removed from parts):
+// 3 = exact (the default), 2 = every output within 1 LSB of the f64 result.
+static int take_precision(std::vector<std::string>& parts) {
+  if (parts.size() < 2) return 3;
+  const std::string last = trim(parts.back());
+  if (last != "exact" && last != "lsb") return 3;
+  parts.pop_back();
+  return last == "lsb" ? 2 : 3;
+}
+
 std::vector<Op> parse_chain(const std::string& spec_in) {
   const std::string spec = trim(spec_in);
   std::vector<Op> ops;
@@ -232,11 +242,15 @@ std::vector<Op> parse_chain(const std::string& spec_in) {
       op.kind = OpKind::Expand;
       op.text = "expand";
     } else if (name == "blur" || name == "gblur") {
+      // blur:K[:sigma][:exact|:lsb]
+      const int digits = take_precision(parts);
+      STRIPE_CHECK(parts.size() <= 3, "blur syntax: blur:K[:sigma][:exact|:lsb]");
       const int K = parts.size() > 1 ? (int)parse_num(parts[1], tok) : 31;
       const double sigma = parts.size() > 2 ? parse_num(parts[2], tok) : 0.0;
       Op c = make_conv_blur(K, sigma, tok);
       c.has_border = op.has_border;
       c.border = op.border;
+      c.conv_digits = digits;
       op = c;
     } else if (name == "conv") {
       // conv:K:w00;w01;...[:exact|:lsb]  (K*K weights, row-major, correlation)
@@ -254,9 +268,10 @@ std::vector<Op> parse_chain(const std::string& spec_in) {
                    "conv:" << op.K << " needs " << op.K * op.K << " weights, got " << op.weights.size());
       op.text = tok;
     } else if (name == "sepconv") {
-      // sepconv:K:h0;...;h(K-1):v0;...;v(K-1)  rank-one KxK correlation
+      // sepconv:K:h0;...;h(K-1):v0;...;v(K-1)[:exact|:lsb]  rank-one KxK correlation
       // weights[dy][dx] = v[dy] * h[dx] (separable MFMA path on the GPU)
-      STRIPE_CHECK(parts.size() == 4, "sepconv syntax: sepconv:K:h0;...;h(K-1):v0;...;v(K-1)");
+      op.conv_digits = take_precision(parts);
+      STRIPE_CHECK(parts.size() == 4, "sepconv syntax: sepconv:K:h0;...;h(K-1):v0;...;v(K-1)[:exact|:lsb]");
       op.kind = OpKind::Conv;
       op.K = (int)parse_num(parts[1], tok);
       STRIPE_CHECK(op.K >= 1 && op.K % 2 == 1 && op.K / 2 <= kMaxRadius, "sepconv K must be odd <= 33");

@@ -31,7 +31,9 @@
 // framework, SURVEY §2 "large-kernel conv".
 #include "dev_common.h"
 #include "stripe/kernels.h"
+#include "stripe/trace.h"
 
+#include <cmath>
 #include <cstdlib>
 #include <type_traits>
 #include <vector>
@@ -53,6 +55,7 @@ struct SepArgs {
   const u4* tw;  // [entry][lane] weight fragments (8 halves each)
   int R, L, nstrips;
   int a0, a2;  // group-grid origins of ranges 0 / 1 (global row multiple of 32)
+  float bias;  // LSB mode: 128 * sum(h) * sum(v), the x - 128 shift of the input
 };
 
 __device__ __forceinline__ void sep_lds_sync() {
@@ -84,11 +87,20 @@ __device__ __forceinline__ uint32_t pack_u8x4(f4 v) {
   return o;
 }
 
-// 4 input bytes -> 4 exact f16 (two dwords): (1024 + b) built by byte permute, minus 1024.
+// 2 input bytes -> 2 exact f16 (one dword): (1024 + b) built by byte permute,
+// minus 1024 (b), or minus 1152 (b - 128, the centred input of the LSB mode).
+template <bool CENTRED = false>
 __device__ __forceinline__ uint32_t bytes_to_h2(uint32_t d, uint32_t sel) {
   const uint32_t biased = __builtin_amdgcn_perm(0x64646464u, d, sel);
   half2v h = __builtin_bit_cast(half2v, biased);
-  h = h - half2v{(_Float16)1024.0f, (_Float16)1024.0f};
+  constexpr _Float16 k = CENTRED ? (_Float16)1152.0f : (_Float16)1024.0f;
+  h = h - half2v{k, k};
+  return __builtin_bit_cast(uint32_t, h);
+}
+
+// 2 f32 -> 2 f16, round to nearest even (the LSB mode's single-part X).
+__device__ __forceinline__ uint32_t f32x2_to_h2(float x, float y) {
+  const half2v h = {(_Float16)x, (_Float16)y};
   return __builtin_bit_cast(uint32_t, h);
 }
 
@@ -126,7 +138,12 @@ struct PlGeom {
 // EDGE: the row width is not a multiple of 4 pixels (the last group of a row
 // is partial: byte stores); otherwise every group is whole or past the row.
 // NX x-tiles per strip, PFD 32-row pairs prefetched ahead, OCC waves per SIMD.
-template <int C, bool EDGE, int NX_, int PFD, int OCC>
+// LSB: the "blur:K:lsb" precision mode -- input centred (x - 128, exact in
+// f16), single f16 weights and a single f16 X, the shift added back as the
+// accumulators' start value: 8 MFMAs per tile instead of 20, every output
+// within 1 LSB of the f64 result (the host bounds the error per weight set and
+// keeps the exact kernel when it cannot promise that).
+template <int C, bool EDGE, int NX_, int PFD, int OCC, bool LSB = false>
 __global__ __launch_bounds__(kSepWaves * 64, OCC) void k_blur_pl(SepArgs sa) {
   using G = PlGeom<C, NX_>;
   constexpr int NX = G::NX;
@@ -153,17 +170,18 @@ __global__ __launch_bounds__(kSepWaves * 64, OCC) void k_blur_pl(SepArgs sa) {
   const int R = sa.R;
 
   // ---- weights: Bh[s][hl] (horizontal, 2 k-steps), Bv[q][s][hl] (vertical) ----
-  half8 bh[2][2], bv[2][2][2];
+  constexpr int NHL = LSB ? 1 : 2;  // weight parts (hi, lo)
+  half8 bh[2][NHL], bv[2][2][NHL];
 #pragma unroll
   for (int s = 0; s < 2; ++s)
 #pragma unroll
-    for (int hl = 0; hl < 2; ++hl) bh[s][hl] = __builtin_bit_cast(half8, sa.tw[(s * 2 + hl) * 64 + lane]);
+    for (int hl = 0; hl < NHL; ++hl) bh[s][hl] = __builtin_bit_cast(half8, sa.tw[(s * 2 + hl) * 64 + lane]);
 #pragma unroll
   for (int q = 0; q < 2; ++q)
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int hl = 0; hl < 2; ++hl)
+      for (int hl = 0; hl < NHL; ++hl)
         bv[q][s][hl] = __builtin_bit_cast(half8, sa.tw[(4 + q * 4 + s * 2 + hl) * 64 + lane]);
 
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);
@@ -239,24 +257,24 @@ __global__ __launch_bounds__(kSepWaves * 64, OCC) void k_blur_pl(SepArgs sa) {
         const uint32_t p01 = __builtin_amdgcn_perm(d1, d0, 0x04010300u);  // R0 R1 G0 G1
         const uint32_t p12 = __builtin_amdgcn_perm(d2, d1, 0x06030502u);  // R2 R3 G2 G3
         const uint32_t pb = __builtin_amdgcn_perm(d2, d1, 0x07040401u);   // B1 B2 -- B3 (byte 2 unused)
-        const uint32_t r01 = bytes_to_h2(p01, 0x04010400u), g01 = bytes_to_h2(p01, 0x04030402u);
-        const uint32_t r23 = bytes_to_h2(p12, 0x04010400u), g23 = bytes_to_h2(p12, 0x04030402u);
-        const uint32_t b01 = bytes_to_h2(__builtin_amdgcn_perm(d0, pb, 0x00000006u), 0x04010400u);  // B0 B1
-        const uint32_t b23 = bytes_to_h2(pb, 0x04030401u);                                         // B2 B3
+        const uint32_t r01 = bytes_to_h2<LSB>(p01, 0x04010400u), g01 = bytes_to_h2<LSB>(p01, 0x04030402u);
+        const uint32_t r23 = bytes_to_h2<LSB>(p12, 0x04010400u), g23 = bytes_to_h2<LSB>(p12, 0x04030402u);
+        const uint32_t b01 = bytes_to_h2<LSB>(__builtin_amdgcn_perm(d0, pb, 0x00000006u), 0x04010400u);  // B0 B1
+        const uint32_t b23 = bytes_to_h2<LSB>(pb, 0x04030401u);                                         // B2 B3
         *reinterpret_cast<u2*>(wl + dst) = u2{r01, r23};
         *reinterpret_cast<u2*>(wl + G::PLANE + dst) = u2{g01, g23};
         *reinterpret_cast<u2*>(wl + 2 * G::PLANE + dst) = u2{b01, b23};
       } else {
         const u4 d = pf[B][i];
         u4 lo, hi;
-        lo.x = bytes_to_h2(d.x, 0x04010400u);
-        lo.y = bytes_to_h2(d.x, 0x04030402u);
-        lo.z = bytes_to_h2(d.y, 0x04010400u);
-        lo.w = bytes_to_h2(d.y, 0x04030402u);
-        hi.x = bytes_to_h2(d.z, 0x04010400u);
-        hi.y = bytes_to_h2(d.z, 0x04030402u);
-        hi.z = bytes_to_h2(d.w, 0x04010400u);
-        hi.w = bytes_to_h2(d.w, 0x04030402u);
+        lo.x = bytes_to_h2<LSB>(d.x, 0x04010400u);
+        lo.y = bytes_to_h2<LSB>(d.x, 0x04030402u);
+        lo.z = bytes_to_h2<LSB>(d.y, 0x04010400u);
+        lo.w = bytes_to_h2<LSB>(d.y, 0x04030402u);
+        hi.x = bytes_to_h2<LSB>(d.z, 0x04010400u);
+        hi.y = bytes_to_h2<LSB>(d.z, 0x04030402u);
+        hi.z = bytes_to_h2<LSB>(d.w, 0x04010400u);
+        hi.w = bytes_to_h2<LSB>(d.w, 0x04030402u);
         *reinterpret_cast<u4*>(wl + dst) = lo;
         *reinterpret_cast<u4*>(wl + dst + 16) = hi;
       }
@@ -309,7 +327,7 @@ __global__ __launch_bounds__(kSepWaves * 64, OCC) void k_blur_pl(SepArgs sa) {
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
-        for (int hl = 0; hl < 2; ++hl)
+        for (int hl = 0; hl < NHL; ++hl)
 #pragma unroll
           for (int h = 0; h < 2; ++h) x[h] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f[h][s], bh[s][hl], x[h], 0, 0, 0);
     };
@@ -319,28 +337,39 @@ __global__ __launch_bounds__(kSepWaves * 64, OCC) void k_blur_pl(SepArgs sa) {
     auto vert = [&](int t, const f4 (&x)[2]) __attribute__((always_inline)) {
       const int i = t / C, c = t % C;
       // accumulator layout -> A operand of the vertical product (k = X row, permuted)
-      uint32_t h[4], l[4];
-      split_h2(x[0][0], x[0][1], h[0], l[0]);
-      split_h2(x[0][2], x[0][3], h[1], l[1]);
-      split_h2(x[1][0], x[1][1], h[2], l[2]);
-      split_h2(x[1][2], x[1][3], h[3], l[3]);
-      const u4 uh = {h[0], h[1], h[2], h[3]}, ul = {l[0], l[1], l[2], l[3]};
-      const half8 ah = __builtin_bit_cast(half8, uh), al = __builtin_bit_cast(half8, ul);
       f4 o4[2], n4[2];
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         o4[q] = acc[c][i][q];
-        n4[q] = f4{0.f, 0.f, 0.f, 0.f};
+        n4[q] = LSB ? f4{sa.bias, sa.bias, sa.bias, sa.bias} : f4{0.f, 0.f, 0.f, 0.f};
       }
-      // four independent 3-MFMA chains, interleaved
-#pragma unroll
-      for (int st = 0; st < 3; ++st)
+      if constexpr (LSB) {
+        const u4 uh = {f32x2_to_h2(x[0][0], x[0][1]), f32x2_to_h2(x[0][2], x[0][3]), f32x2_to_h2(x[1][0], x[1][1]),
+                       f32x2_to_h2(x[1][2], x[1][3])};
+        const half8 ah = __builtin_bit_cast(half8, uh);
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-          const half8 av = st == 2 ? al : ah;
-          if constexpr (FIN) o4[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, bv[q][1][st == 1], o4[q], 0, 0, 0);
-          if constexpr (START) n4[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, bv[q][0][st == 1], n4[q], 0, 0, 0);
+          if constexpr (FIN) o4[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bv[q][1][0], o4[q], 0, 0, 0);
+          if constexpr (START) n4[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bv[q][0][0], n4[q], 0, 0, 0);
         }
+      } else {
+        uint32_t h[4], l[4];
+        split_h2(x[0][0], x[0][1], h[0], l[0]);
+        split_h2(x[0][2], x[0][3], h[1], l[1]);
+        split_h2(x[1][0], x[1][1], h[2], l[2]);
+        split_h2(x[1][2], x[1][3], h[3], l[3]);
+        const u4 uh = {h[0], h[1], h[2], h[3]}, ul = {l[0], l[1], l[2], l[3]};
+        const half8 ah = __builtin_bit_cast(half8, uh), al = __builtin_bit_cast(half8, ul);
+        // four independent 3-MFMA chains, interleaved
+#pragma unroll
+        for (int st = 0; st < 3; ++st)
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const half8 av = st == 2 ? al : ah;
+            if constexpr (FIN) o4[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, bv[q][1][st == 1], o4[q], 0, 0, 0);
+            if constexpr (START) n4[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, bv[q][0][st == 1], n4[q], 0, 0, 0);
+          }
+      }
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         if constexpr (START) acc[c][i][q] = n4[q];
@@ -431,9 +460,49 @@ bool sep_supported(const Pass& p) {
 //  Bv[q][s][hl]: X row hr = 32 s + 16 (j >> 2) + 4 g + (j & 3) (the accumulator
 //             order of the A operand), output row 16 q + n of the 32-row group:
 //             tap t = hr - 16 - 16 q - n + R.
+// Worst-case error (in output LSB) of the LSB mode for 1-D weights h, v: the
+// input is centred (|x - 128| <= 128, exact in f16), the weights are rounded
+// to f16, X to f16 (relative error <= 2^-11), products and sums in f32.
+double sep_lsb_bound(const std::vector<float>& h, const std::vector<float>& v) {
+  double sh = 0, dh = 0, sv = 0, dv = 0, svr = 0;
+  for (float w : h) {
+    sh += std::fabs((double)w);
+    dh += std::fabs((double)w - (double)(float)(_Float16)w);
+  }
+  for (float w : v) {
+    sv += std::fabs((double)w);
+    dv += std::fabs((double)w - (double)(float)(_Float16)w);
+    svr += std::fabs((double)(float)(_Float16)w);
+  }
+  const double e1 = 128.0 * dh;                 // horizontal weight rounding
+  const double xmax = 128.0 * sh + e1;          // |X| of the centred input
+  if (xmax >= 60000.0) return 1e30;             // X would leave the f16 range
+  const double e2 = xmax * std::ldexp(1.0, -11);  // X rounded to f16
+  // + f32 accumulation (K products per pass, 2^-24 each) with a margin
+  return svr * (e1 + e2) + dv * 128.0 * sh + 1e-3 + 2.0 * (double)h.size() * std::ldexp(xmax * (1.0 + sv), -24);
+}
+
 void prepare_sep_consts(const Pass& p, PassConsts* pc, hipStream_t s) {
   const int K = p.K, R = p.R;
   STRIPE_CHECK(sep_supported(p), "separable blur geometry unsupported (K=" << K << ", C=" << p.cmid << ")");
+  // precision mode: 0 = hi + lo splits (exact except ~1e-4 of a tie), 2 = LSB
+  // (single f16 parts on the centred input, every output within 1 LSB; kept
+  // only when the error bound stays < 0.45 LSB)
+  pc->conv_mode = 0;
+  if (p.conv_digits == 2) {
+    const double bound = sep_lsb_bound(p.sep_h, p.sep_v);
+    if (bound < 0.45) {
+      pc->conv_mode = 2;
+      double sh = 0, sv = 0;
+      // the shift back uses the exact weights: only the centred part carries
+      // the f16 rounding (random sign, no systematic bias)
+      for (float w : p.sep_h) sh += (double)w;
+      for (float w : p.sep_v) sv += (double)w;
+      pc->conv_bias = 128.0 * sh * sv;
+    } else {
+      STRIPE_LOG(Info, -1, "blur" << K << " lsb: f16 weights could miss by " << bound << " LSB, using hi + lo parts");
+    }
+  }
   std::vector<_Float16> host((size_t)dev::kSepEntries * 64 * 8, (_Float16)0.f);
   auto put = [&](int e, int lane, int j, float w, int hl) {
     const _Float16 whi = (_Float16)w;
@@ -520,13 +589,29 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
     void (*fn)(dev::SepArgs);
     size_t tile;
   };
-#define STRIPE_BLUR_CFG(CC, EDGE, NX, PFD, OCC) \
-  Cfg { NX, OCC, dev::k_blur_pl<CC, EDGE, NX, PFD, OCC>, (size_t)dev::PlGeom<CC, NX>::TILE }
-  static const Cfg cfgs[2][2] = {{STRIPE_BLUR_CFG(1, false, 16, 2, 1), STRIPE_BLUR_CFG(1, true, 4, 1, 2)},
-                                 {STRIPE_BLUR_CFG(3, false, 2, 1, 2), STRIPE_BLUR_CFG(3, true, 2, 1, 2)}};
-#undef STRIPE_BLUR_CFG
+#define STRIPE_BLUR_CFG(CC, EDGE, NX, PFD, OCC, LSB) \
+  Cfg { NX, OCC, dev::k_blur_pl<CC, EDGE, NX, PFD, OCC, LSB>, (size_t)dev::PlGeom<CC, NX>::TILE }
+  static const Cfg cfgs[2][2][2] = {
+      {{STRIPE_BLUR_CFG(1, false, 16, 2, 1, false), STRIPE_BLUR_CFG(1, true, 4, 1, 2, false)},
+       {STRIPE_BLUR_CFG(3, false, 2, 1, 2, false), STRIPE_BLUR_CFG(3, true, 2, 1, 2, false)}},
+      {{STRIPE_BLUR_CFG(1, false, 16, 2, 1, true), STRIPE_BLUR_CFG(1, true, 2, 1, 2, true)},
+       {STRIPE_BLUR_CFG(3, false, 2, 1, 2, true), STRIPE_BLUR_CFG(3, true, 2, 1, 2, true)}}};
   const bool edge = L.W % 4 != 0;
-  const Cfg& cf = cfgs[p.cmid == 3][edge];
+  const bool lsb = pc.conv_mode == 2;
+  sa.bias = (float)pc.conv_bias;
+  const Cfg* cfp = &cfgs[lsb][p.cmid == 3][edge];
+  // TEMPORARY A/B of LSB configurations (STRIPE_BLUR_XCFG=i)
+  static const Cfg xrgb[] = {STRIPE_BLUR_CFG(3, false, 6, 2, 1, true), STRIPE_BLUR_CFG(3, false, 4, 2, 1, true),
+                             STRIPE_BLUR_CFG(3, false, 4, 3, 1, true), STRIPE_BLUR_CFG(3, false, 5, 2, 1, true)};
+  static const Cfg xgray[] = {STRIPE_BLUR_CFG(1, false, 8, 1, 2, true), STRIPE_BLUR_CFG(1, false, 4, 1, 3, true),
+                              STRIPE_BLUR_CFG(1, false, 8, 2, 2, true), STRIPE_BLUR_CFG(1, false, 4, 2, 2, true)};
+  static const int xcfg = [] {
+    const char* e = std::getenv("STRIPE_BLUR_XCFG");
+    return e ? std::atoi(e) : -1;
+  }();
+  if (lsb && !edge && xcfg >= 0 && xcfg < 4) cfp = p.cmid == 3 ? &xrgb[xcfg] : &xgray[xcfg];
+  const Cfg& cf = *cfp;
+#undef STRIPE_BLUR_CFG
   sa.nstrips = (int)div_up(L.W, 16 * cf.nx);
 
   const int n0 = std::max(0, L.ry[1] - L.ry[0]);

@@ -170,3 +170,55 @@ def test_gpu_conv_lsb_falls_back_when_unsafe(m, rng):
     got = _gpu(m, img, _conv_chain(w) + ":lsb", "reflect101")
     r = oracle.compare(got, oracle.torch_sums(img, w, "reflect101", device="cuda"), GPU_BAND)
     assert r["mismatch_outside_ties"] == 0 and r["mismatch"] <= max(2, r["n"] // 2000), r
+
+
+# ------------------------------------------------------------- blur lsb mode
+# blur:K:lsb / sepconv:..:lsb: the separable MFMA kernel on the centred input
+# (x - 128, exact in f16) with single f16 weights and a single f16 X, the
+# shift added back exactly: 8 MFMAs per tile instead of 20.  Every output
+# within 1 LSB of the f64 result; the host bounds the error per weight set and
+# keeps the hi + lo kernel above 0.45 LSB.
+def test_blur_lsb_spec(C, rng):
+    assert C.plan_info("blur:31:lsb", 3)["passes"][0]["desc"].endswith("lsb")
+    assert C.plan_info("blur:31:4.5:lsb", 1)["passes"][0]["desc"].endswith("lsb")
+    assert "lsb" not in C.plan_info("blur:31:exact", 3)["passes"][0]["desc"]
+    assert "lsb" not in C.plan_info("blur:31", 3)["passes"][0]["desc"]
+    h = ";".join(["0.2"] * 5)
+    assert C.plan_info(f"sepconv:5:{h}:{h}:lsb", 3)["passes"][0]["desc"].endswith("lsb")
+    with pytest.raises(Exception):
+        C.plan_info("blur:31:4.5:lsb:exact", 3)
+    img = _img(rng, (23, 40), 3)
+    assert (C.golden_apply(img, "blur:15:lsb", "reflect101", True) ==
+            C.golden_apply(img, "blur:15", "reflect101", True)).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K", [9, 31, 33])
+@pytest.mark.parametrize("Cc", [1, 3])
+@pytest.mark.parametrize("W", [1100, 1101])
+def test_gpu_blur_lsb_vs_torch(m, rng, K, Cc, W):
+    img = _img(rng, (130, W), Cc)
+    got = _gpu(m, img, f"blur:{K}:lsb", "reflect101")
+    sums = oracle.torch_sums(img, oracle.blur_weights(m._C, K), "reflect101", device="cuda")
+    r = oracle.compare(got, sums, GPU_BAND)
+    print(f"blur:{K} lsb C={Cc} W={W}: {r['mismatch']} of {r['n']} outputs off by one")
+    assert r["max_diff"] <= 1, r
+    # numpy model of the mode (31x31, random pixels): 0.09 % off by one
+    assert r["mismatch"] <= r["n"] // 200, r
+
+
+@pytest.mark.gpu
+def test_gpu_sepconv_lsb_falls_back_when_unsafe(m, rng):
+    # horizontal taps summing to ~20 (X of the centred input up to ~2600,
+    # where an f16 step is 2), vertical taps summing to 1: the single-part mode
+    # could miss by > 1 LSB, so the pass keeps the hi + lo kernel
+    K = 9
+    h = rng.uniform(1.5, 3.0, K).astype(np.float32)
+    v = rng.uniform(0.5, 1.0, K)
+    v = (v / v.sum()).astype(np.float32)
+    chain = f"sepconv:{K}:" + ";".join(repr(float(x)) for x in h) + ":" + ";".join(repr(float(x)) for x in v)
+    img = (_img(rng, (90, 300), 3) % 12).astype(np.uint8)  # outputs ~20 * 6, unsaturated
+    w = np.outer(v.astype(np.float64), h.astype(np.float64)).astype(np.float32)
+    sums = oracle.torch_sums(img, w, "reflect101", device="cuda")
+    r = oracle.compare(_gpu(m, img, chain + ":lsb", "reflect101"), sums, GPU_BAND)
+    assert r["mismatch_outside_ties"] == 0 and r["mismatch"] <= max(2, r["n"] // 2000), r
