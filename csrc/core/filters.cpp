@@ -290,7 +290,7 @@ std::vector<Op> parse_chain(const std::string& spec_in) {
     } else {
       fail("unknown filter '" + name +
            "' (gray[:ref|bt601], contrast:F[:cv], invert, brightness:D, threshold:T, expand, "
-           "emboss3, emboss5, gaussian3/5/7, box3/5, sharpen, laplace, sobel, sobel_l2, blur:K[:sigma], conv:K:w.., sepconv:K:h..:v..)");
+           "emboss3, emboss5, gaussian3/5/7, box3/5, sharpen, laplace, sobel, sobel_l2, blur:K[:sigma][:lsb], conv:K:w..[:lsb], sepconv:K:h..:v..[:lsb])");
     }
     if (op.has_border) op.text += std::string("@") + border_name(op.border);
     ops.push_back(op);

@@ -584,6 +584,11 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
   // flight: 0.586 / 0.649 ms); gray at 16 tiles / 2 pairs / 1 wave (0.213 ms
   // against 0.234 ms at 8 / 1 / 2).  The W % 4 != 0 variant of the wide gray
   // strip spills SGPRs (so does an 8-tile one), so edge frames take 4 tiles.
+  // LSB mode (2.5x fewer MFMAs, 24 fewer weight VGPRs): RGB at 4 tiles / 2
+  // pairs / 1 wave, 0.40-0.43 ms against 0.55 ms at the exact mode's 2 / 1 / 2
+  // (the narrower strip's 2.5x input overfetch now sets the time); gray keeps
+  // 16 / 2 / 1; the W % 4 != 0 variants take 2 tiles / 1 pair / 2 waves (wider
+  // ones spill SGPRs).
   struct Cfg {
     int nx, occ;
     void (*fn)(dev::SepArgs);
@@ -595,22 +600,11 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
       {{STRIPE_BLUR_CFG(1, false, 16, 2, 1, false), STRIPE_BLUR_CFG(1, true, 4, 1, 2, false)},
        {STRIPE_BLUR_CFG(3, false, 2, 1, 2, false), STRIPE_BLUR_CFG(3, true, 2, 1, 2, false)}},
       {{STRIPE_BLUR_CFG(1, false, 16, 2, 1, true), STRIPE_BLUR_CFG(1, true, 2, 1, 2, true)},
-       {STRIPE_BLUR_CFG(3, false, 2, 1, 2, true), STRIPE_BLUR_CFG(3, true, 2, 1, 2, true)}}};
+       {STRIPE_BLUR_CFG(3, false, 4, 2, 1, true), STRIPE_BLUR_CFG(3, true, 2, 1, 2, true)}}};
   const bool edge = L.W % 4 != 0;
   const bool lsb = pc.conv_mode == 2;
   sa.bias = (float)pc.conv_bias;
-  const Cfg* cfp = &cfgs[lsb][p.cmid == 3][edge];
-  // TEMPORARY A/B of LSB configurations (STRIPE_BLUR_XCFG=i)
-  static const Cfg xrgb[] = {STRIPE_BLUR_CFG(3, false, 6, 2, 1, true), STRIPE_BLUR_CFG(3, false, 4, 2, 1, true),
-                             STRIPE_BLUR_CFG(3, false, 4, 3, 1, true), STRIPE_BLUR_CFG(3, false, 5, 2, 1, true)};
-  static const Cfg xgray[] = {STRIPE_BLUR_CFG(1, false, 8, 1, 2, true), STRIPE_BLUR_CFG(1, false, 4, 1, 3, true),
-                              STRIPE_BLUR_CFG(1, false, 8, 2, 2, true), STRIPE_BLUR_CFG(1, false, 4, 2, 2, true)};
-  static const int xcfg = [] {
-    const char* e = std::getenv("STRIPE_BLUR_XCFG");
-    return e ? std::atoi(e) : -1;
-  }();
-  if (lsb && !edge && xcfg >= 0 && xcfg < 4) cfp = p.cmid == 3 ? &xrgb[xcfg] : &xgray[xcfg];
-  const Cfg& cf = *cfp;
+  const Cfg& cf = cfgs[lsb][p.cmid == 3][edge];
 #undef STRIPE_BLUR_CFG
   sa.nstrips = (int)div_up(L.W, 16 * cf.nx);
 

@@ -43,9 +43,10 @@ FILTERS = {
     "laplace": "[[0,1,0],[1,-4,1],[0,1,0]]",
     "sobel": "sat(|Gx| + |Gy|)",
     "sobel_l2 / magnitude": "sat(round(sqrt(Gx^2 + Gy^2))), exact integer rounding",
-    "blur:K[:sigma]": "KxK float Gaussian (MFMA implicit-GEMM path), K <= 33",
-    "conv:K:w0;w1;...": "generic KxK float correlation (MFMA path)",
-    "sepconv:K:h..:v..": "rank-one KxK float correlation v (x) h (separable MFMA path)",
+    "blur:K[:sigma][:lsb]": "KxK float Gaussian (separable MFMA path), K <= 33; :lsb = every output within 1 LSB, "
+                            "2.5x fewer MFMAs",
+    "conv:K:w0;w1;...[:lsb]": "generic KxK float correlation (MFMA path); :lsb = within 1 LSB, 2/3 of the MFMAs",
+    "sepconv:K:h..:v..[:lsb]": "rank-one KxK float correlation v (x) h (separable MFMA path)",
     "...@border": "per-stencil border: reflect101 | replicate | constant | skip",
 }
 
