@@ -22,7 +22,10 @@ run "cfg4 gaussian5 16384x16384x3 full frame" 200 $KB --shape 16384x16384x3 --ch
 run "cfg4 gaussian5 one N=8 stripe 16384x2048x3" 200 $KB --shape 16384x2048x3 --chains gaussian5 --bands=-1 --iters 50
 run "cfg5 blur:31 16384x16384x3 full frame (separable MFMA)" 300 $KB --shape 16384x16384x3 --chains blur:31 --iters 10 --warmup 2
 run "cfg5 blur:31 one N=8 stripe 16384x2048x3" 200 $KB --shape 16384x2048x3 --chains blur:31 --iters 20 --warmup 2
+run "cfg5 blur:31:lsb (every output within 1 LSB) 16384x16384x3 full frame" 300 $KB --shape 16384x16384x3 --chains "blur:31:lsb|" --iters 10 --warmup 2
+run "cfg5 blur:31:lsb one N=8 stripe 16384x2048x3" 200 $KB --shape 16384x2048x3 --chains "blur:31:lsb|" --iters 20 --warmup 2
 run "cfg5b conv:31 arbitrary weights 16384x16384x3 full frame (i8 Toeplitz MFMA)" 300 $KB --shape 16384x16384x3 --chains "$CONV31" --iters 5 --warmup 1
 run "cfg5b conv:31 one N=8 stripe 16384x2048x3" 200 $KB --shape 16384x2048x3 --chains "$CONV31" --iters 10 --warmup 2
+run "cfg5b conv:31:lsb arbitrary weights 16384x16384x3 full frame" 300 $KB --shape 16384x16384x3 --chains "${CONV31%|}:lsb|" --iters 5 --warmup 1
 run "reference pipeline gray:ref,contrast:3.5,emboss3@skip,expand 16384x16384x3" 200 $KB --shape 16384x16384x3 --chains "gray:ref,contrast:3.5,emboss3@skip,expand|gray:ref,contrast:3.5,emboss3@skip|" --bands=-1 --iters 30
 echo done
