@@ -2,6 +2,9 @@
 #include "stripe/chain.h"
 
 #include <algorithm>
+#include <climits>
+#include <cstdint>
+#include <cstdlib>
 #include <sstream>
 
 namespace stripe {
@@ -254,7 +257,52 @@ Plan compile_chain(const std::vector<Op>& ops, int cin, Border default_border, b
   // margins valid (per pixel), and every C stores >= kMaxRadius... check it.
   for (const Pass& p : plan.passes)
     STRIPE_CHECK(p.out_margin_px <= margin_pixels(p.cout), "margin contract too wide");
+  for (Pass& p : plan.passes)
+    if (p.kind != PassKind::Pointwise && p.pro.has_post && p.pro.gray && p.pro.gmode == GrayMode::Ref) {
+      p.post_aff = lut_affine(p.pro.post, &p.post_a, &p.post_b, &p.post_k);
+      if (p.post_aff)
+        p.desc += " post=clamp((" + std::to_string(p.post_a) + "v" + (p.post_b < 0 ? "" : "+") +
+                  std::to_string(p.post_b) + ")>>" + std::to_string(p.post_k) + ")";
+    }
   return plan;
+}
+
+bool lut_affine(const std::array<uint8_t, 256>& lut, int* a_out, int* b_out, int* k_out) {
+  for (int k = 0; k <= 8; ++k) {
+    const int64_t q = int64_t(1) << k;
+    for (int a = -255; a <= 255; ++a) {
+      // b range from the unclamped entries: L q <= a v + b < (L + 1) q
+      int64_t lo = INT32_MIN, hi = INT32_MAX;
+      for (int v = 0; v < 256 && lo <= hi; ++v) {
+        const int L = lut[v];
+        if (L == 0 || L == 255) continue;
+        lo = std::max(lo, L * q - (int64_t)a * v);
+        hi = std::min(hi, (L + 1) * q - 1 - (int64_t)a * v);
+      }
+      if (lo > hi) continue;
+      // a constant-free table (all entries clamped) leaves b open: try the
+      // range's ends and a few values in between
+      const int64_t cands[3] = {lo == INT32_MIN ? -32767 : lo, hi == INT32_MAX ? 32767 : hi,
+                                lo == INT32_MIN || hi == INT32_MAX ? 0 : (lo + hi) / 2};
+      for (int64_t b : cands) {
+        if (std::llabs(b) + 255LL * std::abs(a) >= 32768) continue;
+        bool ok = true;
+        for (int v = 0; v < 256 && ok; ++v) {
+          int64_t t = ((int64_t)a * v + b);
+          t = t >= 0 ? t >> k : -((-t + q - 1) >> k);  // arithmetic shift = floor
+          t = std::min<int64_t>(255, std::max<int64_t>(0, t));
+          ok = t == lut[v];
+        }
+        if (ok) {
+          *a_out = a;
+          *b_out = (int)b;
+          *k_out = k;
+          return true;
+        }
+      }
+    }
+  }
+  return false;
 }
 
 }  // namespace stripe

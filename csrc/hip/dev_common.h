@@ -32,6 +32,9 @@ struct KArgs {
   int out_px;     // x-margin pixels to maintain on the output
   int out_border; // border mode encoded in those margins
   int has_pre, has_post, has_epi;
+  // post LUT as an affine map clamp((post_a * v + post_b) >> post_k, 0, 255)
+  // (exact for every v, found by the host; 0: use the table)
+  int post_aff, post_a, post_b, post_k;
   int gmode;      // 0 bt601, 1 ref
   uint32_t gmul[3];
   int gshift[3];

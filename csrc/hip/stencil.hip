@@ -132,6 +132,10 @@ void launch_stencil(const Pass& p, const PassConsts& pc, const PassLaunch& L, hi
   a.out_border = (int)p.out_margin_border;
   a.has_pre = 0;
   a.has_post = p.pro.has_post;
+  a.post_aff = p.post_aff;
+  a.post_a = p.post_a;
+  a.post_b = p.post_b;
+  a.post_k = p.post_k;
   a.has_epi = p.has_epi;
   const GrayParams gp = gray_params(p.pro.gmode);
   a.gmode = gp.mode;

@@ -141,12 +141,26 @@ __device__ __forceinline__ void gray_ref_pairs(const KArgs& a, const uint32_t (&
   for (int px = 0; px < 16; ++px)
     g[px] = ((byte_at(d, 3 * px) * m0) >> a.gshift[0]) + ((byte_at(d, 3 * px + 1) * m1) >> a.gshift[1]) +
             ((byte_at(d, 3 * px + 2) * m2) >> a.gshift[2]);
-  if (a.has_post) {
+  if (a.has_post && !a.post_aff) {
 #pragma unroll
     for (int px = 0; px < 16; ++px) g[px] = luts[256 + g[px]];
   }
 #pragma unroll
   for (int pp = 0; pp < 8; ++pp) u[pp] = g[2 * pp] | (g[2 * pp + 1] << 16);
+  if (a.has_post && a.post_aff) {
+    // affine post map (contrast, brightness, invert ...) in packed i16: 4 VALU
+    // per pixel pair instead of 2 dependent LDS lookups (random bytes index
+    // the table: bank conflicts and a round trip the wave waits for)
+    const short ma = (short)a.post_a, mb = (short)a.post_b;
+    const i16x2 sh = {(short)a.post_k, (short)a.post_k};
+#pragma unroll
+    for (int pp = 0; pp < 8; ++pp) {
+      i16x2 t = as_i16x2(u[pp]) * ma + mb;
+      t = t >> sh;
+      t = __builtin_elementwise_max(t, (i16x2)(short)0);
+      u[pp] = as_u32(__builtin_elementwise_min(t, (i16x2)(short)255));
+    }
+  }
 }
 
 // Prologue: the 16 output-channel bytes of a raw chunk.

@@ -55,6 +55,12 @@ struct Pass {
   // x-margin contract for the output (what the next stencil consumer needs)
   int out_margin_px = 0;
   Border out_margin_border = Border::Reflect101;
+  // a gray:ref prologue's post LUT as clamp((a * v + b) >> k, 0, 255) when
+  // that is exact for every v (contrast with a dyadic factor, brightness,
+  // invert ...): the stencil kernels then map pixel pairs in packed i16
+  // instead of LDS lookups
+  bool post_aff = false;
+  int post_a = 1, post_b = 0, post_k = 0;
   std::string desc;
 };
 
@@ -74,6 +80,10 @@ Plan compile_chain(const std::vector<Op>& ops, int cin, Border default_border,
                    bool fuse = true);
 
 // Gray-conversion parameters in the form the kernels use.
+// Find (a, b, k) with lut[v] == clamp((a * v + b) >> k, 0, 255) for every v
+// in [0, 255], |a| * 255 + |b| < 2^15 (packed i16 arithmetic), smallest k.
+bool lut_affine(const std::array<uint8_t, 256>& lut, int* a, int* b, int* k);
+
 struct GrayParams {
   int mode = 0;           // 0 = bt601, 1 = ref (per-channel trunc magic)
   uint32_t mult[3] = {0, 0, 0};  // R, G, B

@@ -92,3 +92,35 @@ def test_presets_exist():
         assert p.plan()
     with pytest.raises(KeyError):
         models.Pipeline.preset("nope")
+
+
+# ---- affine post maps: a gray:ref prologue's post LUT as clamp((a v + b) >> k)
+import re as _re
+
+import numpy as np
+
+_AFF = _re.compile(r"post=clamp\(\((-?\d+)v\+?(-?\d+)\)>>(\d+)\)")
+
+
+@pytest.mark.parametrize("pw,affine", [("contrast:3.5", True), ("contrast:3", True), ("contrast:3:cv", True),
+                                       ("contrast:0.25", True), ("brightness:40", True), ("brightness:-17", True),
+                                       ("invert", True), ("contrast:0.25,invert", True), ("contrast:1.7", False),
+                                       ("threshold:100", False),
+                                       ("contrast:3.5,brightness:-30", False)])  # saturates at 225: not one clamp
+def test_post_lut_affine_exact(C, pw, affine):
+    desc = C.plan_info(f"gray:ref,{pw},emboss3", 3)["passes"][0]["desc"]
+    m = _AFF.search(desc)
+    assert (m is not None) == affine, desc
+    if m:
+        a, b, k = (int(x) for x in m.groups())
+        v = np.arange(256, dtype=np.uint8).reshape(1, 256)
+        lut = C.golden_apply(v, pw, "reflect101", True).reshape(-1).astype(np.int64)
+        got = np.clip((a * np.arange(256) + b) >> k, 0, 255)
+        assert (got == lut).all()
+        assert abs(a) * 255 + abs(b) < 32768  # packed i16 arithmetic in the kernel
+
+
+def test_post_affine_only_on_gray_ref(C):
+    # the bt601 / plain-LUT prologues keep their tables (desc carries no post map)
+    for ch in ("gray:bt601,contrast:3.5,emboss3", "contrast:3.5,gaussian5"):
+        assert "post=" not in C.plan_info(ch, 3)["passes"][0]["desc"]

@@ -114,3 +114,18 @@ def test_autotune_picks_band_and_cap(m):
 def test_device_info(m):
     d = m._C.device_info(0)
     assert d["gcn_arch"].startswith("gfx950") and d["cu_count"] >= 1 and d["hbm_gib"] > 1
+
+
+@pytest.mark.parametrize("pw", ["contrast:3.5", "contrast:0.25,invert", "brightness:-17", "contrast:1.7",
+                                "threshold:100"])
+@pytest.mark.parametrize("st", ["emboss3@skip", "gaussian5", "sharpen"])
+@pytest.mark.parametrize("expand", [False, True])
+def test_gray_ref_post_affine_matches_golden(m, pw, st, expand):
+    # gray:ref prologue with the post map in packed i16 (affine) or the LDS table
+    chain = f"gray:ref,{pw},{st}" + (",expand" if expand else "")
+    W, H = 1037, 77
+    img = m._C.synth_rows(9, W, 3, 0, H)
+    x = torch.from_numpy(img).cuda()
+    got = m.ops.apply(x, chain, "reflect101").cpu().numpy()
+    ref = m._C.golden_apply(img, chain, "reflect101", True)
+    assert (got == ref).all()
