@@ -587,8 +587,8 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
   // LSB mode (2.5x fewer MFMAs, 24 fewer weight VGPRs): RGB at 4 tiles / 2
   // pairs / 1 wave, 0.40-0.43 ms against 0.55 ms at the exact mode's 2 / 1 / 2
   // (the narrower strip's 2.5x input overfetch now sets the time); gray keeps
-  // 16 / 2 / 1; the W % 4 != 0 variants take 2 tiles / 1 pair / 2 waves (wider
-  // ones spill SGPRs).
+  // the exact kernels; the W % 4 != 0 RGB variant takes 2 tiles / 1 pair / 2
+  // waves (wider ones spill SGPRs).
   struct Cfg {
     int nx, occ;
     void (*fn)(dev::SepArgs);
@@ -599,10 +599,14 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
   static const Cfg cfgs[2][2][2] = {
       {{STRIPE_BLUR_CFG(1, false, 16, 2, 1, false), STRIPE_BLUR_CFG(1, true, 4, 1, 2, false)},
        {STRIPE_BLUR_CFG(3, false, 2, 1, 2, false), STRIPE_BLUR_CFG(3, true, 2, 1, 2, false)}},
-      {{STRIPE_BLUR_CFG(1, false, 16, 2, 1, true), STRIPE_BLUR_CFG(1, true, 2, 1, 2, true)},
+      {{STRIPE_BLUR_CFG(1, false, 16, 2, 1, false), STRIPE_BLUR_CFG(1, true, 4, 1, 2, false)},  // gray: exact (below)
        {STRIPE_BLUR_CFG(3, false, 4, 2, 1, true), STRIPE_BLUR_CFG(3, true, 2, 1, 2, true)}}};
   const bool edge = L.W % 4 != 0;
-  const bool lsb = pc.conv_mode == 2;
+  // gray frames keep the exact kernel under :lsb (it satisfies the mode and
+  // was faster: 16K gray 0.218-0.220 ms exact vs 0.228-0.231 ms lsb at the same
+  // 16 / 2 / 1 shape; at one wave per SIMD the shorter MFMA chains expose more
+  // latency than they save)
+  const bool lsb = pc.conv_mode == 2 && p.cmid == 3;
   sa.bias = (float)pc.conv_bias;
   const Cfg& cf = cfgs[lsb][p.cmid == 3][edge];
 #undef STRIPE_BLUR_CFG
