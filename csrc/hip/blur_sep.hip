@@ -114,15 +114,22 @@ __device__ __forceinline__ uint32_t f32x2_to_h2(float x, float y) {
 // product is unchanged; for RGB a lane ends with 4 consecutive pixels of one
 // output row in each channel accumulator, i.e. 12 contiguous interleaved
 // bytes: one dwordx3 store.
-template <int C, int NX_>
+//
+// NW > 1: the NW waves of a workgroup take NW adjacent strips of one band and
+// stage their common window once, cooperatively, into a double-buffered tile
+// (one LDS barrier per pair): NW strips of PX pixels read NW PX + 48 staged
+// pixels per row instead of NW (PX + 48) -- RGB at 2 tiles: 176 instead of 320.
+template <int C, int NX_, int NW_ = 1>
 struct PlGeom {
   static constexpr int NX = NX_;                     // 16-pixel x-tiles per strip
+  static constexpr int NW = NW_;                     // waves (strips) sharing one staged window
   static constexpr int PX = 16 * NX;                 // output pixels per strip
-  static constexpr int WPX = PX + 48;                // staged pixels per row: [sx - 16, sx + PX + 32)
+  static constexpr int WPX = NW * PX + 48;           // staged pixels per row: [sx0 - 16, sx0 + NW PX + 32)
   static constexpr int UB = C == 3 ? 12 : 16;        // bytes per staging load (4 RGB / 16 gray pixels)
   static constexpr int UPX = UB / C;                 // pixels per staging load
   static constexpr int U = WPX / UPX;                // loads per staged row
-  static constexpr int LPL = (32 * U + 63) / 64;     // loads per lane per 32-row pair
+  static constexpr int LANES = 64 * NW;              // lanes staging one window
+  static constexpr int LPL = (32 * U + LANES - 1) / LANES;  // loads per lane per 32-row pair
   // plane row bytes: 16 q with q = 2 mod 4.  ds_read_b128 serves a wave in
   // the lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31} (+32), and the
   // fragment of lane (m, g) starts at quad q m + g: with q = 2 mod 4 every
@@ -130,7 +137,11 @@ struct PlGeom {
   // 44 % of the LDS cycles were bank conflicts with q = 11)
   static constexpr int STRIDE = 16 * ((2 * WPX + 15) / 16 + (((2 - (2 * WPX + 15) / 16) % 4) + 4) % 4);
   static constexpr int PLANE = 32 * STRIDE;
-  static constexpr int TILE = C * PLANE;             // LDS bytes per wave
+  static constexpr int TILE = C * PLANE;             // LDS bytes of one staged window
+  // dynamic LDS per workgroup: one window per wave, or NW = all waves sharing
+  // a double-buffered window
+  static constexpr int LDS = NW == 1 ? kSepWaves * TILE : 2 * TILE;
+  static_assert(NW == 1 || NW == kSepWaves, "a shared window spans the whole workgroup");
   static_assert(WPX % UPX == 0, "staged row must be whole loads");
   static_assert(STRIDE % 64 == 32 && STRIDE >= 2 * WPX, "plane stride");
 };
@@ -143,17 +154,31 @@ struct PlGeom {
 // accumulators' start value: 8 MFMAs per tile instead of 20, every output
 // within 1 LSB of the f64 result (the host bounds the error per weight set and
 // keeps the exact kernel when it cannot promise that).
-template <int C, bool EDGE, int NX_, int PFD, int OCC, bool LSB = false>
+template <int C, bool EDGE, int NX_, int PFD, int OCC, bool LSB = false, int NW = 1>
 __global__ __launch_bounds__(kSepWaves * 64, OCC) void k_blur_pl(SepArgs sa) {
-  using G = PlGeom<C, NX_>;
+  using G = PlGeom<C, NX_, NW>;
   constexpr int NX = G::NX;
+  static_assert(NW == 1 || PFD == 1, "shared windows prefetch one pair ahead");
   const KArgs& a = sa.a;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int task = xcd_remap((int)blockIdx.x, (int)gridDim.x, a.nxcd) * kSepWaves + wave;
-  if (task >= sa.nstrips * a.nbands) return;  // wave-uniform
-  uint8_t* wl = lds + wave * G::TILE;
-  const int strip = task % sa.nstrips, by = task / sa.nstrips;
+  const int sl = NW == 1 ? lane : (int)threadIdx.x;  // staging lane
+  int strip, by, sgx;  // strip of this wave, band, first strip of the staged window
+  if constexpr (NW == 1) {
+    const int task = xcd_remap((int)blockIdx.x, (int)gridDim.x, a.nxcd) * kSepWaves + wave;
+    if (task >= sa.nstrips * a.nbands) return;  // wave-uniform
+    strip = task % sa.nstrips;
+    by = task / sa.nstrips;
+    sgx = strip;
+  } else {
+    const int nsg = (sa.nstrips + NW - 1) / NW;  // strip groups
+    const int gt = xcd_remap((int)blockIdx.x, (int)gridDim.x, a.nxcd);
+    if (gt >= nsg * a.nbands) return;  // workgroup-uniform: every wave meets every barrier
+    by = gt / nsg;
+    sgx = (gt % nsg) * NW;
+    strip = sgx + wave;  // past the row (last group): computed, never stored
+  }
+  uint8_t* wl = lds + (NW == 1 ? wave * G::TILE : 0);
   // bands and 32-row groups sit on a grid of global rows (multiples of 32):
   // every output row is summed in the same order whatever the launch's row
   // ranges, so results are independent of the partition, bit for bit
@@ -188,25 +213,26 @@ __global__ __launch_bounds__(kSepWaves * 64, OCC) void k_blur_pl(SepArgs sa) {
   const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
   const int lo_ok = max(-R, -a.row0);  // rows addressable without remapping
   const int hi_ok = min(a.rows - 1 + R, a.Hg - 1 - a.row0);
-  const int sx = strip * G::PX;  // first output pixel of the strip
+  const int sx = strip * G::PX;   // first output pixel of the strip
+  const int wx = sgx * G::PX - 16;  // first staged pixel of the window
   const int m = lane & 15, g = lane >> 4;
 
-  // staging map: load i of a lane is unit u = lane + 64 i -> pair row u / U,
-  // pixels UPX * (u % U) .. of the staged window (window pixel 0 = sx - 16).
-  // The (row, unit) pattern repeats every P loads (64 P = a multiple of U),
-  // so only P (row, column) pairs live in registers.
+  // staging map: load i of a staging lane is unit u = sl + LANES i -> pair
+  // row u / U, pixels UPX * (u % U) .. of the staged window.  The (row, unit)
+  // pattern repeats every P loads (LANES P = a multiple of U), so only P
+  // (row, column) pairs live in registers.
   constexpr int P = [] {
     for (int p = 1; p < G::LPL; ++p)
-      if (64 * p % G::U == 0) return p;
+      if (G::LANES * p % G::U == 0) return p;
     return G::LPL;
   }();
-  constexpr int RSTEP = 64 * P / G::U;  // pair rows advanced every P loads
-  static_assert(P == G::LPL || 64 * P % G::U == 0, "staging period");
+  constexpr int RSTEP = G::LANES * P / G::U;  // pair rows advanced every P loads
+  static_assert(P == G::LPL || G::LANES * P % G::U == 0, "staging period");
   int srow[P];
   int scol[P];  // first staged pixel of the unit, relative to the window start
 #pragma unroll
   for (int i = 0; i < P; ++i) {
-    const int u = lane + 64 * i;
+    const int u = sl + G::LANES * i;
     srow[i] = u / G::U;
     scol[i] = G::UPX * (u % G::U);
   }
@@ -219,7 +245,7 @@ __global__ __launch_bounds__(kSepWaves * 64, OCC) void k_blur_pl(SepArgs sa) {
   // lane part of an interior load's offset: row srow * pitch + window bytes
   uint32_t loff[P];
 #pragma unroll
-  for (int i = 0; i < P; ++i) loff[i] = (uint32_t)(srow[i] * a.in_pitch + (sx - 16 + scol[i]) * C);
+  for (int i = 0; i < P; ++i) loff[i] = (uint32_t)(srow[i] * a.in_pitch + (wx + scol[i]) * C);
   auto load = [&](int i, uint32_t off, auto buf_c) __attribute__((always_inline)) {
     constexpr int B = decltype(buf_c)::value;
     if constexpr (C == 3) pf[B][i] = __builtin_amdgcn_raw_buffer_load_b96(rin, off, 0, 0);
@@ -241,11 +267,11 @@ __global__ __launch_bounds__(kSepWaves * 64, OCC) void k_blur_pl(SepArgs sa) {
         // rows beyond the stripe + halo feed only zero weights: clamp, then border-map
         const int y = yt + srow[i % P] + RSTEP * (i / P);
         const uint32_t roff = in_row_off(a, min(max(y, -R), a.rows - 1 + R));
-        load(i, unit_ok(i) ? roff + (uint32_t)((sx - 16 + scol[i % P]) * C) : kOOB, buf_c);
+        load(i, unit_ok(i) ? roff + (uint32_t)((wx + scol[i % P]) * C) : kOOB, buf_c);
       }
     }
   };
-  auto stage = [&](auto buf_c) __attribute__((always_inline)) {
+  auto stage = [&](auto buf_c, uint8_t* wl) __attribute__((always_inline)) {
     constexpr int B = decltype(buf_c)::value;
 #pragma unroll
     for (int i = 0; i < G::LPL; ++i) {
@@ -293,8 +319,18 @@ __global__ __launch_bounds__(kSepWaves * 64, OCC) void k_blur_pl(SepArgs sa) {
   f4 acc[C][NX][2];  // running vertical sums of the current output group
   auto step = [&](auto fin_c, auto start_c, auto buf_c, int k) __attribute__((always_inline)) {
     constexpr bool FIN = decltype(fin_c)::value, START = decltype(start_c)::value;
-    stage(buf_c);
-    sep_lds_sync();
+    // the window of pair k: the wave's own tile, or buffer k & 1 of the shared
+    // one (written here, read after the barrier; the other buffer's readers of
+    // pair k - 1 all passed this pair's barrier before it is written again)
+    uint8_t* const wt = NW == 1 ? wl : wl + (k & 1) * G::TILE;
+    stage(buf_c, wt);
+    if constexpr (NW == 1) {
+      sep_lds_sync();
+    } else {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");  // s_waitcnt lgkmcnt(0); loads stay in flight
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    }
     // pair k + PFD exists iff group k + PFD - 1 does (pairs 0 .. ngroups)
     if (START && k + PFD <= ngroups) prefetch(k + PFD, buf_c);
     const int yg = base + 32 * (k - 1);  // first row of the group being finished
@@ -313,7 +349,7 @@ __global__ __launch_bounds__(kSepWaves * 64, OCC) void k_blur_pl(SepArgs sa) {
     constexpr int T = NX * C;
     auto hread = [&](int t, half8 (&f)[2][2]) __attribute__((always_inline)) {
       const int i = t / C, c = t % C;
-      const uint8_t* fb = wl + c * G::PLANE + m * G::STRIDE + 2 * (16 * i + 8 * g);
+      const uint8_t* fb = wt + c * G::PLANE + m * G::STRIDE + 2 * ((NW == 1 ? 0 : wave * G::PX) + 16 * i + 8 * g);
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         f[0][s] = *reinterpret_cast<const half8*>(fb + 64 * s);
@@ -416,7 +452,7 @@ __global__ __launch_bounds__(kSepWaves * 64, OCC) void k_blur_pl(SepArgs sa) {
       if (t + 2 < T) hread(t + 2, F[t & 1]);
       vert(t, X[t & 1]);
     }
-    sep_lds_sync();  // fragment reads done before the next pair overwrites the planes
+    if constexpr (NW == 1) sep_lds_sync();  // fragment reads done before the next pair overwrites the planes
   };
   using T_ = std::integral_constant<bool, true>;
   using F_ = std::integral_constant<bool, false>;
@@ -587,20 +623,24 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
   // LSB mode (2.5x fewer MFMAs, 24 fewer weight VGPRs): RGB at 4 tiles / 2
   // pairs / 1 wave, 0.40-0.43 ms against 0.55 ms at the exact mode's 2 / 1 / 2
   // (the narrower strip's 2.5x input overfetch now sets the time); gray keeps
-  // the exact kernels; the W % 4 != 0 RGB variant takes 2 tiles / 1 pair / 2
-  // waves (wider ones spill SGPRs).
+  // the exact kernels.
+  // Workgroup-shared windows (NW = 4, tools/ab/r3/r3_blur_nw.sh): RGB exact at
+  // 2 / 1 / 2 0.556 -> 0.499-0.503 ms, lsb 0.423-0.426 (4 / 2 / 1 per wave) ->
+  // 0.418-0.420; the N=8 stripe and 16K gray move within noise (gray stays per
+  // wave).
   struct Cfg {
-    int nx, occ;
+    int nx, occ, nw;
     void (*fn)(dev::SepArgs);
-    size_t tile;
+    size_t lds;
   };
-#define STRIPE_BLUR_CFG(CC, EDGE, NX, PFD, OCC, LSB) \
-  Cfg { NX, OCC, dev::k_blur_pl<CC, EDGE, NX, PFD, OCC, LSB>, (size_t)dev::PlGeom<CC, NX>::TILE }
+#define STRIPE_BLUR_CFGW(CC, EDGE, NX, PFD, OCC, LSB, NW) \
+  Cfg { NX, OCC, NW, dev::k_blur_pl<CC, EDGE, NX, PFD, OCC, LSB, NW>, (size_t)dev::PlGeom<CC, NX, NW>::LDS }
+#define STRIPE_BLUR_CFG(CC, EDGE, NX, PFD, OCC, LSB) STRIPE_BLUR_CFGW(CC, EDGE, NX, PFD, OCC, LSB, 1)
   static const Cfg cfgs[2][2][2] = {
       {{STRIPE_BLUR_CFG(1, false, 16, 2, 1, false), STRIPE_BLUR_CFG(1, true, 4, 1, 2, false)},
-       {STRIPE_BLUR_CFG(3, false, 2, 1, 2, false), STRIPE_BLUR_CFG(3, true, 2, 1, 2, false)}},
+       {STRIPE_BLUR_CFGW(3, false, 2, 1, 2, false, 4), STRIPE_BLUR_CFGW(3, true, 2, 1, 2, false, 4)}},
       {{STRIPE_BLUR_CFG(1, false, 16, 2, 1, false), STRIPE_BLUR_CFG(1, true, 4, 1, 2, false)},  // gray: exact (below)
-       {STRIPE_BLUR_CFG(3, false, 4, 2, 1, true), STRIPE_BLUR_CFG(3, true, 2, 1, 2, true)}}};
+       {STRIPE_BLUR_CFGW(3, false, 2, 1, 2, true, 4), STRIPE_BLUR_CFGW(3, true, 2, 1, 2, true, 4)}}};
   const bool edge = L.W % 4 != 0;
   // gray frames keep the exact kernel under :lsb (it satisfies the mode and
   // was faster: 16K gray 0.218-0.220 ms exact vs 0.228-0.231 ms lsb at the same
@@ -610,7 +650,10 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
   sa.bias = (float)pc.conv_bias;
   const Cfg& cf = cfgs[lsb][p.cmid == 3][edge];
 #undef STRIPE_BLUR_CFG
+#undef STRIPE_BLUR_CFGW
+  // strips, rounded up to whole windows when NW waves share one
   sa.nstrips = (int)div_up(L.W, 16 * cf.nx);
+  const int64_t nstrips_w = div_up(sa.nstrips, cf.nw) * cf.nw;
 
   const int n0 = std::max(0, L.ry[1] - L.ry[0]);
   const int n1 = L.nrange > 1 ? std::max(0, L.ry[3] - L.ry[2]) : 0;
@@ -629,7 +672,7 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
     const int64_t slots = (int64_t)cf.occ * resident_simds();
     int64_t gpb = 1, best = -1;
     for (int64_t c = 1; c <= 64; ++c) {
-      const int64_t tasks = (int64_t)sa.nstrips * (div_up(g0, c) + div_up(g1, c));
+      const int64_t tasks = nstrips_w * (div_up(g0, c) + div_up(g1, c));
       const int64_t cost = div_up(tasks, slots) * (c + 1);
       if (best < 0 || cost < best) {
         best = cost;
@@ -650,9 +693,9 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
     sa.a2 = n1 ? grid0(a.ry2) : 0;
     a.nb0 = (int)div_up(a.ry1 - sa.a0, band);
     a.nbands = a.nb0 + (n1 ? (int)div_up(a.ry3 - sa.a2, band) : 0);
-    const dim3 grid((unsigned)div_up((int64_t)sa.nstrips * a.nbands, dev::kSepWaves));
-    const size_t lds = (size_t)dev::kSepWaves * cf.tile;
-    cf.fn<<<grid, dev::kSepWaves * 64, lds, s>>>(sa);
+    const dim3 grid((unsigned)(cf.nw == 1 ? div_up((int64_t)sa.nstrips * a.nbands, dev::kSepWaves)
+                                          : nstrips_w / cf.nw * a.nbands));
+    cf.fn<<<grid, dev::kSepWaves * 64, cf.lds, s>>>(sa);
     HIP_CHECK(hipGetLastError());
   }
   if (p.out_margin_px > 0)

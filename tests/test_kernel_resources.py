@@ -48,8 +48,8 @@ def test_hot_kernels_have_occupancy(report):
         if "k_sep" in k or "k_direct" in k:
             assert occ >= 3, (k, occ)
         elif "k_blur_pl" in k:
-            # <C, EDGE, NX, PFD >= 2, OCC = 1, LSB>: one wave per SIMD by design
-            one = re.search(r"ELi[2-9]ELi1ELb[01]EEEvNS0_7SepArgsE$", k) is not None
+            # <C, EDGE, NX, PFD >= 2, OCC = 1, LSB, NW>: one wave per SIMD by design
+            one = re.search(r"ELi[2-9]ELi1ELb[01]ELi[14]EEEvNS0_7SepArgsE$", k) is not None
             assert occ >= (1 if one else 2), (k, occ)
 
 
