@@ -119,6 +119,9 @@ __device__ __forceinline__ uint32_t f32x2_to_h2(float x, float y) {
 // stage their common window once, cooperatively, into a double-buffered tile
 // (one LDS barrier per pair): NW strips of PX pixels read NW PX + 48 staged
 // pixels per row instead of NW (PX + 48) -- RGB at 2 tiles: 176 instead of 320.
+// workgroup size: kSepWaves independent waves, or the NW waves sharing a window
+constexpr int blur_threads(int nw) { return 64 * (nw == 1 ? kSepWaves : nw); }
+
 template <int C, int NX_, int NW_ = 1>
 struct PlGeom {
   static constexpr int NX = NX_;                     // 16-pixel x-tiles per strip
@@ -141,7 +144,8 @@ struct PlGeom {
   // dynamic LDS per workgroup: one window per wave, or NW = all waves sharing
   // a double-buffered window
   static constexpr int LDS = NW == 1 ? kSepWaves * TILE : 2 * TILE;
-  static_assert(NW == 1 || NW == kSepWaves, "a shared window spans the whole workgroup");
+  static constexpr int THREADS = blur_threads(NW);  // workgroup size
+  static_assert(NW == 1 || NW == 4 || NW == 8, "a shared window spans the whole workgroup");
   static_assert(WPX % UPX == 0, "staged row must be whole loads");
   static_assert(STRIDE % 64 == 32 && STRIDE >= 2 * WPX, "plane stride");
 };
@@ -154,8 +158,9 @@ struct PlGeom {
 // accumulators' start value: 8 MFMAs per tile instead of 20, every output
 // within 1 LSB of the f64 result (the host bounds the error per weight set and
 // keeps the exact kernel when it cannot promise that).
+// (launch bounds: OCC waves per SIMD = OCC * 256 / THREADS workgroups per CU)
 template <int C, bool EDGE, int NX_, int PFD, int OCC, bool LSB = false, int NW = 1>
-__global__ __launch_bounds__(kSepWaves * 64, OCC) void k_blur_pl(SepArgs sa) {
+__global__ __launch_bounds__(blur_threads(NW), OCC * 256 / blur_threads(NW)) void k_blur_pl(SepArgs sa) {
   using G = PlGeom<C, NX_, NW>;
   constexpr int NX = G::NX;
   static_assert(NW == 1 || PFD == 1, "shared windows prefetch one pair ahead");
@@ -648,7 +653,16 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
   // latency than they save)
   const bool lsb = pc.conv_mode == 2 && p.cmid == 3;
   sa.bias = (float)pc.conv_bias;
-  const Cfg& cf = cfgs[lsb][p.cmid == 3][edge];
+  const Cfg* cfp = &cfgs[lsb][p.cmid == 3][edge];
+  // TEMPORARY A/B (STRIPE_BLUR_NW=i): 8-wave shared windows
+  static const Cfg xw[2][2] = {{STRIPE_BLUR_CFGW(3, false, 2, 1, 2, false, 8), STRIPE_BLUR_CFGW(3, false, 1, 1, 2, false, 8)},
+                               {STRIPE_BLUR_CFGW(3, false, 2, 1, 2, true, 8), STRIPE_BLUR_CFGW(3, false, 1, 1, 2, true, 8)}};
+  static const int xnw = [] {
+    const char* e = std::getenv("STRIPE_BLUR_NW");
+    return e ? std::atoi(e) : -1;
+  }();
+  if (!edge && p.cmid == 3 && xnw >= 0 && xnw < 2) cfp = &xw[lsb][xnw];
+  const Cfg& cf = *cfp;
 #undef STRIPE_BLUR_CFG
 #undef STRIPE_BLUR_CFGW
   // strips, rounded up to whole windows when NW waves share one
@@ -695,7 +709,7 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
     a.nbands = a.nb0 + (n1 ? (int)div_up(a.ry3 - sa.a2, band) : 0);
     const dim3 grid((unsigned)(cf.nw == 1 ? div_up((int64_t)sa.nstrips * a.nbands, dev::kSepWaves)
                                           : nstrips_w / cf.nw * a.nbands));
-    cf.fn<<<grid, dev::kSepWaves * 64, cf.lds, s>>>(sa);
+    cf.fn<<<grid, 64 * (cf.nw == 1 ? dev::kSepWaves : cf.nw), cf.lds, s>>>(sa);
     HIP_CHECK(hipGetLastError());
   }
   if (p.out_margin_px > 0)
