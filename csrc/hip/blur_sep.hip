@@ -629,10 +629,14 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
   // pairs / 1 wave, 0.40-0.43 ms against 0.55 ms at the exact mode's 2 / 1 / 2
   // (the narrower strip's 2.5x input overfetch now sets the time); gray keeps
   // the exact kernels.
-  // Workgroup-shared windows (NW = 4, tools/ab/r3/r3_blur_nw.sh): RGB exact at
-  // 2 / 1 / 2 0.556 -> 0.499-0.503 ms, lsb 0.423-0.426 (4 / 2 / 1 per wave) ->
-  // 0.418-0.420; the N=8 stripe and 16K gray move within noise (gray stays per
-  // wave).
+  // Workgroup-shared windows (tools/ab/r3/r3_blur_nw.sh, r3_blur_nw8.sh): RGB
+  // exact at 2 / 1 / 2 0.556 -> 0.499-0.505 ms with 4 or 8 waves sharing a
+  // window; lsb 0.423-0.426 (4 / 2 / 1 per wave) -> 0.418-0.420 (4 waves) ->
+  // 0.386-0.393 (8 waves: 304 staged pixels per row for 256 outputs, one
+  // 8-wave workgroup per CU with a 2 x 58 KB tile); the N=8 stripe and 16K
+  // gray move within noise (gray stays per wave).  W % 4 != 0 frames (16383 x
+  // 4099): exact 0.130-0.134 ms with 4 waves vs 0.139-0.142 with 8, lsb
+  // 0.113-0.116 vs 0.108-0.110.
   struct Cfg {
     int nx, occ, nw;
     void (*fn)(dev::SepArgs);
@@ -643,9 +647,9 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
 #define STRIPE_BLUR_CFG(CC, EDGE, NX, PFD, OCC, LSB) STRIPE_BLUR_CFGW(CC, EDGE, NX, PFD, OCC, LSB, 1)
   static const Cfg cfgs[2][2][2] = {
       {{STRIPE_BLUR_CFG(1, false, 16, 2, 1, false), STRIPE_BLUR_CFG(1, true, 4, 1, 2, false)},
-       {STRIPE_BLUR_CFGW(3, false, 2, 1, 2, false, 4), STRIPE_BLUR_CFGW(3, true, 2, 1, 2, false, 4)}},
+       {STRIPE_BLUR_CFGW(3, false, 2, 1, 2, false, 8), STRIPE_BLUR_CFGW(3, true, 2, 1, 2, false, 4)}},
       {{STRIPE_BLUR_CFG(1, false, 16, 2, 1, false), STRIPE_BLUR_CFG(1, true, 4, 1, 2, false)},  // gray: exact (below)
-       {STRIPE_BLUR_CFGW(3, false, 2, 1, 2, true, 4), STRIPE_BLUR_CFGW(3, true, 2, 1, 2, true, 4)}}};
+       {STRIPE_BLUR_CFGW(3, false, 2, 1, 2, true, 8), STRIPE_BLUR_CFGW(3, true, 2, 1, 2, true, 8)}}};
   const bool edge = L.W % 4 != 0;
   // gray frames keep the exact kernel under :lsb (it satisfies the mode and
   // was faster: 16K gray 0.218-0.220 ms exact vs 0.228-0.231 ms lsb at the same
@@ -653,16 +657,7 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
   // latency than they save)
   const bool lsb = pc.conv_mode == 2 && p.cmid == 3;
   sa.bias = (float)pc.conv_bias;
-  const Cfg* cfp = &cfgs[lsb][p.cmid == 3][edge];
-  // TEMPORARY A/B (STRIPE_BLUR_NW=i): 8-wave shared windows
-  static const Cfg xw[2][2] = {{STRIPE_BLUR_CFGW(3, false, 2, 1, 2, false, 8), STRIPE_BLUR_CFGW(3, false, 1, 1, 2, false, 8)},
-                               {STRIPE_BLUR_CFGW(3, false, 2, 1, 2, true, 8), STRIPE_BLUR_CFGW(3, false, 1, 1, 2, true, 8)}};
-  static const int xnw = [] {
-    const char* e = std::getenv("STRIPE_BLUR_NW");
-    return e ? std::atoi(e) : -1;
-  }();
-  if (!edge && p.cmid == 3 && xnw >= 0 && xnw < 2) cfp = &xw[lsb][xnw];
-  const Cfg& cf = *cfp;
+  const Cfg& cf = cfgs[lsb][p.cmid == 3][edge];
 #undef STRIPE_BLUR_CFG
 #undef STRIPE_BLUR_CFGW
   // strips, rounded up to whole windows when NW waves share one
