@@ -163,7 +163,6 @@ template <int C, bool EDGE, int NX_, int PFD, int OCC, bool LSB = false, int NW 
 __global__ __launch_bounds__(blur_threads(NW), OCC * 256 / blur_threads(NW)) void k_blur_pl(SepArgs sa) {
   using G = PlGeom<C, NX_, NW>;
   constexpr int NX = G::NX;
-  static_assert(NW == 1 || PFD == 1, "shared windows prefetch one pair ahead");
   const KArgs& a = sa.a;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -657,7 +656,16 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
   // latency than they save)
   const bool lsb = pc.conv_mode == 2 && p.cmid == 3;
   sa.bias = (float)pc.conv_bias;
-  const Cfg& cf = cfgs[lsb][p.cmid == 3][edge];
+  const Cfg* cfp = &cfgs[lsb][p.cmid == 3][edge];
+  // TEMPORARY A/B (STRIPE_BLUR_NW=i): two pairs in flight on the shared windows
+  static const Cfg xw[2][2] = {{STRIPE_BLUR_CFGW(3, false, 2, 2, 2, false, 8), STRIPE_BLUR_CFGW(3, false, 2, 2, 1, false, 8)},
+                               {STRIPE_BLUR_CFGW(3, false, 2, 2, 2, true, 8), STRIPE_BLUR_CFGW(3, false, 2, 2, 1, true, 8)}};
+  static const int xnw = [] {
+    const char* e = std::getenv("STRIPE_BLUR_NW");
+    return e ? std::atoi(e) : -1;
+  }();
+  if (!edge && p.cmid == 3 && xnw >= 0 && xnw < 2) cfp = &xw[lsb][xnw];
+  const Cfg& cf = *cfp;
 #undef STRIPE_BLUR_CFG
 #undef STRIPE_BLUR_CFGW
   // strips, rounded up to whole windows when NW waves share one

@@ -1,5 +1,5 @@
 #!/bin/bash
-# 8-wave shared blur windows (STRIPE_BLUR_NW = 0: 2 tiles, 1: 1 tile per wave): correctness, kbench
+# shared blur windows, A/B variants selected by STRIPE_BLUR_NW = 0, 1 (see the launcher): correctness, kbench
 set -o pipefail
 O=gpurun_out/r3blurnw8; mkdir -p $O
 for x in 0 1; do
