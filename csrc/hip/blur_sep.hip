@@ -635,7 +635,10 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
   // 8-wave workgroup per CU with a 2 x 58 KB tile); the N=8 stripe and 16K
   // gray move within noise (gray stays per wave).  W % 4 != 0 frames (16383 x
   // 4099): exact 0.130-0.134 ms with 4 waves vs 0.139-0.142 with 8, lsb
-  // 0.113-0.116 vs 0.108-0.110.
+  // 0.113-0.116 vs 0.108-0.110.  Two pairs in flight (PFD = 2, the register
+  // prefetch two pairs ahead) on the 8-wave windows: exact 0.494-0.497 ->
+  // 0.481-0.491 ms, lsb 0.389-0.391 -> 0.365-0.367, the N=8 stripe's lsb
+  // 0.0487 -> 0.0455 (r3_blur_nw8.sh).
   struct Cfg {
     int nx, occ, nw;
     void (*fn)(dev::SepArgs);
@@ -646,9 +649,9 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
 #define STRIPE_BLUR_CFG(CC, EDGE, NX, PFD, OCC, LSB) STRIPE_BLUR_CFGW(CC, EDGE, NX, PFD, OCC, LSB, 1)
   static const Cfg cfgs[2][2][2] = {
       {{STRIPE_BLUR_CFG(1, false, 16, 2, 1, false), STRIPE_BLUR_CFG(1, true, 4, 1, 2, false)},
-       {STRIPE_BLUR_CFGW(3, false, 2, 1, 2, false, 8), STRIPE_BLUR_CFGW(3, true, 2, 1, 2, false, 4)}},
+       {STRIPE_BLUR_CFGW(3, false, 2, 2, 2, false, 8), STRIPE_BLUR_CFGW(3, true, 2, 1, 2, false, 4)}},
       {{STRIPE_BLUR_CFG(1, false, 16, 2, 1, false), STRIPE_BLUR_CFG(1, true, 4, 1, 2, false)},  // gray: exact (below)
-       {STRIPE_BLUR_CFGW(3, false, 2, 1, 2, true, 8), STRIPE_BLUR_CFGW(3, true, 2, 1, 2, true, 8)}}};
+       {STRIPE_BLUR_CFGW(3, false, 2, 2, 2, true, 8), STRIPE_BLUR_CFGW(3, true, 2, 1, 2, true, 8)}}};
   const bool edge = L.W % 4 != 0;
   // gray frames keep the exact kernel under :lsb (it satisfies the mode and
   // was faster: 16K gray 0.218-0.220 ms exact vs 0.228-0.231 ms lsb at the same
@@ -656,16 +659,7 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
   // latency than they save)
   const bool lsb = pc.conv_mode == 2 && p.cmid == 3;
   sa.bias = (float)pc.conv_bias;
-  const Cfg* cfp = &cfgs[lsb][p.cmid == 3][edge];
-  // TEMPORARY A/B (STRIPE_BLUR_NW=i): two pairs in flight on the shared windows
-  static const Cfg xw[2][2] = {{STRIPE_BLUR_CFGW(3, false, 2, 2, 2, false, 8), STRIPE_BLUR_CFGW(3, false, 2, 2, 1, false, 8)},
-                               {STRIPE_BLUR_CFGW(3, false, 2, 2, 2, true, 8), STRIPE_BLUR_CFGW(3, false, 2, 2, 1, true, 8)}};
-  static const int xnw = [] {
-    const char* e = std::getenv("STRIPE_BLUR_NW");
-    return e ? std::atoi(e) : -1;
-  }();
-  if (!edge && p.cmid == 3 && xnw >= 0 && xnw < 2) cfp = &xw[lsb][xnw];
-  const Cfg& cf = *cfp;
+  const Cfg& cf = cfgs[lsb][p.cmid == 3][edge];
 #undef STRIPE_BLUR_CFG
 #undef STRIPE_BLUR_CFGW
   // strips, rounded up to whole windows when NW waves share one
