@@ -452,6 +452,17 @@ def main():
             nbytes = H * W * pinfo["cout"]
             shm = None
             if world > 1 or a.ref_shm:
+                # the frame lives in /dev/shm: a tmpfs smaller than the frame
+                # would SIGBUS on first touch (no exception to guard), so rank 0
+                # checks the free space and every rank follows its decision
+                try:
+                    st = os.statvfs("/dev/shm")
+                    free = st.f_bavail * st.f_frsize
+                except OSError:
+                    free = 0
+                if from_root([1.0 if free >= nbytes + (64 << 20) else 0.0])[0] < 1.0:
+                    scopes["ref_window"] = {"skipped": f"/dev/shm has {free} B free, the host frame needs {nbytes} B"}
+                    return
                 names = [f"stripe_refwin_{os.getpid()}" if rank == 0 else None]
                 if world > 1:
                     dist.broadcast_object_list(names, src=0)
