@@ -638,7 +638,9 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
   // 0.113-0.116 vs 0.108-0.110.  Two pairs in flight (PFD = 2, the register
   // prefetch two pairs ahead) on the 8-wave windows: exact 0.494-0.497 ->
   // 0.481-0.491 ms, lsb 0.389-0.391 -> 0.365-0.367, the N=8 stripe's lsb
-  // 0.0487 -> 0.0455 (r3_blur_nw8.sh).
+  // 0.0487 -> 0.0455 (r3_blur_nw8.sh).  Gray on 8-wave windows of 8-tile strips
+  // (r3_blur_gray.sh): 16K 0.211-0.212 (16 tiles per wave, 1 wave/SIMD) ->
+  // 0.201-0.202 ms, 16384x2048 0.037 -> 0.034.
   struct Cfg {
     int nx, occ, nw;
     void (*fn)(dev::SepArgs);
@@ -648,9 +650,9 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
   Cfg { NX, OCC, NW, dev::k_blur_pl<CC, EDGE, NX, PFD, OCC, LSB, NW>, (size_t)dev::PlGeom<CC, NX, NW>::LDS }
 #define STRIPE_BLUR_CFG(CC, EDGE, NX, PFD, OCC, LSB) STRIPE_BLUR_CFGW(CC, EDGE, NX, PFD, OCC, LSB, 1)
   static const Cfg cfgs[2][2][2] = {
-      {{STRIPE_BLUR_CFG(1, false, 16, 2, 1, false), STRIPE_BLUR_CFG(1, true, 4, 1, 2, false)},
+      {{STRIPE_BLUR_CFGW(1, false, 8, 1, 2, false, 8), STRIPE_BLUR_CFG(1, true, 4, 1, 2, false)},
        {STRIPE_BLUR_CFGW(3, false, 2, 2, 2, false, 8), STRIPE_BLUR_CFGW(3, true, 2, 1, 2, false, 4)}},
-      {{STRIPE_BLUR_CFG(1, false, 16, 2, 1, false), STRIPE_BLUR_CFG(1, true, 4, 1, 2, false)},  // gray: exact (below)
+      {{STRIPE_BLUR_CFGW(1, false, 8, 1, 2, false, 8), STRIPE_BLUR_CFG(1, true, 4, 1, 2, false)},  // gray: exact (below)
        {STRIPE_BLUR_CFGW(3, false, 2, 2, 2, true, 8), STRIPE_BLUR_CFGW(3, true, 2, 1, 2, true, 8)}}};
   const bool edge = L.W % 4 != 0;
   // gray frames keep the exact kernel under :lsb (it satisfies the mode and
