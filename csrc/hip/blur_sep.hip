@@ -702,11 +702,16 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
     const int band = (int)(32 * gpb);
 
     a.band = band;
-    static const int nxcd = [] {
+    // XCD-contiguous workgroups when the pass stays in the Infinity Cache (an
+    // N=8 stripe): neighbouring windows' shared columns become L2 hits (lsb
+    // 16384x2048 RGB 0.0454-0.046 -> 0.0431 ms, exact unchanged; a frame
+    // streaming from HBM gains nothing, r3_blur_band2.sh); STRIPE_XCD forces it
+    static const int env_xcd = [] {
       const char* e = std::getenv("STRIPE_XCD");
-      return e ? std::atoi(e) : 0;
+      return e ? std::atoi(e) : -1;
     }();
-    a.nxcd = nxcd;
+    const int64_t pass_bytes = (int64_t)(n0 + n1) * L.W * 2 * p.cmid;
+    a.nxcd = env_xcd >= 0 ? env_xcd : (pass_bytes > dev::kNtMinBytes ? 0 : dev::kXcdCount);
     a.nb0 = (int)div_up(a.ry1 - sa.a0, band);
     a.nbands = a.nb0 + (n1 ? (int)div_up(a.ry3 - sa.a2, band) : 0);
     const dim3 grid((unsigned)(cf.nw == 1 ? div_up((int64_t)sa.nstrips * a.nbands, dev::kSepWaves)
