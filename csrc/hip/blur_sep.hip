@@ -4,27 +4,30 @@
 // passes, both run as GEMMs on the matrix cores with the intermediate kept in
 // registers (no LDS round trip, no second kernel):
 //
-//   horizontal  X[16 rows][16 bytes] = In[16 rows][window] . Th[window][16]
-//               Th is the banded Toeplitz matrix of the 1-D weights over the
-//               channel-interleaved bytes (tap stride C), so RGB needs no
-//               de-interleave; A = input bytes staged in LDS as exact f16.
-//   vertical    Out^T[16 bytes][16 rows] = X^T[16][64 rows] . Tv^T[64][16]
+//   horizontal  X[16 rows][16 px] = In[16 rows][64-px window] . Th[64][16]
+//               per channel: Th is the banded Toeplitz matrix of the 1-D
+//               weights; A = the channel's input pixels, staged in LDS as
+//               exact f16 planes (RGB de-interleaved while staging).
+//   vertical    Out^T[16 px][16 rows] = X^T[16][64 rows] . Tv^T[64][16]
 //               X comes straight from the horizontal MFMA's accumulator layout
 //               (column on the lane, rows in registers = the A operand of a
 //               product that sums over X's rows), and the transposed product
-//               leaves each lane with 4 consecutive output bytes of one row,
-//               so results leave as one dword store per lane.
+//               leaves each lane with 4 consecutive output pixels of one row
+//               (RGB: 12 interleaved bytes, one dwordx3 store).
 //
 // Precision: u8 inputs are exact in f16; weights and X are split into f16
 // hi + lo parts (2 MFMAs for the horizontal pass, 3 for the vertical), so the
 // f32 result is within ~1e-5 of the f64 golden (conv
-// passes match within 1 LSB, ties only).
+// passes match within 1 LSB, ties only).  The ":lsb" mode (LSB below) takes
+// one f16 part of each on the centred input: every output within 1 LSB.
 //
-// Work: one wave = one 128-byte column strip x one band of rows (a multiple
-// of 32), wave-independent (own LDS tile, no workgroup barrier).
-// 32 output rows need 64 rows of X; each 32-row X pair is consumed as soon as
-// it is made: it finishes the previous output group (k-step 1) and starts the
-// next one (k-step 0), so only the running f32 sums stay in registers.
+// Work: a wave owns a strip of NX 16-pixel tiles x one band of rows (a
+// multiple of 32); the NW waves of a workgroup own NW adjacent strips and
+// stage their common window cooperatively (NW = 1: every wave its own tile,
+// no workgroup barrier).  32 output rows need 64 rows of X; each 32-row X
+// pair is consumed as soon as it is made: it finishes the previous output
+// group (k-step 1) and starts the next one (k-step 0), so only the running
+// f32 sums stay in registers.
 //
 // Reference parity: the reference has no large-kernel blur (its only float
 // work is kernel.cu:39-47's contrast); this is the MFMA showcase of the
