@@ -125,3 +125,18 @@ def test_gpu_backends_and_file_rendezvous(tmp_path):
         outs.append(o)
     for o in outs:
         assert run("cmp", ref, o, check=False).returncode == 0, o
+
+
+def test_precision_suffixes_in_cli(tmp_path):
+    # blur:K:lsb / conv:..:lsb parse through the native CLI; the host backend
+    # runs the exact golden path whatever the requested precision
+    r = run("info", "--chain", "blur:9:lsb")
+    assert "lsb" in r.stdout
+    r = run("info", "--chain", "gray:ref,contrast:3.5,emboss3@skip")
+    assert "post=clamp((7v-640)>>1)" in r.stdout
+    src = tmp_path / "in.ppm"
+    run("gen", "--synthetic", "64x40x3", "--seed", "3", "--output", src)
+    a, b = tmp_path / "a.ppm", tmp_path / "b.ppm"
+    run("run", "--input", src, "--output", a, "--chain", "blur:9", "--ranks", "1", "--backend", "host")
+    run("run", "--input", src, "--output", b, "--chain", "blur:9:lsb", "--ranks", "2", "--backend", "host")
+    assert json.loads(run("cmp", a, b).stdout)["max_abs"] == 0
