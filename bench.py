@@ -7,35 +7,46 @@ row-partitioned over N MI355X (one process per GPU, RCCL over xGMI).
 
 One step = one full-frame gaussian5 pass over the distributed frame: every rank
 exchanges its 2 halo rows with its neighbours (ncclSend/ncclRecv on a side
-stream) while its interior rows are filtered, then filters its boundary rows.
-Steps are iterated (ping-pong), so each step's halo rows are required work.
-With k = halo_depth > 1 (auto on > 1 rank) the exchange is communication-
-avoiding: k*2 rows travel once per k steps and each step also recomputes the
-shrinking band of neighbour rows the next step needs (more arithmetic, same
-bytes on the wire, bit-identical output); --halo-depth 1 exchanges every step.
+stream, every step: halo depth 1) while its interior rows are filtered, then
+filters its boundary rows.  Steps are iterated (ping-pong), so each step's halo
+rows are required work.
+
+Cache temperature of the headline.  A step's per-GPU working set is its stripe
+in + out: 1.61 GB on one GPU, 201 MB on each of 8.  When it fits the 256 MiB
+Infinity Cache (N=8), iterating one frame would read every step's input from
+the cache, not HBM; the headline then steps round-robin over F independent
+frames (F engines, each its own stripe pair, sharing one stream) with
+F x working set > 2 x 256 MiB, so every step reads data evicted long before --
+a stream of distinct frames, the way a video-rate workload sees the GPUs.  The
+warm single-frame number (resident_warm) and the communication-avoiding deep
+halo (resident_deep: k*2 rows exchanged once per k steps, bit-identical) are
+reported beside it as named scopes, never as `value`.
 
 Order of work (the timed region holds nothing but the K steps):
-  autotune (band height x occupancy cap, per pass and box; also ramps the
-  clock) -> W warmup steps -> K timed steps (barrier + device sync on both
-  sides, max over ranks) -> per-step device-event distribution -> golden
-  verification of the same engine -> copy roofline -> the other scopes.
-Round 2's driver number read 16 % slow because a host-side verification sat
-between the autotune and 5 warmup steps and the GPU clock dropped meanwhile
-(profiles/r3/headline_diag.txt).
+  identity (what RCCL and the runtime report, gathered to rank 0) -> autotune
+  (band height x occupancy cap x memory policy, on cold data when the frames
+  rotate; also ramps the clock) -> W warmup steps -> K timed steps (barrier +
+  device sync on both sides, max over ranks) -> per-step device events of
+  max(K, 20) more steps -> golden verification -> copy roofline -> the other
+  scopes, each skipped once the wall-time budget is spent.
+
+Hang-proofing: STRIPE_COMM_TIMEOUT_S defaults to 120 s here (every RCCL and
+gloo wait is bounded by it), and a native "last words" watchdog on every rank
+writes rank 0's record so far (the complete headline once it exists) and ends
+the process when --budget-s runs out or torchrun stops the group with SIGTERM
+after a peer died -- so the one JSON line prints well inside the driver's
+600 s even if an extra scope hangs.
 
 Scopes reported beside the headline ("resident": the frame stays in HBM):
-  resident_cold   the same steps rotating over enough stripe copies that the
-                  per-GPU working set exceeds the 256 MiB Infinity Cache
-                  (only when one stripe fits it: N=8 stripes do)
+  resident_warm   one frame iterated in place (cache-warm when it fits)
+  resident_deep   (N > 1) deep halo: one exchange per k steps, k auto
   dist_*          root GPU frame -> scatter -> filter -> gather -> root GPU
-                  (the reference's window, kernel.cu:135-225, device-resident):
-                  sequential three calls, the pipelined run_dist (direct on
-                  one GPU), and on > 1 GPU the link-aware weighted split
-                  (plan_dist_split from a measured link probe)
+                  (the reference's window, kernel.cu:135-225, device-resident)
   ref_window      the reference's exact window end, kernel.cu:190-226:
-                  filter + D2H + gather into rank 0's host memory (every rank
-                  downloads its stripe into its slice of a shared host frame)
-  e2e             pinned host stripe -> H2D -> filter -> D2H -> pinned host
+                  filter + D2H + gather into rank 0's host memory
+  e2e             pinned host stripe -> H2D -> filter -> D2H -> pinned host,
+                  with the same-box host-link roofline (H2D alone, D2H alone,
+                  both at once) that explains it
 Data: seeded synthetic random pixels (no dataset).
 
 Prints ONE JSON line on rank 0 (driver contract).
@@ -55,6 +66,7 @@ import numpy as np
 METRIC = "Mpixels/sec, 5x5 Gaussian blur on 16384x16384 RGB at 1/2/4/8 MI355X"
 BASELINE_MPX = None  # the reference publishes no number
 MALL_BYTES = 256 << 20  # MI355X Infinity Cache
+T_START = time.monotonic()
 
 
 def parse():
@@ -69,17 +81,24 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--band", type=int, default=0)
+    ap.add_argument("--frames", type=int, default=0,
+                    help="frames the headline steps over (0: auto, enough to defeat the Infinity Cache; 1: one "
+                         "frame iterated in place)")
+    ap.add_argument("--deep-steps", type=int, default=-1, help="steps of the deep-halo scope (-1: --steps; 0: skip)")
     ap.add_argument("--halo-depth", type=int, default=0,
-                    help="steps per halo exchange (0: auto, 1: exchange every step)")
+                    help="steps per exchange of the resident_deep scope (0: auto); the headline exchanges every step")
     ap.add_argument("--dist-steps", type=int, default=5, help="steps of each dist-scope measurement (0: skip)")
     ap.add_argument("--ref-steps", type=int, default=3, help="steps of the ref-window measurement (0: skip)")
     ap.add_argument("--e2e-steps", type=int, default=3, help="steps of the e2e-scope measurement (0: skip)")
-    ap.add_argument("--cold-steps", type=int, default=-1,
-                    help="steps of the cache-cold resident scope (-1: --steps; 0: skip)")
     ap.add_argument("--ref-shm", action="store_true",
                     help="ref-window host frame in POSIX shared memory even on one rank (tests the multi-rank path)")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-autotune", action="store_true", help="skip the per-shape band / occupancy autotune")
+    ap.add_argument("--budget-s", type=float, default=420.0,
+                    help="wall-time budget: extra scopes are skipped after 60 %% of it, and the watchdog writes the "
+                         "record and exits at 100 %%")
+    ap.add_argument("--comm-timeout-s", type=float, default=120.0,
+                    help="default of STRIPE_COMM_TIMEOUT_S (bound of every collective wait) for this run")
     ap.add_argument("--backend", default="rccl", choices=["rccl", "host", "gloo-gpu"],
                     help="rccl: GPU engine + RCCL (the benchmark); host: CPU golden engine + gloo (plumbing "
                          "tests); gloo-gpu: GPU engine, gloo transport through pinned host memory, processes may "
@@ -111,8 +130,13 @@ def build_info(root):
     return info
 
 
+def elapsed_s() -> float:
+    return time.monotonic() - T_START
+
+
 def main():
     a = parse()
+    os.environ.setdefault("STRIPE_COMM_TIMEOUT_S", str(a.comm_timeout_s))
     # libraries (RCCL's init banner, HIP warnings) print to stdout; keep stdout for
     # the one JSON line of the driver contract and send everything else to stderr
     sys.stdout.flush()
@@ -128,6 +152,11 @@ def main():
     from mpi_cuda_imagemanipulation_amd.models import Pipeline
     from mpi_cuda_imagemanipulation_amd.utils.log import get_logger
 
+    rank_env = int(os.environ.get("RANK", "0"))
+    # every rank: the watchdog ends a rank that outlives the budget; rank 0's
+    # also writes the record (non-zero exit until the headline exists)
+    C.last_words_arm(json_fd if rank_env == 0 else -1, max(30.0, a.budget_s - elapsed_s()) + (0 if rank_env == 0 else 15),
+                     3)
     ctx = parallel.init({"rccl": "rccl", "host": "gloo", "gloo-gpu": "gloo-gpu"}[a.backend])
     log = get_logger("bench", ctx.rank)
     dev = ctx.device
@@ -140,7 +169,6 @@ def main():
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     W, H, Cc = a.width, a.height, a.channels
-    pipe = Pipeline(a.chain, overlap=not a.no_overlap, halo_depth=a.halo_depth)
 
     def barrier():
         if world > 1:
@@ -165,6 +193,9 @@ def main():
         if world > 1:
             dist.broadcast(t, 0)
         return [float(x) for x in t.tolist()]
+
+    # ---- who is running: the transport's and the runtime's own view ----
+    ids = parallel.world_identity(ctx)
 
     pinfo = C.plan_info(a.chain, Cc)
     iterable = pinfo["cin"] == pinfo["cout"]
@@ -199,68 +230,93 @@ def main():
                 ok &= same(get_rows(lo, lo + 4 * reach)[reach:3 * reach], ref[reach:3 * reach])
         return ok
 
-    dp = parallel.DistributedPipeline(ctx, pipe, W, H, Cc, autotune=not a.no_autotune)
+    part, active = C.plan_rows(H, world, R)
+    max_rows = max(r for _, r in part)
+    ws_max = max_rows * W * (pinfo["cin"] + pinfo["cout"])  # per-GPU bytes of one step (the same on every rank)
+    fits_mall = ws_max <= MALL_BYTES
+    # frames the headline rotates over: enough that F x working set > 2 x the
+    # Infinity Cache when one working set fits it (only for iterable chains)
+    nframes = a.frames if a.frames > 0 else (
+        min(8, int(math.ceil(2 * MALL_BYTES / max(1, ws_max))) + 1) if (fits_mall and iterable and dev) else 1)
+    cold = nframes > 1
+
+    # ---- headline engines: halo exchanged every step, F frames on one stream ----
+    pipe1 = Pipeline(a.chain, overlap=not a.no_overlap, halo_depth=1)
+    dp = parallel.DistributedPipeline(ctx, pipe1, W, H, Cc, autotune=not a.no_autotune, cold=cold)
     if a.band > 0:
         dp.engine.set_tuning([a.band] * len(dp.engine.bands), [-1] * len(dp.engine.bands))
     row0, rows = dp.stripe
-    part, active = C.plan_rows(H, world, R)
-
-    def run_steps(n):
-        # iterable chains ping-pong in one call; a chain that changes the channel
-        # count re-reads its (unchanged) input each step instead
-        if iterable:
-            dp.run(n)
-        else:
-            for _ in range(n):
-                dp.engine.rewind()
-                dp.run(1)
-
-    # ---- resident scope (headline): tune -> warmup -> K timed steps ----
-    dp.load_synthetic(a.seed)
+    frames = [dp] + [parallel.DistributedPipeline(ctx, pipe1, W, H, Cc, cold=cold) for _ in range(nframes - 1)]
+    stream = torch.cuda.Stream() if dev else None
+    if dev:
+        for f in frames:
+            f.use_stream(stream.cuda_stream)
+    for i, f in enumerate(frames):
+        f.load_synthetic(a.seed + i)
     dp.engine.tune()
-    if a.warmup > 0:
-        run_steps(a.warmup)
+    for f in frames[1:]:
+        f.engine.set_tuning(dp.engine.bands, dp.engine.caps, dp.engine.policies)
+
+    def step(i):
+        f = frames[i % nframes]
+        if not iterable:  # a chain that changes the channel count re-reads its (unchanged) input
+            f.engine.rewind()
+        f.run(1)
+
+    def sync_frames():
+        for f in frames:
+            f.synchronize()
+
+    for i in range(a.warmup):
+        step(i)
+    sync_frames()
     sync()
     barrier()
     sync()
     t0 = time.perf_counter()
-    run_steps(a.steps)
-    dp.synchronize()
+    for i in range(a.steps):
+        step(i)
+    sync_frames()
     sync()
     barrier()
     t1 = time.perf_counter()
     ms = max_over_ranks((t1 - t0) * 1e3)
     ms_per_step = ms / a.steps
     mpx = W * H / (ms_per_step * 1e-3) / 1e6
-    # device-event stage times of the timed call on rank 0 (compute = the whole
-    # run(K) call, halo = its last exchange)
+    # device-event stage times of frame 0's last step on rank 0
     stages = {"resident": {k: round(v, 4) for k, v in dp.stage_times().items() if k in ("compute", "halo")}}
-    log.info("resident: %.5f ms/step over %d steps", ms_per_step, a.steps)
+    log.info("resident: %.5f ms/step over %d steps (%d frame(s))", ms_per_step, a.steps, nframes)
 
-    # per-step device time distribution (events between calls; a call is one
-    # deep-halo block on > 1 rank, so its time is split over its steps)
-    per = max(1, dp.engine.halo_depth) if iterable else 1
+    # per-step device time distribution: events on the shared stream between
+    # steps, max(K, 20) steps (untimed by the host clock above)
     step_ms = None
     if dev and rows > 0:
-        calls = dp.engine.run_timed(max(per, a.steps), per, not iterable)
-        step_ms = stats([c / per for c in calls])
+        n_ev = max(a.steps, 20)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(n_ev + 1)]
+        ev[0].record(stream)
+        for i in range(n_ev):
+            step(i)
+            ev[i + 1].record(stream)
+        sync_frames()
+        ev[-1].synchronize()
+        step_ms = stats([ev[i].elapsed_time(ev[i + 1]) for i in range(n_ev)])
 
     def ramp(ms_target=30.0):
         """GPU clock ramp before a timed scope: the host-side checks between
         scopes leave the GPU idle long enough to drop its clock"""
         if not dev or rows == 0:
             return
-        dp.load_synthetic(a.seed)
         n = max(1, int(ms_target / max(1e-3, ms_per_step)))
-        run_steps(min(n, 2000))
-        dp.synchronize()
+        for i in range(min(n, 2000)):
+            step(i)
+        sync_frames()
 
     # ---- correctness of the timed engine (untimed, after the timed region):
     # n_it iterated steps through the same schedule vs the golden path on edge
     # crops and on this stripe's upper seam ----
     verify = None
     if not a.no_verify:
-        n_it = max(2, dp.engine.halo_depth + 1) if iterable else 1
+        n_it = 2 if iterable else 1
         dp.load_synthetic(a.seed)
         dp.run(n_it)
         out = dp.result_stripe()
@@ -299,16 +355,80 @@ def main():
         copy_ms = sorted(ev[i].elapsed_time(ev[i + 1]) for i in range(20))[10]
         del src, dst
         torch.cuda.empty_cache()
-    fits_mall = step_bytes <= MALL_BYTES
-    max_rows = max(r for _, r in part)
-    ws_max = max_rows * W * (pinfo["cin"] + pinfo["cout"])  # the same on every rank
 
-    scopes = {"resident": {"mpx_s": round(mpx, 1), "ms": round(ms_per_step, 5), "verified": verify}}
+    scopes = {"resident": {"mpx_s": round(mpx, 1), "ms": round(ms_per_step, 5), "verified": verify,
+                           "frames": nframes, "halo_depth": 1, "cache": "cold" if cold else (
+                               "exceeds the Infinity Cache" if not fits_mall else "warm")}}
+    med = step_ms["median"] if step_ms else None
+    rec = {
+        "metric": METRIC,
+        "value": round(mpx, 1),
+        "unit": "Mpixels/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_per_step, 5),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None if BASELINE_MPX is None else round(mpx / BASELINE_MPX, 3),
+        "dtype": "uint8 (int32 accumulate, exact)",
+        "backend": a.backend,
+        "data": "synthetic (seeded random pixels)",
+        "config": {
+            "model": a.chain,
+            "image": f"{W}x{H}x{Cc}",
+            "global_batch": 1,
+            "seq_len": H,
+            "parallelism": f"rowpart{world}+halo",
+            "scope": ("resident: halo exchange every step + full-frame filter per step"
+                      + (f", round-robin over {nframes} frames so every step reads HBM-cold data" if cold else "")),
+        },
+        "verified_vs_golden": verify,
+        # rank 0's per-step device time (HIP events between steps) and the
+        # same-box copy of the same per-GPU bytes (read + write)
+        "step_ms_device": step_ms,
+        "bytes_per_step_per_gpu": step_bytes,
+        "copy_roofline_ms": None if copy_ms is None else round(copy_ms, 5),
+        "frac_of_copy_roofline": None if not (copy_ms and med) else round(copy_ms / med, 4),
+        "hbm_tb_s": None if not med else round(step_bytes / (med * 1e-3) / 1e12, 3),
+        "working_set_fits_mall": fits_mall,
+        "frames": nframes,
+        "scopes": scopes,
+        "tuned": {"band_rows": dp.engine.bands, "occupancy_caps": dp.engine.caps, "policies": dp.engine.policies,
+                  "cold": cold},
+        "halo_depth": 1,
+        "stripe_rows": [r for _, r in part],
+        "stage_ms_rank0": stages,
+        "world": {"summary": parallel.identity_summary(ids), "ranks": ids},
+        "device": C.device_info(ctx.gpu) if dev else {},
+        "build": build_info(root),
+        "host": socket.gethostname(),
+        "torch": torch.__version__,
+        "budget": {"budget_s": a.budget_s, "comm_timeout_s": float(os.environ["STRIPE_COMM_TIMEOUT_S"]),
+                   "skipped": []},
+    }
+
+    def publish(final=False):
+        """rank 0: the record so far becomes the watchdog's last words (exit 0:
+        the headline is complete)"""
+        if rank == 0:
+            rec["elapsed_s"] = round(elapsed_s(), 1)
+            if not final:
+                rec["partial"] = "the wall-time budget ran out or the group was stopped during the extra scopes"
+            else:
+                rec.pop("partial", None)
+            C.last_words_set(json.dumps(rec), 0)
+
+    publish()
 
     def guarded(name, fn):
-        """run one extra scope; an exception is reported in the record (after every
-        rank agrees the scope failed) instead of ending the run without the
-        headline line"""
+        """run one extra scope unless the budget is spent; an exception is
+        reported in the record (after every rank agrees the scope failed)
+        instead of ending the run without the headline line"""
+        # every rank takes the same decision (rank 0's clock)
+        if from_root([1.0 if elapsed_s() > 0.6 * a.budget_s else 0.0])[0] > 0:
+            rec["budget"]["skipped"].append(name)
+            return
         ok, err = True, None
         try:
             fn()
@@ -317,44 +437,61 @@ def main():
             log.error("scope %s failed: %s", name, err)
         if not all_ok(ok):
             scopes.setdefault(name, {})["error"] = err or "failed on another rank"
+        publish()
 
-    def scope_cold():
-        # ---- resident scope, Infinity-Cache cold: rotate over enough stripe
-        # copies that each step's input was last touched > 256 MiB ago ----
-        cold_steps = a.steps if a.cold_steps < 0 else a.cold_steps
-        nrot = int(math.ceil(2 * MALL_BYTES / max(1, ws_max))) + 1
-        if cold_steps > 0 and ws_max <= MALL_BYTES and iterable and nrot <= 8:
-            engines = [dp] + [parallel.DistributedPipeline(ctx, pipe, W, H, Cc) for _ in range(nrot - 1)]
-            for e in engines[1:]:
-                e.engine.set_tuning(dp.engine.bands, dp.engine.caps)
-            for e in engines:
-                e.load_synthetic(a.seed)
-            ramp()
-            for i in range(2 * nrot):  # warm: every copy once
-                engines[i % nrot].run(1)
-            for e in engines:
-                e.synchronize()
-            sync()
-            barrier()
-            t0 = time.perf_counter()
-            for i in range(cold_steps):
-                engines[i % nrot].run(1)
-            for e in engines:
-                e.synchronize()
-            sync()
-            barrier()
-            cms = max_over_ranks((time.perf_counter() - t0) * 1e3) / cold_steps
-            scopes["resident_cold"] = {"mpx_s": round(W * H / (cms * 1e-3) / 1e6, 1), "ms": round(cms, 5),
-                                       "stripe_copies": nrot, "halo_every_step": True}
-            del engines
-        elif cold_steps > 0 and ws_max > MALL_BYTES:
-            scopes["resident_cold"] = {"same_as": "resident",
-                                       "note": f"per-GPU working set {ws_max} B exceeds the 256 MiB Infinity Cache"}
+    def scope_warm():
+        # ---- one frame iterated in place, halo every step (cache-warm when
+        # the working set fits the Infinity Cache) ----
+        if nframes == 1 or not iterable:
+            return
+        ramp()
+        sync()
+        barrier()
+        t0 = time.perf_counter()
+        dp.run(a.steps)
+        dp.synchronize()
+        sync()
+        barrier()
+        wms = max_over_ranks((time.perf_counter() - t0) * 1e3) / a.steps
+        scopes["resident_warm"] = {"mpx_s": round(W * H / (wms * 1e-3) / 1e6, 1), "ms": round(wms, 5),
+                                   "frames": 1, "halo_depth": 1}
+
+    def scope_deep():
+        # ---- communication-avoiding deep halo: one exchange of k*S rows per
+        # k steps (bit-identical), one frame ----
+        deep_steps = a.steps if a.deep_steps < 0 else a.deep_steps
+        if world == 1 or not iterable or deep_steps <= 0:
+            return
+        dd = parallel.DistributedPipeline(ctx, Pipeline(a.chain, overlap=not a.no_overlap, halo_depth=a.halo_depth),
+                                          W, H, Cc)
+        k = dd.engine.halo_depth
+        if k <= 1:
+            scopes["resident_deep"] = {"same_as": "resident_warm", "halo_depth": k}
+            return
+        dd.engine.set_tuning(dp.engine.bands, dp.engine.caps, dp.engine.policies)
+        n = k * int(math.ceil(deep_steps / k))  # whole exchange blocks
+        dd.load_synthetic(a.seed)
+        dd.run(2 * k)
+        dd.synchronize()
+        sync()
+        barrier()
+        t0 = time.perf_counter()
+        dd.run(n)
+        dd.synchronize()
+        sync()
+        barrier()
+        dms = max_over_ranks((time.perf_counter() - t0) * 1e3) / n
+        calls = dd.engine.run_timed(max(n, 20 * k), k, False) if dev and rows > 0 else []
+        scopes["resident_deep"] = {"mpx_s": round(W * H / (dms * 1e-3) / 1e6, 1), "ms": round(dms, 5),
+                                   "halo_depth": k, "steps": n, "frames": 1,
+                                   "step_ms_device": stats([c / k for c in calls])}
+        del dd
 
     def scope_dist():
         # ---- dist scopes (root frame -> scatter -> filter -> gather -> root) ----
         dist_chunks = 0
         if a.dist_steps > 0:
+            pipe = Pipeline(a.chain, overlap=not a.no_overlap)
             dd = parallel.DistributedPipeline(ctx, pipe, W, H, Cc, root_buffers=True)
             dd.engine.set_tuning(dp.engine.bands, dp.engine.caps)
             if rank == 0:
@@ -367,21 +504,20 @@ def main():
                 full = d.engine.store_root()
                 return all_ok(check_frame_rows(lambda lo, hi: full[lo:hi], cuts))
 
-            def time_dist(d, step):
+            def time_dist(d, step_fn):
                 ramp()
                 for _ in range(2):
-                    step()
+                    step_fn()
                 d.synchronize()
                 sync()
                 barrier()
                 t0 = time.perf_counter()
                 for _ in range(a.dist_steps):
-                    step()
+                    step_fn()
                 d.synchronize()
                 sync()
                 barrier()
-                dms = max_over_ranks((time.perf_counter() - t0) * 1e3) / a.dist_steps
-                return dms
+                return max_over_ranks((time.perf_counter() - t0) * 1e3) / a.dist_steps
 
             def seq_step():
                 dd.scatter()
@@ -478,38 +614,89 @@ def main():
             base = frame.ctypes.data
             pinned = shm is None or C.host_register(base, nbytes)
             mine = base + row0 * W * pinfo["cout"]
-            dp.load_synthetic(a.seed)
-            dp.synchronize()
-            dp.engine.run_to_host_ptr(mine, 8)
-            dp.synchronize()
-            barrier()
-            ok = None
-            full = None
-            if not a.no_verify:
-                full = frame.reshape(H, W, -1) if pinfo["cout"] > 1 else frame.reshape(H, W)
-                ok = all_ok(rank != 0 or check_frame_rows(lambda lo, hi: full[lo:hi], [r0 for r0, _ in part[1:active]]))
-            ramp()
-            dp.engine.run_to_host_ptr(mine, 8)
-            dp.synchronize()
-            sync()
-            barrier()
-            t0 = time.perf_counter()
-            for _ in range(a.ref_steps):
+            try:
+                dp.load_synthetic(a.seed)
+                dp.synchronize()
                 dp.engine.run_to_host_ptr(mine, 8)
                 dp.synchronize()
-                barrier()  # rank 0's window ends when every stripe is in its memory
-            rms = max_over_ranks((time.perf_counter() - t0) * 1e3) / a.ref_steps
-            scopes["ref_window"] = {"mpx_s": round(W * H / (rms * 1e-3) / 1e6, 1), "ms": round(rms, 5), "verified": ok,
-                                    "host_frame": "shared memory" if shm is not None else "pinned", "pinned": bool(pinned)}
-            stages["ref_window"] = {k: round(v, 4) for k, v in dp.stage_times().items() if k in ("compute", "d2h", "e2e")}
-            if shm is not None:
-                if pinned:
-                    C.host_unregister(base)
-                del frame, full
                 barrier()
-                shm.close()
-                if rank == 0:
-                    shm.unlink()
+                ok = None
+                full = None
+                if not a.no_verify:
+                    full = frame.reshape(H, W, -1) if pinfo["cout"] > 1 else frame.reshape(H, W)
+                    ok = all_ok(rank != 0 or check_frame_rows(lambda lo, hi: full[lo:hi],
+                                                              [r0 for r0, _ in part[1:active]]))
+                ramp()
+                dp.engine.run_to_host_ptr(mine, 8)
+                dp.synchronize()
+                sync()
+                barrier()
+                t0 = time.perf_counter()
+                for _ in range(a.ref_steps):
+                    dp.engine.run_to_host_ptr(mine, 8)
+                    dp.synchronize()
+                    barrier()  # rank 0's window ends when every stripe is in its memory
+                rms = max_over_ranks((time.perf_counter() - t0) * 1e3) / a.ref_steps
+                scopes["ref_window"] = {"mpx_s": round(W * H / (rms * 1e-3) / 1e6, 1), "ms": round(rms, 5),
+                                        "verified": ok, "host_frame": "shared memory" if shm is not None else "pinned",
+                                        "pinned": bool(pinned)}
+                stages["ref_window"] = {k: round(v, 4) for k, v in dp.stage_times().items()
+                                        if k in ("compute", "d2h", "e2e")}
+            finally:
+                if shm is not None:
+                    if pinned:
+                        C.host_unregister(base)
+                    del frame
+                    full = None
+                    barrier()
+                    shm.close()
+                    if rank == 0:
+                        shm.unlink()
+
+    def host_link(nbytes: int) -> dict:
+        """Same-box pinned host <-> device rates on this rank's stripe bytes:
+        H2D alone, D2H alone, and both directions at once (two streams), GB/s
+        per direction, median of 3.  The e2e scope cannot beat its slowest
+        direction, nor the concurrent rate when the link serialises them."""
+        h_src = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+        h_dst = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+        d_a = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        d_b = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        s_up, s_down = torch.cuda.Stream(), torch.cuda.Stream()
+
+        def timed(up, down):
+            res = []
+            for _ in range(4):
+                sync()
+                e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+                if up:
+                    e[0].record(s_up)
+                    with torch.cuda.stream(s_up):
+                        d_a.copy_(h_src, non_blocking=True)
+                    e[1].record(s_up)
+                if down:
+                    e[2].record(s_down)
+                    with torch.cuda.stream(s_down):
+                        h_dst.copy_(d_b, non_blocking=True)
+                    e[3].record(s_down)
+                sync()
+                res.append((e[0].elapsed_time(e[1]) if up else 0.0, e[2].elapsed_time(e[3]) if down else 0.0))
+            res = res[1:]
+            return [sorted(r[i] for r in res)[len(res) // 2] for i in (0, 1)]
+
+        h2d_ms, _ = timed(True, False)
+        _, d2h_ms = timed(False, True)
+        both_up, both_down = timed(True, True)
+        gbs = lambda ms: round(nbytes / (ms * 1e-3) / 1e9, 2) if ms > 0 else None  # noqa: E731
+        out = {"bytes": nbytes, "h2d_gb_s": gbs(h2d_ms), "d2h_gb_s": gbs(d2h_ms),
+               "both_h2d_gb_s": gbs(both_up), "both_d2h_gb_s": gbs(both_down),
+               "h2d_ms": round(h2d_ms, 3), "d2h_ms": round(d2h_ms, 3),
+               "both_ms": round(max(both_up, both_down), 3)}
+        # serialised: doing both at once takes about as long as one after the other
+        out["directions_serialise"] = bool(max(both_up, both_down) > 0.85 * (h2d_ms + d2h_ms))
+        del h_src, h_dst, d_a, d_b
+        torch.cuda.empty_cache()
+        return out
 
     def scope_e2e():
         # ---- e2e scope (pinned host stripe -> H2D -> filter -> D2H -> pinned host) ----
@@ -531,57 +718,34 @@ def main():
             scopes["e2e"] = {"mpx_s": round(W * H / (ems * 1e-3) / 1e6, 1), "ms": round(ems, 5)}
             stages["e2e"] = {k: round(v, 4) for k, v in dp.stage_times().items()
                              if k in ("h2d", "compute", "halo", "d2h", "e2e")}
+            if rows > 0:
+                hl = host_link(max(bytes_in, bytes_out))
+                # the floor the link allows this scope: both directions' bytes at
+                # the concurrent rates if they overlap, else one after the other
+                floor = hl["both_ms"] if not hl["directions_serialise"] else hl["h2d_ms"] + hl["d2h_ms"]
+                hl["e2e_floor_ms"] = round(floor, 3)
+                hl["e2e_frac_of_floor"] = round(floor / ems, 3) if ems > 0 else None
+                scopes["e2e"]["host_link_rank0"] = hl
 
-    for name, fn, on in (("resident_cold", scope_cold, True), ("dist", scope_dist, a.dist_steps > 0),
-                         ("ref_window", scope_ref, a.ref_steps > 0 and dev),
-                         ("e2e", scope_e2e, a.e2e_steps > 0 and dev)):
-        if on:
+    try:
+        for name, fn in (("resident_warm", scope_warm), ("resident_deep", scope_deep), ("dist", scope_dist),
+                         ("ref_window", scope_ref), ("e2e", scope_e2e)):
             guarded(name, fn)
+    except Exception as e:  # noqa: BLE001 - a collective between scopes failed (a peer died or stalled)
+        log.error("extra scopes abandoned: %s: %s", type(e).__name__, e)
+        rec["budget"]["abandoned"] = f"{type(e).__name__}: {e}"[:300]
+        if rank == 0:
+            publish()
+            C.last_words_emit()  # the headline is complete: report it, then leave
+            C.last_words_disarm()
+            sys.stderr.flush()
+            os._exit(0)
+        raise
 
+    publish(final=True)
     if rank == 0:
-        med = step_ms["median"] if step_ms else None
-        rec = {
-            "metric": METRIC,
-            "value": round(mpx, 1),
-            "unit": "Mpixels/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(ms_per_step, 5),
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": None if BASELINE_MPX is None else round(mpx / BASELINE_MPX, 3),
-            "dtype": "uint8 (int32 accumulate, exact)",
-            "backend": a.backend,
-            "data": "synthetic (seeded random pixels)",
-            "config": {
-                "model": a.chain,
-                "image": f"{W}x{H}x{Cc}",
-                "global_batch": 1,
-                "seq_len": H,
-                "parallelism": f"rowpart{world}+halo",
-                "scope": "resident: halo exchange + full-frame filter per step",
-            },
-            "verified_vs_golden": verify,
-            # rank 0's per-step device time (HIP events between steps) and the
-            # same-box copy of the same per-GPU bytes (read + write)
-            "step_ms_device": step_ms,
-            "bytes_per_step_per_gpu": step_bytes,
-            "copy_roofline_ms": None if copy_ms is None else round(copy_ms, 5),
-            "frac_of_copy_roofline": None if not (copy_ms and med) else round(copy_ms / med, 4),
-            "hbm_tb_s": None if not med else round(step_bytes / (med * 1e-3) / 1e12, 3),
-            "working_set_fits_mall": fits_mall,
-            "scopes": scopes,
-            "tuned": {"band_rows": dp.engine.bands, "occupancy_caps": dp.engine.caps},
-            "halo_depth": dp.engine.halo_depth,
-            "stripe_rows": [r for _, r in part],
-            "stage_ms_rank0": stages,
-            "device": C.device_info(ctx.gpu) if dev else {},
-            "build": build_info(root),
-            "host": socket.gethostname(),
-            "torch": torch.__version__,
-        }
-        os.write(json_fd, (json.dumps(rec) + "\n").encode())
+        C.last_words_emit()
+    C.last_words_disarm()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

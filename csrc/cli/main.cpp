@@ -294,6 +294,26 @@ int cmd_gen(const Args& a) {
 
 int cmd_info(const Args& a) {
   const int n = device_count();
+  if (a.get("format") == "json") {
+    // runtime identity as one JSON line: which HIP runtime / RCCL copies this
+    // process mapped (the Python path reports the same through C.runtime_libs)
+    int rt = 0;
+    if (hipRuntimeGetVersion(&rt) != hipSuccess) (void)hipGetLastError();
+    std::ostringstream js;
+    js << "{\"devices\":" << n << ",\"hip_runtime\":" << rt << ",\"rccl_version\":\"" << rccl_version()
+       << "\",\"libs\":{";
+    bool first = true;
+    for (const char* stem : {"librccl", "libamdhip64", "libhsa-runtime64"}) {
+      js << (first ? "" : ",") << "\"" << stem << "\":[";
+      first = false;
+      const auto v = mapped_libraries(stem);
+      for (size_t i = 0; i < v.size(); ++i) js << (i ? "," : "") << "\"" << v[i] << "\"";
+      js << "]";
+    }
+    js << "}}";
+    std::printf("%s\n", js.str().c_str());
+    return 0;
+  }
   std::printf("devices: %d\n", n);
   for (int d = 0; d < n; ++d) {
     hipDeviceProp_t p;
@@ -437,7 +457,7 @@ void usage() {
                "        [--no-overlap] [--no-pipeline] [--graphs] [--band ROWS] [--halo-depth K] [--dist-chunks K]\n"
                "  cmp   a.ppm b.ppm [--tol T]\n"
                "  gen   --synthetic WxHxC [--seed S] --output out.ppm\n"
-               "  info  [--chain C] [--channels C]\n");
+               "  info  [--chain C] [--channels C] [--format json]\n");
 }
 
 }  // namespace

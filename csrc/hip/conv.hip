@@ -442,12 +442,18 @@ __global__ __launch_bounds__(256, 2) void k_conv_i8(ConvI8Args ca) {
     for (int r = 0; r < 4; ++r)
 #pragma unroll
       for (int c = 0; c < C; ++c) {
-        // digit sums are exact in f32 (|D| <= 961 * 128 * 128 < 2^24) and the
-        // scales are powers of two; the three f32 FMAs round the result to
-        // ~2^-15 (an output changes only within ~1e-4 of a tie), and
-        // v_cvt_pk_u8_f32 rounds half to even and saturates
-        const float lo2 = __builtin_fmaf((float)acc[1][c][mt][r], s1, __builtin_fmaf((float)acc[0][c][mt][r], s0, bias));
-        const float v = ND == 3 ? __builtin_fmaf((float)acc[ND - 1][c][mt][r], s2, lo2) : lo2;
+        // a digit sum |D| <= K^2 * 128 * 128 reaches 1.78e7 > 2^24 at K = 33,
+        // so each goes to f32 as two exact parts (D - (D & 255) keeps <= 17
+        // significant bits, D & 255 <= 8); the scales are powers of two, the
+        // f32 FMAs round the result to ~2^-15 (an output changes only within
+        // ~1e-4 of a tie), and v_cvt_pk_u8_f32 rounds half to even and saturates
+        auto part = [&](int d, float s, float acc_in) __attribute__((always_inline)) {
+          const int D = acc[d][c][mt][r];
+          const int lo8 = D & 255;
+          return __builtin_fmaf((float)(D - lo8), s, __builtin_fmaf((float)lo8, s, acc_in));
+        };
+        const float lo2 = part(1, s1, part(0, s0, bias));
+        const float v = ND == 3 ? part(ND - 1, s2, lo2) : lo2;
         otile[(16 * mt + 4 * g + r) * kOS + (16 * wave + m) * C + c] = (uint8_t)__builtin_amdgcn_cvt_pk_u8_f32(v, 0, 0u);
       }
   __syncthreads();

@@ -175,8 +175,12 @@ void launch_stencil(const Pass& p, const PassConsts& pc, const PassLaunch& L, hi
   // smaller working set (the 16K x 2K stripe of an 8-GPU run, 8K^2 gray) keeps
   // the default policy so the next iteration reads its input from the cache
   // (8K^2 gray gaussian5: 0.030 ms default vs 0.034 ms nt).
+  // The size rule is only the default: the engine passes the policy it tuned
+  // (L.nt), and a cache-cold stripe (EngineConfig::cold: a stream of frames, or
+  // a working set evicted between steps) streams from HBM however small its
+  // pass is -- the data's temperature, not the pass size, is what matters.
   const int64_t pass_bytes = (int64_t)(n0 + n1) * L.W * (p.cin + p.cout);
-  bool nt = pass_bytes > dev::kNtMinBytes;
+  bool nt = L.nt >= 0 ? L.nt != 0 : pass_bytes > dev::kNtMinBytes;
   if (const char* e = std::getenv("STRIPE_NT")) nt = std::atoi(e) != 0;  // A/B switch
   // A pass that stays in the Infinity Cache is bound by L2 / fabric traffic: the
   // XCD-contiguous workgroup remap turns the halo rows that vertically adjacent
@@ -184,7 +188,7 @@ void launch_stencil(const Pass& p, const PassConsts& pc, const PassLaunch& L, hi
   // 0.0394-0.0401 -> 0.0372 ms at 8-row bands, profiles/r2/xcd_remap_stripe.txt).
   // A pass streaming from HBM gains nothing from it (round 1: FETCH_SIZE 1.40x ->
   // 1.15x of ideal, time unchanged, profiles/fetch_xcd_bands_16k_r1.txt).
-  a.nxcd = pass_bytes > dev::kNtMinBytes ? 0 : dev::kXcdCount;
+  a.nxcd = nt ? 0 : dev::kXcdCount;
   using namespace sdef;
   switch (p.sid) {
     case StencilId::Emboss3: dev::launch_filter<Emboss3>(p, a, tiles, n0, n1, band, nt, L.wgs, s); break;

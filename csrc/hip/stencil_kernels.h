@@ -843,13 +843,17 @@ inline void plan_bands(KArgs& a, dim3& grid, int tiles, int n0, int n1, int band
 // sobel 0.315 -> 0.293; direct emboss3 0.300 -> 0.283 at 3; the gray-prologue
 // direct kernels read 3 bytes per output byte and gain nothing).  The cap is an
 // LDS reservation (dynamic shared memory the kernel never touches) sized so
-// only `target` workgroups fit a CU's LDS; STRIPE_NT_WGS overrides (0 = no cap).
-inline size_t nt_lds_reserve(const void* fn, int target) {
+// only `target` workgroups fit a CU's LDS; STRIPE_NT_WGS overrides the cap of
+// HBM-streaming launches (stencil_cap; 0 = no cap).
+inline int env_nt_wgs() {
   static const int env = [] {
     const char* e = std::getenv("STRIPE_NT_WGS");
     return e ? std::atoi(e) : -1;
   }();
-  if (env >= 0) target = env;
+  return env;
+}
+
+inline size_t nt_lds_reserve(const void* fn, int target) {
   if (target <= 0) return 0;
   static std::mutex mu;
   static std::map<std::tuple<const void*, int, int>, size_t> cache;
@@ -873,6 +877,7 @@ inline size_t nt_lds_reserve(const void* fn, int target) {
 // and memory behaviour of the box: round-2 driver run);
 // wgs < 0 takes the family default, applied to HBM-streaming launches only.
 inline int stencil_cap(bool nt, int wgs, int family_default) {
+  if (nt && env_nt_wgs() >= 0) return env_nt_wgs();  // A/B runs pin the streaming cap only
   if (wgs >= 0) return wgs;
   return nt ? family_default : 0;
 }

@@ -20,6 +20,7 @@
 #include <functional>
 #include <memory>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "stripe/common.h"
@@ -44,15 +45,32 @@ class Comm {
   // (comm_timeout_s(), STRIPE_COMM_TIMEOUT_S) and abort the group on timeout
   // or on an asynchronous communicator error instead of hanging (Q9).
   virtual void wait(hipStream_t s);
+  // What the transport itself reports about this rank (RCCL: ncclCommCount,
+  // ncclCommCuDevice, ncclCommUserRank and the bounded init / pre-connect
+  // times): the analogue of MPI_Comm_size / rank (kernel.cu:106-107), recorded
+  // by the benchmark so a multi-GPU record proves N ranks on N devices.
+  virtual std::vector<std::pair<std::string, double>> identity() const {
+    return {{"rank", (double)rank()}, {"size", (double)size()}};
+  }
 };
 
 // ---- RCCL ----
+// Communicators are created non-blocking (ncclCommInitRankConfig, blocking = 0)
+// and every RCCL step that can wait on a peer -- init, the p2p connection
+// setup inside ncclGroupEnd, finalize -- is polled through
+// ncclCommGetAsyncError under comm_timeout_s() (await_progress) instead of
+// blocking.  Each rank's p2p peers (neighbours +-1 and the root) are connected
+// once at creation, inside the same bound, so a dead or late peer fails the
+// creation rather than the first halo exchange or scatter.
 using UniqueId = std::array<char, 128>;
 UniqueId rccl_unique_id();
 std::unique_ptr<Comm> make_rccl_comm(const UniqueId& id, int rank, int world, int device);
 // One process driving `devices.size()` GPUs (caller runs one thread per rank).
 std::vector<std::unique_ptr<Comm>> make_rccl_comms_all(const std::vector<int>& devices);
 std::string rccl_version();
+// p2p peers a rank connects at creation: the ranks next to it and the root
+// (the root: every rank).  Symmetric: r is in peers(q) iff q is in peers(r).
+std::vector<int> preconnect_peers(int rank, int world);
 
 // ---- in-process groups ----
 class LocalHub;
@@ -69,6 +87,11 @@ struct CallbackOps {
   std::function<void(void*, size_t, int)> recv;
   std::function<void()> group_end;
   std::function<void()> barrier;
+  // Optional: group_end only posts the group and `poll` reports its progress
+  // (0 done, 1 pending, 2 failed); the wait is bounded by comm_timeout_s()
+  // (await_progress), so a peer that never answers fails the group instead
+  // of blocking it.
+  std::function<int()> poll;
 };
 std::unique_ptr<Comm> make_callback_comm(int rank, int world, CallbackOps ops);
 

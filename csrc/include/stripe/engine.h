@@ -53,6 +53,12 @@ struct EngineConfig {
   std::vector<double> row_weights;  // non-empty: weighted row split, one weight per rank
                                 // (plan_rows_weighted; the link-aware split of the
                                 // root-resident dist step, plan_dist_split)
+  bool cold = false;            // the stripe's input is cache-cold at every step (a stream of
+                                // distinct frames, or other work evicting it in between):
+                                // stencil passes default to the HBM-streaming memory policy
+                                // whatever their size, and the autotuner times every candidate
+                                // on cold data (a rotation of scratch stripes larger than the
+                                // 256 MiB Infinity Cache) and tunes the policy too
   bool graphs = false;          // replay iterated chains from a captured hipGraph when a run()
                                 // involves no collective (single rank, or no halo exchange).
                                 // Off by default: measured on MI355X/ROCm 7, graph replay of
@@ -152,16 +158,20 @@ class Engine {
   int graph_launches() const { return graph_launches_; }
   // Iterations per chain-level halo exchange (0: one exchange per pass and iteration).
   int halo_depth() const { return depth_; }
-  // Tuned band heights and occupancy caps per pass (after autotune), for reporting.
+  // Tuned band heights, occupancy caps and memory policies per pass (after
+  // autotune), for reporting.
   std::vector<int> bands() const;
   std::vector<int> caps() const;
+  std::vector<int> policies() const;
   // Run the band / occupancy-cap autotune now (EngineConfig::autotune; otherwise
   // the first run() does it): keeps the tuning out of a timed region.
   void tune() {
     if (cfg_.autotune && !tuned_) autotune_bands();
   }
   // Adopt another engine's tuning (same chain and stripe shape; skips autotune).
-  void set_tuning(const std::vector<int>& bands, const std::vector<int>& caps);
+  // `policies` may be empty (keep each pass's memory policy).
+  void set_tuning(const std::vector<int>& bands, const std::vector<int>& caps,
+                  const std::vector<int>& policies = {});
 
   // ---- output ----
   void store_packed(void* dst, bool dst_device);          // own output stripe, packed
@@ -214,6 +224,7 @@ class Engine {
     Buffer luts;
     int band = 0;  // tuned stencil band height (0: kernel default / cfg.band)
     int wgs = -1;  // tuned occupancy cap (resident workgroups per CU; -1: family default)
+    int nt = -1;   // tuned memory policy (PassLaunch::nt; -1: cold ? streaming : size rule)
   };
   void autotune_bands();
   bool tuned_ = false;

@@ -53,6 +53,10 @@ struct PassLaunch {
   int band = 0;                  // rows per workgroup (0 = auto)
   int wgs = -1;                  // stencil occupancy cap, resident workgroups per CU
                                  // (-1: the kernel family's default, 0: no cap)
+  int nt = -1;                   // stencil memory policy: 1 HBM-streaming (nt stores, linear
+                                 // workgroup order), 0 cache-resident (default stores, XCD-aware
+                                 // order), -1 chosen by the launch's size against the
+                                 // Infinity Cache
   // Allocation view for buffer-descriptor kernels (branch-free OOB masking):
   // origin = base + org, zero row origin = in_base + in_zero; sizes < 2 GiB.
   const uint8_t* in_base = nullptr;

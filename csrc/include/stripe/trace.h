@@ -10,8 +10,10 @@
 //     (STRIPE_COMM_TIMEOUT_S, default 600 s) after which the group aborts.
 #pragma once
 
+#include <functional>
 #include <sstream>
 #include <string>
+#include <vector>
 
 namespace stripe {
 
@@ -30,13 +32,43 @@ class TraceRange {
 void trace_mark(const char* msg);
 
 // STRIPE_FAULT grammar: comma-separated "stage[@rank][:mode]".  stage is one of
-// load, scatter, halo, compute, gather, store, e2e; rank an integer or '*'
+// load, scatter, halo, compute, gather, store, e2e, dist (entry of the
+// pipelined root-frame step, Engine::run_dist); rank an integer or '*'
 // (default: every rank); mode "throw" (default: stripe::Error, which the group
-// drivers turn into a collective abort) or "exit" (std::_Exit(3): a crashed
-// process, for multi-process tests of the bounded waits).
+// drivers turn into a collective abort), "exit" (std::_Exit(3): a crashed
+// process, for multi-process tests of the bounded waits) or "stall" (sleep
+// 2 x STRIPE_COMM_TIMEOUT_S + 5 s, then exit: a live peer that never answers).
 void fault_point(const char* stage, int rank);
 
 double comm_timeout_s();
+
+// Bounded progress loop of an asynchronous communicator operation (RCCL
+// non-blocking init / group end / finalize, a callback comm's posted group):
+// `probe` is polled until it reports Done; Failed (its message in *err), the
+// `aborted` flag raised by another thread, or `limit_s` elapsed end the loop
+// by calling `give_up(message)` (which tears the communicator down) and
+// raising stripe::Error.  Returns the milliseconds spent.  The reference's
+// failure path is the hang this replaces (kernel.cu:111-114).
+enum class Progress : int { Done = 0, Pending = 1, Failed = 2 };
+// "Last words" of a benchmark process: one pre-formatted line that reaches
+// `fd` exactly once -- from last_words_emit() on the normal path, or, if the
+// run is still going at `deadline_s` (seconds from arming) or receives
+// SIGTERM (torchrun stopping the group after a peer died), from a native
+// watchdog thread / signal handler that writes it and ends the process with
+// `exit_code`.  Native, so a rank blocked inside a long native call (which
+// holds no Python frame to run a handler in) still reports.  The line is
+// replaced with last_words_set() as results accumulate.
+void last_words_arm(int fd, double deadline_s, int exit_code);
+void last_words_set(const std::string& line, int exit_code = -1);  // exit_code < 0: keep
+bool last_words_emit();  // writes the current line unless already written; true if this call wrote
+void last_words_disarm();
+
+// Paths of the shared objects mapped into this process whose file name starts
+// with `stem` (e.g. "librccl"), from /proc/self/maps: which HIP runtime / RCCL
+// copy a process actually runs (the benchmark record and a test pin it).
+std::vector<std::string> mapped_libraries(const std::string& stem);
+double await_progress(const std::string& what, double limit_s, const std::function<Progress(std::string*)>& probe,
+                      const std::function<bool()>& aborted, const std::function<void(const std::string&)>& give_up);
 
 // Leveled, rank-prefixed log lines on stderr (SURVEY §5 metrics / logging; the
 // reference prints with std::cout from rank 0 only, kernel.cu:186-188,230-232).

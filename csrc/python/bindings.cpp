@@ -215,7 +215,41 @@ PYBIND11_MODULE(_C, m) {
       .def("barrier", [](PyComm& c) {
         py::gil_scoped_release nogil;
         c.comm->barrier();
+      })
+      .def("abort", [](PyComm& c, const std::string& why) { c.comm->abort(why); })
+      .def("identity", [](const PyComm& c) {
+        py::dict d;
+        for (const auto& kv : c.comm->identity()) d[kv.first.c_str()] = kv.second;
+        return d;
       });
+  m.def("preconnect_peers", &preconnect_peers, py::arg("rank"), py::arg("world"));
+  // the bounded progress loop of the non-blocking communicators, driven by a
+  // Python probe (0 done, 1 pending, 2 failed): unit tests of the state machine
+  m.def("await_progress", [](const std::string& what, double limit_s, py::function probe, py::object aborted) {
+    py::list gave_up;
+    std::function<bool()> ab;
+    if (!aborted.is_none()) ab = [aborted]() { return aborted().cast<bool>(); };
+    const double ms = await_progress(
+        what, limit_s,
+        [&](std::string* err) {
+          const int st = probe().cast<int>();
+          if (st == 2) *err = "probe reported failure";
+          return st == 0 ? Progress::Done : st == 1 ? Progress::Pending : Progress::Failed;
+        },
+        ab, [&](const std::string& why) { gave_up.append(why); });
+    return ms;
+  }, py::arg("what"), py::arg("limit_s"), py::arg("probe"), py::arg("aborted") = py::none());
+  // HIP runtime / RCCL / HSA libraries mapped into this process (one of each
+  // expected: the extension resolves to the copies torch loaded)
+  m.def("last_words_arm", &last_words_arm, py::arg("fd"), py::arg("deadline_s"), py::arg("exit_code") = 3);
+  m.def("last_words_set", &last_words_set, py::arg("line"), py::arg("exit_code") = -1);
+  m.def("last_words_emit", &last_words_emit);
+  m.def("last_words_disarm", &last_words_disarm);
+  m.def("runtime_libs", []() {
+    py::dict d;
+    for (const char* stem : {"librccl", "libamdhip64", "libhsa-runtime64"}) d[stem] = mapped_libraries(stem);
+    return d;
+  });
   m.def("rccl_unique_id", []() {
     UniqueId id = rccl_unique_id();
     return py::bytes(id.data(), id.size());
@@ -265,6 +299,9 @@ PYBIND11_MODULE(_C, m) {
     d["l2_bytes"] = pr.l2CacheSize;
     d["lds_per_cu"] = (int64_t)pr.maxSharedMemoryPerMultiProcessor;
     d["pci_bus_id"] = pr.pciBusID;
+    char bdf[32] = {0};
+    if (hipDeviceGetPCIBusId(bdf, (int)sizeof bdf, dev) == hipSuccess) d["pci"] = std::string(bdf);
+    else (void)hipGetLastError();
     d["hip_runtime"] = rt;
     d["hip_driver"] = drv;
     d["rccl"] = rccl_version();
@@ -283,8 +320,15 @@ PYBIND11_MODULE(_C, m) {
     return c;
   });
   m.def("make_callback_comm", [](int rank, int world, py::function group_start, py::function send,
-                                 py::function recv, py::function group_end, py::function barrier) {
+                                 py::function recv, py::function group_end, py::function barrier, py::object poll) {
     CallbackOps ops;
+    if (!poll.is_none()) {
+      py::function pf = poll;
+      ops.poll = [pf]() {
+        py::gil_scoped_acquire g;
+        return pf().cast<int>();
+      };
+    }
     ops.group_start = [group_start]() {
       py::gil_scoped_acquire g;
       group_start();
@@ -308,7 +352,8 @@ PYBIND11_MODULE(_C, m) {
     auto c = std::make_unique<PyComm>();
     c->comm = make_callback_comm(rank, world, std::move(ops));
     return c;
-  });
+  }, py::arg("rank"), py::arg("world"), py::arg("group_start"), py::arg("send"), py::arg("recv"),
+     py::arg("group_end"), py::arg("barrier"), py::arg("poll") = py::none());
 
   // the callback comm's device-buffer face: takes over `host` (left empty)
   m.def("make_staged_comm", [](PyComm* host, int device) {
@@ -336,6 +381,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("root_buffers", &EngineConfig::root_buffers)
       .def_readwrite("autotune", &EngineConfig::autotune)
       .def_readwrite("graphs", &EngineConfig::graphs)
+      .def_readwrite("cold", &EngineConfig::cold)
       .def_readwrite("pipeline", &EngineConfig::pipeline)
       .def_readwrite("halo_depth", &EngineConfig::halo_depth)
       .def_readwrite("dist_chunks", &EngineConfig::dist_chunks)
@@ -440,6 +486,7 @@ PYBIND11_MODULE(_C, m) {
       }, py::arg("chunks") = 8)
       .def_property_readonly("bands", &Engine::bands)
       .def_property_readonly("caps", &Engine::caps)
+      .def_property_readonly("policies", &Engine::policies)
       .def("run_timed", [](Engine& e, int it, int per, bool rewind_each) {
         py::gil_scoped_release rel;
         return e.run_timed(it, per, rewind_each);
@@ -457,7 +504,8 @@ PYBIND11_MODULE(_C, m) {
         py::gil_scoped_release nogil;
         e.run_to_host(reinterpret_cast<void*>(p), chunks);
       }, py::arg("ptr"), py::arg("chunks") = 8)
-      .def("set_tuning", &Engine::set_tuning)
+      .def("set_tuning", &Engine::set_tuning, py::arg("bands"), py::arg("caps"),
+           py::arg("policies") = std::vector<int>{})
       .def("tune", [](Engine& e) {
         py::gil_scoped_release nogil;
         e.tune();

@@ -5,6 +5,7 @@
 // group_end() completes this rank's receives, then waits for its sends to be
 // consumed (so the sender may reuse its buffer afterwards).
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
@@ -15,6 +16,7 @@
 
 #include "stripe/comm.h"
 #include "stripe/kernels.h"
+#include "stripe/trace.h"
 
 namespace stripe {
 
@@ -211,16 +213,59 @@ class CallbackComm final : public Comm {
   int size() const override { return world_; }
   const char* backend() const override { return "callback"; }
   bool device_buffers() const override { return false; }
-  void group_start() override { ops_.group_start(); }
-  void send(const void* buf, size_t bytes, int peer, hipStream_t) override { ops_.send(buf, bytes, peer); }
-  void recv(void* buf, size_t bytes, int peer, hipStream_t) override { ops_.recv(buf, bytes, peer); }
-  void group_end() override { ops_.group_end(); }
-  void barrier() override { ops_.barrier(); }
-  void abort(const std::string& why) override { fail("callback comm aborted: " + why); }
+  void group_start() override {
+    enter();
+    ops_.group_start();
+  }
+  void send(const void* buf, size_t bytes, int peer, hipStream_t) override {
+    enter();
+    ops_.send(buf, bytes, peer);
+  }
+  void recv(void* buf, size_t bytes, int peer, hipStream_t) override {
+    enter();
+    ops_.recv(buf, bytes, peer);
+  }
+  void group_end() override {
+    enter();
+    ops_.group_end();
+    if (!ops_.poll) return;
+    // posted group: bounded progress polling (the same state machine as the
+    // RCCL communicator's non-blocking group end)
+    await_progress(
+        "callback comm group on rank " + std::to_string(rank_), comm_timeout_s(),
+        [&](std::string* err) {
+          const int st = ops_.poll();
+          if (st == 0) return Progress::Done;
+          if (st == 1) return Progress::Pending;
+          *err = "transport reported failure";
+          return Progress::Failed;
+        },
+        [&] { return aborted_.load(); }, [&](const std::string& why) { mark(why); });
+  }
+  void barrier() override {
+    enter();
+    ops_.barrier();
+  }
+  // flag only: the rank's driving thread fails at its next call (or inside a
+  // posted group's progress loop)
+  void abort(const std::string& why) override { mark(why); }
 
  private:
+  void mark(const std::string& why) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!aborted_.load()) why_ = why;
+    aborted_.store(true);
+  }
+  void enter() {
+    if (!aborted_.load()) return;
+    std::lock_guard<std::mutex> lk(mu_);
+    fail("callback comm of rank " + std::to_string(rank_) + " was aborted: " + why_);
+  }
   int rank_, world_;
   CallbackOps ops_;
+  std::mutex mu_;
+  std::atomic<bool> aborted_{false};
+  std::string why_;
 };
 
 // Device-buffer face of a host-buffer communicator (gloo callbacks): N

@@ -16,7 +16,10 @@ from __future__ import annotations
 
 import ctypes
 import datetime
+import json
 import os
+import socket
+import threading
 from dataclasses import dataclass
 
 import numpy as np
@@ -55,11 +58,19 @@ def _host_view(ptr: int, n: int) -> "torch.Tensor":
 
 class GlooComm:
     """Callback communicator: the engine's grouped send/recv on host buffers,
-    executed as torch.distributed P2P ops (gloo)."""
+    executed as torch.distributed P2P ops (gloo).
+
+    group_end only posts the batch; the native side polls `poll` under
+    STRIPE_COMM_TIMEOUT_S (the same bounded state machine as the non-blocking
+    RCCL communicator), so a peer that never posts its half fails the group
+    with a message instead of blocking it."""
 
     def __init__(self, group=None):
         self.group = group
         self.ops = []
+        self.done = threading.Event()
+        self.done.set()
+        self.err = None
 
     def group_start(self):
         self.ops = []
@@ -71,17 +82,41 @@ class GlooComm:
         self.ops.append(dist.P2POp(dist.irecv, _host_view(ptr, n), peer, self.group))
 
     def group_end(self):
-        if self.ops:
-            for r in dist.batch_isend_irecv(self.ops):
-                r.wait()
+        works = dist.batch_isend_irecv(self.ops) if self.ops else []
         self.ops = []
+        self.done = threading.Event()
+        self.err = None
+        if not works:
+            self.done.set()
+            return
+        # gloo p2p works only progress inside wait(): a helper thread waits on
+        # them and `poll` reads its state (a stalled peer leaves the helper
+        # blocked until the process group's own timeout; the native side has
+        # given up and raised by then)
+
+        def waiter():
+            try:
+                for w in works:
+                    w.wait()
+            except Exception as e:  # noqa: BLE001 - reported to the native side as a failed group
+                self.err = e
+            finally:
+                self.done.set()
+
+        threading.Thread(target=waiter, daemon=True).start()
+
+    def poll(self) -> int:
+        """0: every posted op completed, 1: pending, 2: an op failed."""
+        if not self.done.is_set():
+            return 1
+        return 2 if self.err is not None else 0
 
     def barrier(self):
         dist.barrier(group=self.group)
 
     def native(self, rank: int, world: int):
         return C.make_callback_comm(rank, world, self.group_start, self.send, self.recv, self.group_end,
-                                    self.barrier)
+                                    self.barrier, self.poll)
 
 
 def init(backend: str = "auto") -> DistContext:
@@ -130,15 +165,57 @@ def init(backend: str = "auto") -> DistContext:
     return DistContext(rank, world, local_rank, device, comm, gpu, backend)
 
 
+def rank_identity(ctx: DistContext) -> dict:
+    """What this rank's transport and runtime say about it: the communicator's
+    own view (RCCL: ncclCommCount / ncclCommCuDevice / ncclCommUserRank and the
+    bounded init / pre-connect times), the GPU's PCI address, and the HIP
+    runtime / RCCL libraries actually mapped into the process."""
+    d = {"rank": ctx.rank, "world": ctx.world, "transport": ctx.transport, "gpu": ctx.gpu,
+         "host": socket.gethostname(), "pid": os.getpid()}
+    if ctx.comm is not None:
+        d["comm"] = {k: (int(v) if float(v).is_integer() else round(float(v), 3)) for k, v in ctx.comm.identity().items()}
+    if ctx.device:
+        info = C.device_info(ctx.gpu)
+        d["pci"] = info.get("pci")
+        d["hip_runtime"] = info.get("hip_runtime")
+    d["rccl_version"] = C.rccl_version()
+    d["libs"] = C.runtime_libs()
+    return d
+
+
+def world_identity(ctx: DistContext) -> list:
+    """rank_identity of every rank, gathered on every rank (rank order)."""
+    mine = rank_identity(ctx)
+    if ctx.world == 1:
+        return [mine]
+    out = [None] * ctx.world
+    dist.all_gather_object(out, mine)
+    return out
+
+
+def identity_summary(ids: list) -> dict:
+    """Checks over world_identity(): one distinct GPU per rank, the
+    communicator's rank count equal to the world size on every rank, and one
+    copy of each runtime library per process, the same everywhere."""
+    pcis = [(i.get("host"), i.get("pci")) for i in ids]
+    counts = {i.get("comm", {}).get("nccl_count") for i in ids}
+    libsets = {json.dumps(i.get("libs"), sort_keys=True) for i in ids}
+    one_copy = all(len(v) <= 1 for i in ids for v in (i.get("libs") or {}).values())
+    return {"ranks": len(ids), "distinct_gpus": len(set(pcis)), "nccl_count": sorted(c for c in counts if c is not None),
+            "devices": [i.get("comm", {}).get("nccl_device", i.get("gpu")) for i in ids],
+            "same_libs_everywhere": len(libsets) == 1, "one_copy_per_lib": one_copy}
+
+
 class DistributedPipeline:
     """Per-rank handle on the native engine for one image geometry."""
 
     def __init__(self, ctx: DistContext, pipeline, W: int, H: int, Cc: int = 3, root_buffers: bool = False,
-                 autotune: bool = False, row_weights=None):
+                 autotune: bool = False, row_weights=None, cold: bool = False):
         self.ctx = ctx
         cfg = pipeline.config(W, H, Cc, "device" if ctx.device else "host",
                               device=ctx.gpu if ctx.device else -1, autotune=autotune, row_weights=row_weights)
         cfg.root_buffers = root_buffers
+        cfg.cold = bool(cold)  # stream of cache-cold frames: streaming policy, cold autotune
         self.engine = C.Engine(cfg, ctx.comm)
         self.W, self.H, self.C = W, H, Cc
 
@@ -178,6 +255,11 @@ class DistributedPipeline:
     def synchronize(self):
         self.engine.synchronize()
 
+    def use_stream(self, stream_handle: int):
+        """Queue this engine's work on an external HIP stream (e.g. a torch
+        stream shared by several engines, which then run in issue order)."""
+        self.engine.use_external_stream(int(stream_handle))
+
 
 def run_local_group(pipeline, image: np.ndarray, ranks: int, backend: str = "host", iterations: int = 1):
     """N in-process ranks (threads): 'local' shares this process's GPU, 'host' uses the CPU."""
@@ -209,4 +291,4 @@ def probe_link_rate(ctx: DistContext, nbytes: int = 64 << 20, reps: int = 3) -> 
 
 
 __all__ = ["DistContext", "GlooComm", "init", "DistributedPipeline", "plan_rows", "plan_rows_weighted", "dist_split",
-           "probe_link_rate", "run_local_group"]
+           "probe_link_rate", "run_local_group", "rank_identity", "world_identity", "identity_summary"]

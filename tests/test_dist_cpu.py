@@ -102,8 +102,9 @@ def test_gloo_iterated(tmp_path, C):
 
 @pytest.mark.parametrize("nproc,depth", [(2, 0), (3, 3)])
 def test_bench_host_backend_multi_rank(tmp_path, nproc, depth):
-    """bench.py under torchrun on the host engine + gloo; depth 3 runs the
-    deep-halo schedule across processes (exchange every 3 steps, 7 steps)."""
+    """bench.py under torchrun on the host engine + gloo; the headline exchanges
+    every step, and depth 3 runs the resident_deep scope's schedule across
+    processes (exchange every 3 steps, 7 steps rounded up to 9)."""
     port = _free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus",
@@ -120,8 +121,10 @@ def test_bench_host_backend_multi_rank(tmp_path, nproc, depth):
         assert k in rec
     assert rec["n_gpus"] == nproc and rec["steps"] == (7 if depth else 3) and rec["value"] > 0
     assert rec["verified_vs_golden"] is True
+    assert rec["halo_depth"] == 1  # the headline exchanges every step
+    deep = rec["scopes"]["resident_deep"]
     if depth:
-        assert rec["halo_depth"] == depth
+        assert deep["halo_depth"] == depth and deep["steps"] % depth == 0
 
 
 @pytest.mark.parametrize("nproc,preset,chain,chunks", [(3, None, "gaussian5,sobel", 0), (2, "ref-cpu", None, 0),

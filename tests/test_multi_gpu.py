@@ -1,6 +1,6 @@
 """Real multi-GPU runs (one process per GPU over RCCL), skipped on 1-GPU boxes.
 
-bench.py under torchrun on N = 2 (and 4 when present) GPUs: the iterated
+bench.py under torchrun on N = 2, 4 and 8 GPUs when present: the iterated
 deep-halo schedule and the dist scope must verify against the golden path on
 the stripe seams.  The CPU (gloo) and single-GPU (local ranks) suites cover
 the same partition/halo logic; this checks the RCCL transport itself.
@@ -33,7 +33,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("n", [2, 4])
+@pytest.mark.parametrize("n", [2, 4, 8])
 @pytest.mark.parametrize("chain,depth", [("gaussian5", 0), ("gaussian5", 1), ("sobel", 0), ("blur:9", 0)])
 def test_torchrun_bench_rccl(n, chain, depth):
     if _ngpus() < n:
@@ -50,6 +50,14 @@ def test_torchrun_bench_rccl(n, chain, depth):
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == n and rec["value"] > 0
     assert rec["verified_vs_golden"] is True
+    # RCCL's own view: n ranks in the communicator, n distinct GPUs, one
+    # runtime / RCCL copy per process, the same in every process
+    summ = rec["world"]["summary"]
+    assert summ["ranks"] == n and summ["distinct_gpus"] == n and summ["nccl_count"] == [n]
+    assert sorted(summ["devices"]) == list(range(n))
+    assert summ["one_copy_per_lib"] and summ["same_libs_everywhere"]
+    for sc in rec["scopes"].values():
+        assert "error" not in sc, sc
 
 
 @pytest.mark.parametrize("n,chunks", [(1, 0), (2, 0), (4, 0), (2, 4), (4, 8)])

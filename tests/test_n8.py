@@ -51,7 +51,10 @@ def test_bench_host_8_processes(tmp_path):
     rec = recs[0]
     assert rec["n_gpus"] == N and rec["steps"] == 9 and rec["value"] > 0
     assert rec["verified_vs_golden"] is True
-    assert rec["halo_depth"] >= 2  # auto deep halo at 200-row stripes
+    assert rec["halo_depth"] == 1  # the headline exchanges every step
+    assert rec["scopes"]["resident_deep"]["halo_depth"] >= 2  # auto deep halo at 200-row stripes
+    summ = rec["world"]["summary"]
+    assert summ["ranks"] == N and summ["one_copy_per_lib"] and summ["same_libs_everywhere"]
     assert rec["stripe_rows"] == [200] * N
     assert rec["scopes"]["dist_sequential"]["verified"] is True
 

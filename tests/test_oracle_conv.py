@@ -159,6 +159,29 @@ def test_gpu_conv_lsb_vs_torch(m, rng, K, Cc):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("lsb", [False, True])
+@pytest.mark.parametrize("Cc", [1, 3])
+def test_gpu_conv33_uniform_box_saturated(m, rng, lsb, Cc):
+    # K = 33 goes to the i8 digit kernel, where a top-digit sum over a uniform
+    # box on saturated pixels reaches 1089 * 128 * 127 > 2^24: the
+    # epilogue converts each sum in two exact parts, so the result stays the
+    # correctly rounded one
+    K = 33
+    w = oracle.f32_weights(np.full((K, K), 1.0 / (K * K)))
+    img = np.where(rng.random((120, 260)) < 0.5, 0, 255).astype(np.uint8)
+    img[:, :130] = 0
+    img[:60, 130:] = 255
+    if Cc == 3:
+        img = np.stack([img, 255 - img, img], axis=-1)
+    chain = _conv_chain(w) + (":lsb" if lsb else "")
+    got = _gpu(m, img, chain, "reflect101")
+    r = oracle.compare(got, oracle.torch_sums(img, w, "reflect101", device="cuda"), GPU_BAND)
+    assert r["max_diff"] <= 1, r
+    if not lsb:
+        assert r["mismatch_outside_ties"] == 0, r
+
+
+@pytest.mark.gpu
 def test_gpu_conv_lsb_falls_back_when_unsafe(m, rng):
     # one dominant tap: 16-bit digits of the small ones could miss by >= 0.45
     # LSB, so the pass runs on 24-bit digits and stays exact except ties

@@ -1,0 +1,240 @@
+"""Bounded communicator progress, pre-connect topology, runtime identity and
+the benchmark's hang-proofing.
+
+The reference's failure path is a hang: a rank that errors returns 1 without
+MPI_Abort and its peers wait in MPI forever (kernel.cu:111-114).
+Here every wait of a non-blocking communicator runs through one state
+machine, await_progress (RCCL init / group end / pre-connect; the gloo
+callback comm's posted groups), tested below through its Python hook, through
+a callback communicator driven by an engine, and across processes.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+import time
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _seq(states):
+    it = iter(states)
+    last = [states[-1]]
+
+    def probe():
+        try:
+            last[0] = next(it)
+        except StopIteration:
+            pass
+        return last[0]
+
+    return probe
+
+
+def test_await_progress_done_after_pending(C):
+    ms = C.await_progress("op", 5.0, _seq([1, 1, 1, 0]))
+    assert ms >= 0
+
+
+def test_await_progress_failure_raises(C):
+    with pytest.raises(Exception, match="op failed"):
+        C.await_progress("op", 5.0, _seq([1, 2]))
+
+
+def test_await_progress_timeout_is_bounded(C):
+    t0 = time.time()
+    with pytest.raises(Exception, match="did not complete within"):
+        C.await_progress("stuck op", 0.3, lambda: 1)
+    took = time.time() - t0
+    assert 0.3 <= took < 5
+
+
+def test_await_progress_sees_abort_flag(C):
+    calls = []
+
+    def aborted():
+        calls.append(1)
+        return len(calls) > 3
+
+    with pytest.raises(Exception, match="aborted while waiting"):
+        C.await_progress("op", 30.0, lambda: 1, aborted)
+
+
+@pytest.mark.parametrize("world", range(1, 10))
+def test_preconnect_peers_symmetric(C, world):
+    peers = [set(C.preconnect_peers(r, world)) for r in range(world)]
+    for r in range(world):
+        assert r not in peers[r]
+        for q in peers[r]:
+            assert r in peers[q], (r, q)
+        # neighbours +-1 (halo exchange) and the root (scatter / gather)
+        need = {q for q in (r - 1, r + 1, 0) if 0 <= q < world and q != r}
+        assert need <= peers[r]
+    assert peers[0] == set(range(1, world))
+
+
+def _callback_engine(C, poll, world=2, rank=0):
+    """rank `rank` of a `world`-rank host engine over a callback comm whose
+    groups never complete (poll) -- nobody answers the halo exchange"""
+    import mpi_cuda_imagemanipulation_amd as m
+
+    noop = lambda *a: None  # noqa: E731
+    comm = C.make_callback_comm(rank, world, noop, noop, noop, noop, noop, poll)
+    cfg = m.models.Pipeline("gaussian5", halo_depth=1).config(64, 40, 3, "host")
+    e = C.Engine(cfg, comm)
+    e.load_synthetic(1)
+    return e, comm
+
+
+def test_callback_comm_posted_group_times_out(C, monkeypatch):
+    monkeypatch.setenv("STRIPE_COMM_TIMEOUT_S", "0.5")
+    e, _ = _callback_engine(C, lambda: 1)
+    t0 = time.time()
+    with pytest.raises(Exception, match="callback comm group on rank 0 did not complete"):
+        e.run(1)
+    assert time.time() - t0 < 10
+
+
+def test_callback_comm_failed_group_raises(C):
+    e, _ = _callback_engine(C, lambda: 2)
+    with pytest.raises(Exception, match="transport reported failure"):
+        e.run(1)
+
+
+def test_callback_comm_abort_flag(C):
+    e, comm = _callback_engine(C, lambda: 0)
+    e.run(1)  # completes (poll: done)
+    comm.abort("peer 1 failed")
+    with pytest.raises(Exception, match="was aborted: peer 1 failed"):
+        e.run(1)
+
+
+def test_callback_comm_identity_default(C):
+    noop = lambda *a: None  # noqa: E731
+    comm = C.make_callback_comm(1, 3, noop, noop, noop, noop, noop)
+    assert comm.identity() == {"rank": 1.0, "size": 3.0}
+
+
+def test_one_runtime_copy_per_process(C):
+    # torch (imported by the loader first) and the extension share one HIP
+    # runtime, one RCCL and one HSA runtime: the extension resolves to the
+    # copies torch mapped (same SONAMEs), never to a second stack
+    libs = C.runtime_libs()
+    for stem in ("libamdhip64", "librccl", "libhsa-runtime64"):
+        assert len(libs[stem]) == 1, (stem, libs[stem])
+    import torch
+
+    tlib = os.path.join(os.path.dirname(torch.__file__), "lib")
+    assert libs["librccl"][0].startswith(tlib), libs
+    assert libs["libamdhip64"][0].startswith(tlib), libs
+
+
+def test_cli_binds_the_same_rccl_as_python(C):
+    # `stripe info` reports the libraries it mapped: the CLI runs the same
+    # HIP runtime / RCCL build as the Python path (RUNPATH: torch's lib first)
+    exe = os.path.join(ROOT, "bin", "stripe")
+    if not os.path.exists(exe):
+        pytest.skip("CLI not built")
+    r = subprocess.run([exe, "info", "--format", "json"], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES=""))
+    assert r.returncode == 0, r.stderr
+    info = json.loads(r.stdout.strip().splitlines()[-1])
+    libs = C.runtime_libs()
+    assert info["libs"]["librccl"] == libs["librccl"]
+    assert info["libs"]["libamdhip64"] == libs["libamdhip64"]
+    assert info["rccl_version"] == C.rccl_version()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+STALL_WORKER = r'''
+import os, sys, time
+sys.path.insert(0, os.environ["STRIPE_ROOT"])
+from mpi_cuda_imagemanipulation_amd import parallel, models
+ctx = parallel.init("gloo")
+dp = parallel.DistributedPipeline(ctx, models.Pipeline("gaussian5", halo_depth=1), 64, 48, 3)
+dp.load_synthetic(1)
+t0 = time.time()
+try:
+    dp.run(1)
+    print("RANK", ctx.rank, "FINISHED", flush=True)
+except Exception as e:
+    print("RANK", ctx.rank, "ERROR after %.1fs:" % (time.time() - t0), str(e)[:300], flush=True)
+    os._exit(7)
+'''
+
+
+def test_stalled_peer_bounded_by_comm_timeout(tmp_path):
+    """Rank 1 is alive but never answers its halo exchange (STRIPE_FAULT
+    halo@1:stall); rank 0's posted gloo group must fail at the comm bound
+    with a message naming the wait, not block."""
+    script = tmp_path / "w.py"
+    script.write_text(STALL_WORKER)
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), STRIPE_ROOT=ROOT, STRIPE_FAULT="halo@1:stall", STRIPE_COMM_TIMEOUT_S="4",
+                   CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT))
+    try:
+        o0, _ = procs[0].communicate(timeout=90)
+    finally:
+        procs[1].kill()
+        procs[1].communicate()
+    out = o0.decode(errors="replace")
+    assert procs[0].returncode == 7, out
+    assert "callback comm group on rank 0 did not complete within" in out, out
+
+
+def _bench(tmp_path, n, extra, env_extra, timeout=240):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", str(n), "--backend", "host", "--width", "96", "--height", "64", "--steps", "3", "--warmup", "1",
+           "--dist-steps", "2", *extra]
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1", **env_extra)
+    t0 = time.time()
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout, cwd=str(tmp_path))
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    return r, lines, time.time() - t0
+
+
+def test_bench_peer_exit_still_reports_headline(tmp_path):
+    """A peer dies in an extra scope (STRIPE_FAULT=scatter@1:exit, the dist
+    scope's scatter): the headline line still prints, once."""
+    r, lines, took = _bench(tmp_path, 2, ["--comm-timeout-s", "20", "--budget-s", "120"],
+                            {"STRIPE_FAULT": "scatter@1:exit"})
+    assert len(lines) == 1, r.stdout + r.stderr[-3000:]
+    rec = json.loads(lines[0])
+    assert rec["value"] > 0 and rec["verified_vs_golden"] is True and rec["n_gpus"] == 2
+    assert took < 120
+
+
+def test_bench_stalled_peer_within_budget(tmp_path):
+    """A live peer stalls in an extra scope: rank 0 reports the headline
+    within the wall-time budget instead of running into the driver's limit."""
+    r, lines, took = _bench(tmp_path, 2, ["--comm-timeout-s", "5", "--budget-s", "60"],
+                            {"STRIPE_FAULT": "scatter@1:stall"})
+    assert len(lines) == 1, r.stdout + r.stderr[-3000:]
+    rec = json.loads(lines[0])
+    assert rec["value"] > 0 and rec["verified_vs_golden"] is True
+    assert rec["elapsed_s"] < 60
+
+
+def test_bench_budget_skips_extra_scopes(tmp_path):
+    # a budget already spent before the extra scopes: they are skipped and
+    # listed, the headline is complete, the run exits 0
+    r, lines, _ = _bench(tmp_path, 2, ["--budget-s", "0.01"], {})
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert len(lines) == 1
+    rec = json.loads(lines[0])
+    assert set(rec["budget"]["skipped"]) >= {"dist", "resident_deep"}
+    assert "partial" not in rec
