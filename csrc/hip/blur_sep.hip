@@ -631,7 +631,7 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
   // pairs / 1 wave, 0.40-0.43 ms against 0.55 ms at the exact mode's 2 / 1 / 2
   // (the narrower strip's 2.5x input overfetch now sets the time); gray keeps
   // the exact kernels.
-  // Workgroup-shared windows (tools/ab/r3/r3_blur_nw.sh, r3_blur_nw8.sh): RGB
+  // Workgroup-shared windows (round-3 A/B runs, profiles/r3/blur/): RGB
   // exact at 2 / 1 / 2 0.556 -> 0.499-0.505 ms with 4 or 8 waves sharing a
   // window; lsb 0.423-0.426 (4 / 2 / 1 per wave) -> 0.418-0.420 (4 waves) ->
   // 0.386-0.393 (8 waves: 304 staged pixels per row for 256 outputs, one

@@ -213,6 +213,12 @@ class Engine {
 
   void synchronize();
   const PhaseTimes& times() const { return times_; }
+  // Device-event stage timing (on by default).  Each timestamped event costs
+  // the GPU ~8 us per step between dependent kernels (measured on MI355X,
+  // tools/hostbench.py: a 16384x2048 RGB gaussian5 step 57.6 -> 49.4 us), so
+  // a step loop that times itself another way turns it off.
+  void set_stage_timing(bool on) { stage_timing_ = on; }
+  bool stage_timing() const { return stage_timing_; }
   // device pointer + pitch of the current input/output stripe origins (for tests)
   const uint8_t* input_origin() const;
   const uint8_t* output_origin() const;
@@ -232,6 +238,7 @@ class Engine {
   uint8_t* root_origin(const Buffer& b, int C) const;
   void exchange_halo(uint8_t* org, int C, int R, hipStream_t s);
   bool time_halo_ = true;  // record the halo stage events (last iteration of a run only)
+  bool stage_timing_ = true;  // set_stage_timing
   void run_pass(const Pass& p, const uint8_t* in, uint8_t* out);
   bool pipelined_ok() const;
   int chain_reach() const;  // sum of the chain's radii if every pass can extend its rows, else 0

@@ -545,6 +545,7 @@ PYBIND11_MODULE(_C, m) {
         e.synchronize();
       })
       .def_property_readonly("times", [](const Engine& e) { return e.times(); })
+      .def_property("stage_timing", &Engine::stage_timing, &Engine::set_stage_timing)
       .def_property_readonly("graph_launches", &Engine::graph_launches);
 
   m.def("run_local_group", [](const EngineConfig& cfg, int world, const U8Array& a, int iterations) {

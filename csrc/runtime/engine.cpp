@@ -118,7 +118,10 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
     HIP_CHECK(hipStreamCreateWithFlags(&s_comm_, hipStreamNonBlocking));
     own_streams_ = true;
     own_compute_ = true;
-    for (auto& e : ev_) HIP_CHECK(hipEventCreate(&e));
+    // ev_[0..5] only order streams (no timestamps: a timing event costs the
+    // GPU several microseconds per record); ev_[6..7] time the autotune
+    for (int i = 0; i < 8; ++i)
+      HIP_CHECK(hipEventCreateWithFlags(&ev_[i], i >= 6 ? hipEventDefault : hipEventDisableTiming));
     for (auto& pr : sev_)
       for (auto& e : pr) HIP_CHECK(hipEventCreate(&e));
   }
@@ -259,12 +262,24 @@ thread_local double host_stage_t0[(int)Stage::kCount];
 
 // Device backend: events on the stage's stream, read after synchronize();
 // host backend: the stage ran synchronously, so the host clock is exact.
+static bool stage_events_on() {
+  static const bool v = [] {
+    const char* e = std::getenv("STRIPE_STAGE_EVENTS");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return v;
+}
+
 void Engine::stage_begin(Stage st, hipStream_t s) {
-  if (device()) HIP_CHECK(hipEventRecord(sev_[(int)st][0], s));
-  else host_stage_t0[(int)st] = host_ms();
+  if (device()) {
+    if (stage_timing_ && stage_events_on()) HIP_CHECK(hipEventRecord(sev_[(int)st][0], s));
+  } else {
+    host_stage_t0[(int)st] = host_ms();
+  }
 }
 
 void Engine::stage_end(Stage st, hipStream_t s) {
+  if (device() && !(stage_timing_ && stage_events_on())) return;
   if (device()) {
     HIP_CHECK(hipEventRecord(sev_[(int)st][1], s));
     sev_used_[(int)st] = true;

@@ -5,7 +5,7 @@ Layers:
   ops       - filters on torch tensors (HIP kernels) or numpy arrays (golden CPU path)
   models    - filter chains ("models"): presets ref-gpu / ref-cpu, north-star configs
   parallel  - row-partitioned distributed pipeline: RCCL / local / host / gloo comms
-  utils     - PPM/PGM I/O, synthetic frames, timing
+  utils     - PPM/PGM I/O, synthetic frames, logging
 The native core (C++/HIP, csrc/) is loaded from `_C`; the `stripe` CLI in bin/
 drives the same core without Python.
 """
