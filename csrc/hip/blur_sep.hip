@@ -664,7 +664,20 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
   // latency than they save)
   const bool lsb = pc.conv_mode == 2 && p.cmid == 3;
   sa.bias = (float)pc.conv_bias;
-  const Cfg& cf = cfgs[lsb][p.cmid == 3][edge];
+  // A/B variants of the RGB non-edge kernel (STRIPE_BLUR_VARIANT=n): 1 = two
+  // independent 4-wave workgroups per CU (NW 4, two pairs in flight), 2 = the
+  // same with one pair in flight, 3 = the 8-wave windows with one pair in flight
+  static const Cfg variants[2][4] = {
+      {STRIPE_BLUR_CFGW(3, false, 2, 2, 2, false, 8), STRIPE_BLUR_CFGW(3, false, 2, 2, 2, false, 4),
+       STRIPE_BLUR_CFGW(3, false, 2, 1, 2, false, 4), STRIPE_BLUR_CFGW(3, false, 2, 1, 2, false, 8)},
+      {STRIPE_BLUR_CFGW(3, false, 2, 2, 2, true, 8), STRIPE_BLUR_CFGW(3, false, 2, 2, 2, true, 4),
+       STRIPE_BLUR_CFGW(3, false, 2, 1, 2, true, 4), STRIPE_BLUR_CFGW(3, false, 2, 1, 2, true, 8)}};
+  static const int env_variant = [] {
+    const char* e = std::getenv("STRIPE_BLUR_VARIANT");
+    return e ? std::atoi(e) : 0;
+  }();
+  const Cfg& cf = (p.cmid == 3 && !edge && env_variant > 0 && env_variant < 4) ? variants[lsb][env_variant]
+                                                                               : cfgs[lsb][p.cmid == 3][edge];
 #undef STRIPE_BLUR_CFG
 #undef STRIPE_BLUR_CFGW
   // strips, rounded up to whole windows when NW waves share one

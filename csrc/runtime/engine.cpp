@@ -1419,10 +1419,35 @@ void Engine::run_dist(int chunks) {
   stage_begin(Stage::Scatter, s_comm_);
   transfer(0, -1, -1);
   record(dev ? evT[0] : nullptr, s_comm_);
-  if (root) {  // beside the transfers: nothing it reads or writes is in flight
-    stage_begin(Stage::Compute, s_compute_);
-    compute_root();
-    stage_end(Stage::Compute, s_compute_);
+  // The root's own share runs beside the transfers (nothing it reads or
+  // writes is in flight).  On the device its launch is asynchronous; the host
+  // backend filters synchronously, so there it runs on a worker thread --
+  // otherwise every chunk after the first would wait for the root's whole
+  // share (a root-heavy weighted split made the host step slower).
+  std::thread root_worker;
+  std::exception_ptr root_err;
+  struct JoinGuard {
+    std::thread& t;
+    ~JoinGuard() {
+      if (t.joinable()) t.join();
+    }
+  } join_guard{root_worker};
+  if (root) {
+    if (dev) {
+      stage_begin(Stage::Compute, s_compute_);
+      compute_root();
+      stage_end(Stage::Compute, s_compute_);
+    } else {
+      root_worker = std::thread([&] {
+        try {
+          stage_begin(Stage::Compute, nullptr);  // host clock, this thread
+          compute_root();
+          stage_end(Stage::Compute, nullptr);
+        } catch (...) {
+          root_err = std::current_exception();
+        }
+      });
+    }
   }
   for (int k = 0; k < n; ++k) {
     if (k + 1 < n) {
@@ -1451,6 +1476,8 @@ void Engine::run_dist(int chunks) {
     HIP_CHECK(hipEventRecord(dist_ev_[2 * n], s_comm_));
     HIP_CHECK(hipStreamWaitEvent(s_compute_, dist_ev_[2 * n], 0));
   }
+  if (root_worker.joinable()) root_worker.join();
+  if (root_err) std::rethrow_exception(root_err);
   if (root) {  // the root's output is in the root buffer only (as with dist_direct)
     out_buf_ = -1;
     out_c_ = cout;
