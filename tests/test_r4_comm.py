@@ -238,3 +238,72 @@ def test_bench_budget_skips_extra_scopes(tmp_path):
     rec = json.loads(lines[0])
     assert set(rec["budget"]["skipped"]) >= {"dist", "resident_deep"}
     assert "partial" not in rec
+
+
+# ------------------------------------------------------------------ GPU box
+@pytest.mark.gpu
+def test_rccl_comm_identity_and_nonblocking_gpu(C):
+    # a one-rank RCCL communicator goes through the same non-blocking init,
+    # pre-connect and bounded waits as the multi-rank path
+    import torch
+
+    torch.cuda.set_device(0)
+    comm = C.make_rccl_comm(C.rccl_unique_id(), 0, 1, 0)
+    ident = comm.identity()
+    assert ident["nccl_count"] == 1 and ident["nccl_device"] == 0 and ident["nccl_user_rank"] == 0
+    assert ident["nonblocking"] == 1 and ident["init_ms"] >= 0
+    comm.barrier()  # an all-reduce through the bounded enqueue + stream wait
+
+
+@pytest.mark.gpu
+def test_gpu_process_maps_one_runtime(C):
+    import torch
+
+    import mpi_cuda_imagemanipulation_amd as m
+
+    x = torch.randint(0, 256, (64, 96, 3), dtype=torch.uint8, device="cuda")
+    m.ops.apply(x, "gaussian5")
+    torch.cuda.synchronize()
+    libs = C.runtime_libs()
+    for stem in ("libamdhip64", "librccl", "libhsa-runtime64"):
+        assert len(libs[stem]) == 1, libs
+    tlib = os.path.join(os.path.dirname(torch.__file__), "lib")
+    assert libs["libamdhip64"][0].startswith(tlib) and libs["librccl"][0].startswith(tlib), libs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chain", ["gaussian5", "sobel", "emboss3"])
+def test_cold_engine_autotune_exact_gpu(C, chain):
+    # EngineConfig.cold: the autotuner times candidates on a rotation of cold
+    # scratch stripes and tunes the memory policy; the output stays exact
+    import mpi_cuda_imagemanipulation_amd as m
+
+    W, H, Cc = 2048, 512, (1 if chain == "sobel" else 3)
+    cfg = m.models.Pipeline(chain).config(W, H, Cc, "device", device=0, autotune=True)
+    cfg.cold = True
+    e = C.Engine(cfg)
+    e.load_synthetic(7)
+    e.run(1)
+    out = e.store_packed()
+    assert e.policies[0] in (0, 1) and e.bands[0] > 0
+    ref = C.golden_apply(C.synth_rows(7, W, Cc, 0, H), chain, "reflect101", True)
+    assert (out == ref).all()
+
+
+@pytest.mark.gpu
+def test_stage_timing_switch_gpu(C):
+    import mpi_cuda_imagemanipulation_amd as m
+
+    e = C.Engine(m.models.Pipeline("gaussian5").config(1024, 256, 3, "device", device=0))
+    e.load_synthetic(3)
+    e.run(1)
+    e.synchronize()
+    assert e.times.as_dict()["compute"] > 0
+    e.stage_timing = False
+    e.load_synthetic(3)
+    e.run(2)
+    e.synchronize()
+    ref = C.synth_rows(3, 1024, 3, 0, 256)
+    for _ in range(2):
+        ref = C.golden_apply(ref, "gaussian5", "reflect101", True)
+    assert (e.store_packed() == ref).all()
