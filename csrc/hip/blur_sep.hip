@@ -727,7 +727,9 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
       return e ? std::atoi(e) : -1;
     }();
     const int64_t pass_bytes = (int64_t)(n0 + n1) * L.W * 2 * p.cmid;
-    a.nxcd = env_xcd >= 0 ? env_xcd : (pass_bytes > dev::kNtMinBytes ? 0 : dev::kXcdCount);
+    // (the engine's memory policy decides for a cache-cold stripe: L.nt = 1)
+    const bool streaming = L.nt >= 0 ? L.nt != 0 : pass_bytes > dev::kNtMinBytes;
+    a.nxcd = env_xcd >= 0 ? env_xcd : (streaming ? 0 : dev::kXcdCount);
     a.nb0 = (int)div_up(a.ry1 - sa.a0, band);
     a.nbands = a.nb0 + (n1 ? (int)div_up(a.ry3 - sa.a2, band) : 0);
     const dim3 grid((unsigned)(cf.nw == 1 ? div_up((int64_t)sa.nstrips * a.nbands, dev::kSepWaves)

@@ -108,3 +108,26 @@ def test_run_distributed_rccl_in_process(n, chunks, chain):
         assert got.shape == ref.shape and np.abs(got.astype(int) - ref).max() <= 1
     else:
         assert got.shape == ref.shape and np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("n,chunks,stage", [(2, 4, "scatter"), (2, 0, "halo"), (4, 8, "dist"), (8, 0, "compute")])
+def test_rccl_in_process_fault_aborts_group(monkeypatch, n, chunks, stage):
+    """One rank of an in-process RCCL group fails (STRIPE_FAULT): every rank's
+    thread must fail fast -- the failing thread raises the others' abort
+    flags and each rank tears its non-blocking communicator down from its own
+    thread, inside a bounded poll, instead of waiting in ncclGroupEnd or a
+    stream for the dead rank."""
+    if _ngpus() < n:
+        pytest.skip(f"needs {n} GPUs")
+    import time
+
+    sys.path.insert(0, ROOT)
+    import mpi_cuda_imagemanipulation_amd as m
+
+    img = m.utils.synthetic_image(4, 611, 257, 3)
+    monkeypatch.setenv("STRIPE_FAULT", f"{stage}@1")
+    monkeypatch.setenv("STRIPE_COMM_TIMEOUT_S", "60")
+    t0 = time.time()
+    with pytest.raises(Exception, match="injected fault|aborted"):
+        m.models.Pipeline("gaussian5", dist_chunks=chunks).run_distributed(img, n, backend="rccl")
+    assert time.time() - t0 < 45, "peers of the failing rank must not wait for the comm timeout"
