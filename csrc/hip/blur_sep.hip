@@ -486,35 +486,6 @@ __global__ __launch_bounds__(blur_threads(NW), OCC * 256 / blur_threads(NW)) voi
     if (k & 1) step(T_{}, F_{}, B1{}, k);
     else step(T_{}, F_{}, B0{}, k);
   }
-  // x-margins of this band's output rows (the next pass's border reads), by
-  // the waves whose strip holds the margin's source pixels (launch_blur_sep
-  // guarantees the first / last strip holds them all; a.out_px = 0 keeps the
-  // separate fill launch): after vmcnt(0) the wave's own stores are done, and
-  // the reads go through L2 (sc0) so they see them
-  // (shared-window variants only: the per-wave gray edge kernel is at its
-  // SGPR limit and keeps the fill launch)
-  if (NW > 1 && a.out_px > 0 && (sx <= a.out_px || sx + G::PX >= a.W - 1 - a.out_px) && sx < a.W) {
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    const int nb = a.out_px * C;          // margin bytes per side
-    const int per_row = 2 * nb;
-    for (int e = lane; e < (ye - ys) * per_row; e += 64) {
-      const int y = ys + e / per_row;
-      const int qq = e % per_row;
-      const int side = qq >= nb;
-      const int kk = (side ? qq - nb : qq) / C + 1;
-      const int ch = (side ? qq - nb : qq) % C;
-      const int mm = side ? a.W - 1 + kk : -kk;
-      const int src = border_index_dev(mm, a.W, a.out_border);
-      // the byte is this wave's if its source pixel lies in the strip (a
-      // constant border has no source: the strip at that row end writes it)
-      const int owner = src >= 0 ? src : (side ? a.W - 1 : 0);
-      if (owner < sx || owner >= sx + G::PX) continue;
-      const uint32_t row = a.out_org + (uint32_t)((int64_t)y * a.out_pitch);
-      uint8_t v = 0;
-      if (src >= 0) v = __builtin_amdgcn_raw_buffer_load_b8(rout, row + (uint32_t)(src * C + ch), 0, 1);
-      __builtin_amdgcn_raw_buffer_store_b8(v, rout, row + (uint32_t)(mm * C + ch), 0, 0);
-    }
-  }
 }
 
 }  // namespace dev
@@ -711,18 +682,6 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
 #undef STRIPE_BLUR_CFGW
   // strips, rounded up to whole windows when NW waves share one
   sa.nstrips = (int)div_up(L.W, 16 * cf.nx);
-  // output x-margins written by the kernel's edge waves after each band (the
-  // fill launch, 9.6 us per pass on 16K rows in round 3, remains for other
-  // border modes and for rows whose first / last strip cannot hold all the
-  // margins' source pixels)
-  const int last_px = L.W - 16 * cf.nx * (sa.nstrips - 1);  // pixels of the row's last strip
-  const bool kernel_margins = cf.nw > 1 && p.out_margin_px > 0 && p.out_margin_px < 16 * cf.nx &&
-                              last_px >= p.out_margin_px + 1 &&
-                              L.W >= 2 * p.out_margin_px + 2 &&
-                              (p.out_margin_border == Border::Reflect101 || p.out_margin_border == Border::Replicate ||
-                               p.out_margin_border == Border::Constant);
-  a.out_px = kernel_margins ? p.out_margin_px : 0;
-  a.out_border = (int)p.out_margin_border;
   const int64_t nstrips_w = div_up(sa.nstrips, cf.nw) * cf.nw;
 
   const int n0 = std::max(0, L.ry[1] - L.ry[0]);
@@ -778,7 +737,7 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
     cf.fn<<<grid, 64 * (cf.nw == 1 ? dev::kSepWaves : cf.nw), cf.lds, s>>>(sa);
     HIP_CHECK(hipGetLastError());
   }
-  if (p.out_margin_px > 0 && !kernel_margins)
+  if (p.out_margin_px > 0)
     for (int r = 0; r < L.nrange; ++r)
       launch_fill_margins(L.out, L.out_pitch, L.W, p.cmid, L.ry[2 * r], L.ry[2 * r + 1], p.out_margin_px,
                           p.out_margin_border, s);
