@@ -299,8 +299,8 @@ def main():
              nstreams)
 
     # per-step device time distribution: an event on the step's stream after
-    # each step (step i = end(i) - end(i - 1)), max(K, 20) steps, untimed by the
-    # host clock above (the events themselves add a few us a step)
+    # each step, max(K, 20) steps, untimed by the host clock above (the events
+    # themselves add a few us a step)
     step_ms = None
     if dev and rows > 0:
         n_ev = max(a.steps, 20)
@@ -314,7 +314,10 @@ def main():
             ev[i + 1].record(frame_stream(i))
         sync_frames()
         sync()
-        step_ms = stats([ev[i].elapsed_time(ev[i + 1]) for i in range(n_ev)])
+        # with s streams consecutive steps overlap: a step's time is the span
+        # of s consecutive steps divided by s (s = 1: the plain delta)
+        w = nstreams
+        step_ms = stats([ev[i].elapsed_time(ev[i + w]) / w for i in range(n_ev - w + 1)])
     # device-event stage times of one step of frame 0 on rank 0
     dp.engine.stage_timing = True
     step(0)

@@ -173,7 +173,9 @@ class RcclComm final : public Comm {
       if (el > limit)
         abort("rank " + std::to_string(rank_) + ": collective did not complete within " + std::to_string(limit) +
               " s (STRIPE_COMM_TIMEOUT_S)");
-      if (it > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+      // spin for the first millisecond (a step's tail: the caller times it),
+      // then back off
+      if (el > 1e-3) std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
   }
 

@@ -257,8 +257,10 @@ double await_progress(const std::string& what, double limit_s, const std::functi
       if (give_up) give_up(why);
       fail(why);
     }
-    // spin briefly (enqueue-only operations finish in microseconds), then back off
-    if (it > 64) std::this_thread::sleep_for(std::chrono::microseconds(it > 4096 ? 1000 : 20));
+    // spin for the first millisecond (enqueue-only operations finish in
+    // microseconds), then back off
+    const double el = elapsed();
+    if (el > 1e-3) std::this_thread::sleep_for(std::chrono::microseconds(el > 0.1 ? 1000 : 20));
   }
 }
 
