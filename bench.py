@@ -235,49 +235,25 @@ def main():
 
     part, active = C.plan_rows(H, world, R)
     max_rows = max(r for _, r in part)
-    ws_max = max_rows * W * (pinfo["cin"] + pinfo["cout"])  # per-GPU bytes of one step (the same on every rank)
-    fits_mall = ws_max <= MALL_BYTES
-    # frames the headline rotates over: enough that F x working set > 2 x the
-    # Infinity Cache when one working set fits it (only for iterable chains)
-    nframes = a.frames if a.frames > 0 else (
-        min(8, int(math.ceil(2 * MALL_BYTES / max(1, ws_max))) + 1) if (fits_mall and iterable and dev) else 1)
-    cold = nframes > 1
 
-    # ---- headline engines: halo exchanged every step, F frames on one stream ----
+    # ---- headline: a FrameStream (halo exchanged every step; when a stripe
+    # fits the Infinity Cache, round-robin over enough frames that every step
+    # reads HBM-cold data; consecutive frames on alternating streams) ----
     pipe1 = Pipeline(a.chain, overlap=not a.no_overlap, halo_depth=1)
-    dp = parallel.DistributedPipeline(ctx, pipe1, W, H, Cc, autotune=not a.no_autotune, cold=cold)
+    fs = parallel.FrameStream(ctx, pipe1, W, H, Cc, frames=a.frames, streams=a.streams, autotune=not a.no_autotune)
+    ws_max, fits_mall, cold = fs.ws_max, fs.fits_mall, fs.cold
+    nframes, nstreams = len(fs), fs.nstreams
+    frames, streams = fs.frames, fs.streams
+    stream = streams[0] if streams else None
+    dp = fs.head
     if a.band > 0:
         dp.engine.set_tuning([a.band] * len(dp.engine.bands), [-1] * len(dp.engine.bands))
     row0, rows = dp.stripe
-    frames = [dp] + [parallel.DistributedPipeline(ctx, pipe1, W, H, Cc, cold=cold) for _ in range(nframes - 1)]
-    nstreams = a.streams if a.streams > 0 else (2 if nframes > 1 else 1)
-    nstreams = max(1, min(nstreams, nframes))
-    streams = [torch.cuda.Stream() for _ in range(nstreams)] if dev else []
-    stream = streams[0] if dev else None
-    if dev:
-        for i, f in enumerate(frames):
-            f.use_stream(streams[i % nstreams].cuda_stream)
-            # the step loops time themselves (host clock; events between steps
-            # below): per-call stage events would cost the GPU ~8 us a step
-            f.engine.stage_timing = False
-    for i, f in enumerate(frames):
-        f.load_synthetic(a.seed + i)
-    dp.engine.tune()
-    for f in frames[1:]:
-        f.engine.set_tuning(dp.engine.bands, dp.engine.caps, dp.engine.policies)
-
-    def step(i):
-        f = frames[i % nframes]
-        if not iterable:  # a chain that changes the channel count re-reads its (unchanged) input
-            f.engine.rewind()
-        f.run(1)
-
-    def sync_frames():
-        for f in frames:
-            f.synchronize()
-
-    def frame_stream(i):
-        return streams[(i % nframes) % nstreams]
+    fs.load_synthetic(a.seed)
+    fs.tune()
+    step = fs.step
+    sync_frames = fs.synchronize
+    frame_stream = fs.stream_of
 
     for i in range(a.warmup):
         step(i)

@@ -307,3 +307,39 @@ def test_stage_timing_switch_gpu(C):
     for _ in range(2):
         ref = C.golden_apply(ref, "gaussian5", "reflect101", True)
     assert (e.store_packed() == ref).all()
+
+
+def test_frame_stream_host_each_frame_exact(C, monkeypatch):
+    # FrameStream: frames stepped round-robin, each an independent iterated
+    # stripe (frame f = seed + f); after 2 rounds every frame equals 2 golden
+    # passes of its own input
+    import mpi_cuda_imagemanipulation_amd as m
+    from mpi_cuda_imagemanipulation_amd import parallel
+
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    ctx = parallel.init("gloo")
+    fs = parallel.FrameStream(ctx, m.models.Pipeline("gaussian5", halo_depth=1), 70, 33, 3, frames=3)
+    assert len(fs) == 3 and fs.nstreams == 1 and not fs.streams  # host engines: no streams
+    fs.load_synthetic(5)
+    fs.tune()
+    for _ in range(6):
+        fs.step()
+    fs.synchronize()
+    for f in range(3):
+        ref = C.synth_image(5 + f, 70, 33, 3)
+        for _ in range(2):
+            ref = C.golden_apply(ref, "gaussian5", "reflect101", True)
+        assert (fs.frames[f].result_stripe() == ref).all(), f
+
+
+def test_frame_stream_auto_frames_rule(C, monkeypatch):
+    # auto frame count: 1 on the host or when one stripe exceeds the cache
+    import mpi_cuda_imagemanipulation_amd as m
+    from mpi_cuda_imagemanipulation_amd import parallel
+
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    ctx = parallel.init("gloo")
+    fs = parallel.FrameStream(ctx, m.models.Pipeline("gaussian5"), 64, 40, 3)
+    assert len(fs) == 1 and fs.fits_mall and not fs.cold  # host engines never rotate
