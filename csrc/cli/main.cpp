@@ -14,10 +14,10 @@
 //                [--no-fuse] [--no-overlap] [--verbose]
 //   stripe bench --synthetic 16384x16384x3 --seed 1 --chain gaussian5 --ranks 1,2,4,8
 //                --iters 20 --warmup 5 --scope resident,dist,e2e [--backend rccl|local]
-//                [--json out.json]
+//                [--frames F] [--json out.json]     (F: stream of F frames, resident scope)
 //   stripe cmp   a.ppm b.ppm [--tol 0]
 //   stripe gen   --synthetic WxHxC --seed S --output x.ppm
-//   stripe info  [--chain ...] [--channels C]
+//   stripe info  [--chain ...] [--channels C] [--format json]
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -360,11 +360,45 @@ int cmd_bench(const Args& a) {
       std::vector<double> per_rank(N, 0);
       std::mutex mu;
       std::exception_ptr err;
+      // --frames F (resident scope): a stream of F independent frames stepped
+      // round-robin, each engine on its own stream (parallel.FrameStream's
+      // native counterpart: one frame's kernel boundary overlaps the next)
+      const int nframes = scope == "resident" ? std::max(1, a.geti("frames", 1)) : 1;
       auto body = [&](int r) {
         try {
           EngineConfig c = cfg;
           c.root_buffers = scope == "dist";
           if (!g.devices.empty()) c.device = g.devices[r];
+          if (nframes > 1) {
+            c.cold = true;
+            std::vector<std::unique_ptr<Engine>> fr;
+            for (int f = 0; f < nframes; ++f) {
+              EngineConfig cf = c;
+              cf.autotune = c.autotune && f == 0;
+              fr.push_back(std::make_unique<Engine>(cf, g.comms[r]));
+              fr.back()->set_stage_timing(false);
+              fr.back()->load_synthetic(seed + (uint64_t)f);
+            }
+            fr[0]->tune();
+            for (int f = 1; f < nframes; ++f) fr[f]->set_tuning(fr[0]->bands(), fr[0]->caps(), fr[0]->policies());
+            const bool it_ok = fr[0]->plan().cin == fr[0]->plan().cout;
+            auto fstep = [&](int i) {
+              Engine& fe = *fr[(size_t)(i % nframes)];
+              if (!it_ok) fe.rewind();
+              fe.run(1);
+            };
+            for (int i = 0; i < warmup; ++i) fstep(i);
+            for (auto& fe : fr) fe->synchronize();
+            g.comms[r]->barrier();
+            const double t0 = now_ms();
+            for (int i = 0; i < iters; ++i) fstep(i);
+            for (auto& fe : fr) fe->synchronize();
+            g.comms[r]->barrier();
+            const double t1 = now_ms();
+            std::lock_guard<std::mutex> lk(mu);
+            per_rank[r] = (t1 - t0) / iters;
+            return;
+          }
           Engine e(c, g.comms[r]);
           if (scope == "dist") {
             if (r == 0) e.load_root(full.data.data(), false);
@@ -430,8 +464,9 @@ int cmd_bench(const Args& a) {
       char buf[512];
       std::snprintf(buf, sizeof buf,
                     "{\"metric\":\"Mpixels/s\",\"scope\":\"%s\",\"value\":%.1f,\"ms_per_iter\":%.4f,\"n_ranks\":%d,"
-                    "\"backend\":\"%s\",\"chain\":\"%s\",\"W\":%d,\"H\":%d,\"C\":%d,\"iters\":%d,\"warmup\":%d}",
-                    scope.c_str(), mpx, ms, N, backend.c_str(), cfg.chain.c_str(), W, H, C, iters, warmup);
+                    "\"backend\":\"%s\",\"chain\":\"%s\",\"W\":%d,\"H\":%d,\"C\":%d,\"iters\":%d,\"warmup\":%d,"
+                    "\"frames\":%d}",
+                    scope.c_str(), mpx, ms, N, backend.c_str(), cfg.chain.c_str(), W, H, C, iters, warmup, nframes);
       std::printf("%s\n", buf);
       std::fflush(stdout);
       results.push_back(buf);
@@ -455,6 +490,7 @@ void usage() {
                "  bench --synthetic WxHxC [--seed S] [--chain C] [--ranks 1,2,4,8] [--iters N] [--warmup N]\n"
                "        [--scope resident|device,dist,e2e] [--backend rccl|local|host] [--json out.json]\n"
                "        [--no-overlap] [--no-pipeline] [--graphs] [--band ROWS] [--halo-depth K] [--dist-chunks K]\n"
+               "        [--frames F]  (resident: a stream of F independent frames, cache-cold tuning)\n"
                "  cmp   a.ppm b.ppm [--tol T]\n"
                "  gen   --synthetic WxHxC [--seed S] --output out.ppm\n"
                "  info  [--chain C] [--channels C] [--format json]\n");

@@ -105,6 +105,24 @@ def test_bench_host(tmp_path):
     assert all(x["value"] > 0 for x in recs)
 
 
+def test_bench_frames_host(tmp_path):
+    # --frames F: the resident scope steps a stream of F independent frames
+    js = tmp_path / "f.json"
+    run("bench", "--synthetic", "128x64x3", "--chain", "gaussian5", "--ranks", "1,2", "--iters", "4",
+        "--warmup", "1", "--frames", "3", "--backend", "host", "--json", js)
+    recs = [json.loads(l) for l in js.read_text().splitlines()]
+    assert [(x["n_ranks"], x["frames"]) for x in recs] == [(1, 3), (2, 3)] and all(x["value"] > 0 for x in recs)
+
+
+@pytest.mark.gpu
+def test_gpu_bench_frames_local(tmp_path):
+    js = tmp_path / "f.json"
+    run("bench", "--synthetic", "2048x512x3", "--chain", "gaussian5", "--ranks", "1,2", "--iters", "8",
+        "--warmup", "2", "--frames", "4", "--backend", "local", "--json", js)
+    recs = [json.loads(l) for l in js.read_text().splitlines()]
+    assert [x["frames"] for x in recs] == [4, 4] and all(x["value"] > 0 for x in recs)
+
+
 @pytest.mark.gpu
 def test_gpu_backends_and_file_rendezvous(tmp_path):
     """local (4 logical ranks on one GPU), rccl (in-process) and the one-process-
