@@ -48,14 +48,20 @@ Progress comm_progress(ncclComm_t c, std::string* err) {
 
 // Poll every communicator of `comms` to completion under the bound; on failure
 // abort them all (an in-process group fails as one).
+// `give_up` (default: ncclCommAbort on every handle, for communicators no
+// RcclComm owns yet) runs once before the error is raised.
 double await_comms(const std::string& what, const std::vector<ncclComm_t>& comms,
-                   const std::function<bool()>& aborted = nullptr) {
+                   const std::function<void(const std::string&)>& give_up = nullptr) {
   double ms = 0;
   for (size_t i = 0; i < comms.size(); ++i) {
     ms += await_progress(
         what + (comms.size() > 1 ? " (communicator " + std::to_string(i) + ")" : std::string()), comm_timeout_s(),
-        [&](std::string* err) { return comm_progress(comms[i], err); }, aborted,
-        [&](const std::string&) {
+        [&](std::string* err) { return comm_progress(comms[i], err); }, nullptr,
+        [&](const std::string& why) {
+          if (give_up) {
+            give_up(why);
+            return;
+          }
           for (ncclComm_t c : comms)
             if (c) ncclCommAbort(c);
         });
@@ -376,7 +382,11 @@ std::vector<std::unique_ptr<Comm>> make_rccl_comms_all(const std::vector<int>& d
       const ncclResult_t e = ncclGroupEnd();  // always close the group, even after a failed enqueue
       NCCL_CHECK(bad);
       if (e != ncclSuccess && e != ncclInProgress) NCCL_CHECK(e);
-      await_comms("RCCL in-process p2p pre-connect", comms);
+      // the RcclComm objects own the handles now: flag them (their destructors
+      // abort each communicator exactly once)
+      await_comms("RCCL in-process p2p pre-connect", comms, [&](const std::string& why) {
+        for (auto* c : raw) c->abort(why);
+      });
       for (int r = 0; r < n; ++r) {
         HIP_CHECK(hipSetDevice(devices[(size_t)r]));
         raw[(size_t)r]->wait(raw[(size_t)r]->side_stream());

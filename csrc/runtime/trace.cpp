@@ -241,7 +241,7 @@ double await_progress(const std::string& what, double limit_s, const std::functi
                       const std::function<bool()>& aborted, const std::function<void(const std::string&)>& give_up) {
   const auto t0 = std::chrono::steady_clock::now();
   auto elapsed = [&] { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
-  for (int it = 0;; ++it) {
+  for (;;) {
     std::string err;
     std::string why;
     if (aborted && aborted()) {

@@ -7,3 +7,4 @@ timeout -k 10 200 python bench.py --steps 20 --warmup 5 --height 2048 > $O/bench
 timeout -k 10 200 python bench.py --steps 100 --warmup 10 --height 2048 --dist-steps 0 --ref-steps 0 --e2e-steps 0 > $O/bench_stripe_k100.json 2> $O/bench_stripe_k100.err || exit 1
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $O/prof_blur -o blur -- python3 tools/kbench.py --chains "blur:31" --shape 16384x16384x3 --iters 10 > $O/prof_blur.txt 2>&1 || exit 1
+bash tools/gpu_r4_shared.sh
