@@ -1,5 +1,6 @@
 mkdir -p gpurun_out/r4/run2
 O=gpurun_out/r4/run2
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_r4_comm.py tests/test_cli.py -m gpu > $O/tests.txt 2>&1 || exit 1
 bash tools/gpu_r4_blur.sh || exit 1
 timeout -k 10 200 python bench.py --steps 20 --warmup 5 > $O/bench_n1.json 2> $O/bench_n1.err || exit 1
 timeout -k 10 200 python bench.py --steps 20 --warmup 5 --frames 2 > $O/bench_n1_f2.json 2> $O/bench_n1_f2.err || exit 1
