@@ -81,6 +81,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--band", type=int, default=0)
+    ap.add_argument("--halo-schedule", default="auto", choices=["auto", "serial", "overlap", "pipeline"],
+                    help="halo schedule of the headline steps at N>1 (auto: time each on the real transport before "
+                         "the timed region and keep the fastest, max over ranks)")
     ap.add_argument("--frames", type=int, default=0,
                     help="frames the headline steps over (0: auto, enough to defeat the Infinity Cache; 1: one "
                          "frame iterated in place)")
@@ -251,6 +254,19 @@ def main():
     row0, rows = dp.stripe
     fs.load_synthetic(a.seed)
     fs.tune()
+    # which halo schedule is fastest depends on the link and the transport's
+    # per-exchange cost: at N>1 measure them here, untimed, on every rank
+    if world == 1:
+        sched = {"chosen": "none", "ms": {}, "requested": a.halo_schedule}  # no exchange
+    elif a.no_overlap:
+        fs.set_schedule("serial")
+        sched = {"chosen": fs.schedule, "ms": {}, "requested": "serial"}
+    elif a.halo_schedule != "auto":
+        fs.set_schedule(a.halo_schedule)
+        sched = {"chosen": fs.schedule, "ms": {}, "requested": a.halo_schedule}
+    else:
+        sched = dict(fs.pick_schedule(max_over_ranks, barrier), requested="auto")
+    log.info("halo schedule: %s %s", sched["chosen"], sched["ms"])
     step = fs.step
     sync_frames = fs.synchronize
     frame_stream = fs.stream_of
@@ -398,6 +414,7 @@ def main():
         "tuned": {"band_rows": dp.engine.bands, "occupancy_caps": dp.engine.caps, "policies": dp.engine.policies,
                   "cold": cold},
         "halo_depth": 1,
+        "halo_schedule": sched,
         "stripe_rows": [r for _, r in part],
         "stage_ms_rank0": stages,
         "world": {"summary": parallel.identity_summary(ids), "ranks": ids},

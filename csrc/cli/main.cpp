@@ -400,6 +400,10 @@ int cmd_bench(const Args& a) {
             return;
           }
           Engine e(c, g.comms[r]);
+          // the loop times itself on the host; timestamped stage events between
+          // dependent kernels would cost the GPU ~8 us a step
+          // (profiles/r4/cold/README.md) and nothing here reads them
+          e.set_stage_timing(false);
           if (scope == "dist") {
             if (r == 0) e.load_root(full.data.data(), false);
           } else if (scope == "e2e") {

@@ -219,6 +219,15 @@ class Engine {
   // a step loop that times itself another way turns it off.
   void set_stage_timing(bool on) { stage_timing_ = on; }
   bool stage_timing() const { return stage_timing_; }
+  // Halo schedule of a one-step run() over > 1 ranks: 0 serial (exchange,
+  // then the whole stripe on one stream), 1 overlap (interior rows beside the
+  // exchange, boundary rows after it), 2 pipeline (core / rim / edge on three
+  // streams, run_pipelined).  set_halo_schedule() picks the request (the
+  // EngineConfig overlap / pipeline flags); halo_schedule() is what run(1)
+  // actually does (a host engine, one rank or a chain the pipeline does not
+  // take fall back), so callers can time only the schedules that differ.
+  void set_halo_schedule(int s);
+  int halo_schedule() const;
   // device pointer + pitch of the current input/output stripe origins (for tests)
   const uint8_t* input_origin() const;
   const uint8_t* output_origin() const;

@@ -546,6 +546,18 @@ PYBIND11_MODULE(_C, m) {
       })
       .def_property_readonly("times", [](const Engine& e) { return e.times(); })
       .def_property("stage_timing", &Engine::stage_timing, &Engine::set_stage_timing)
+      // "serial" | "overlap" | "pipeline": set = request, get = what run(1) does
+      .def_property(
+          "halo_schedule",
+          [](const Engine& e) {
+            static const char* names[] = {"serial", "overlap", "pipeline"};
+            return std::string(names[e.halo_schedule()]);
+          },
+          [](Engine& e, const std::string& s) {
+            const int v = s == "serial" ? 0 : s == "overlap" ? 1 : s == "pipeline" ? 2 : -1;
+            STRIPE_CHECK(v >= 0, "halo schedule must be serial, overlap or pipeline, got '" << s << "'");
+            e.set_halo_schedule(v);
+          })
       .def_property_readonly("graph_launches", &Engine::graph_launches);
 
   m.def("run_local_group", [](const EngineConfig& cfg, int world, const U8Array& a, int iterations) {

@@ -577,6 +577,20 @@ bool Engine::pipelined_ok() const {
   return R > 0 && rows > 4 * R && comm_ != nullptr;
 }
 
+void Engine::set_halo_schedule(int s) {
+  STRIPE_CHECK(s >= 0 && s <= 2, "halo schedule must be 0 (serial), 1 (overlap) or 2 (pipeline), got " << s);
+  cfg_.overlap = s >= 1;
+  cfg_.pipeline = s == 2;
+}
+
+int Engine::halo_schedule() const {
+  // mirrors run(1)'s dispatch and run_pass's split for a single-pass chain
+  if (!device() || !cfg_.halo || part_.active <= 1) return 0;
+  if (cfg_.pipeline && cfg_.overlap && pipelined_ok()) return 2;
+  const int R = plan_.passes.empty() ? 0 : plan_.passes[0].R;
+  return cfg_.overlap && stripe().rows > 2 * R ? 1 : 0;
+}
+
 void Engine::run_pipelined(int iterations) {
   const Pass& p = plan_.passes[0];
   const int R = p.R, rows = stripe().rows;

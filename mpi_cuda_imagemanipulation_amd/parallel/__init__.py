@@ -20,6 +20,7 @@ import json
 import os
 import socket
 import threading
+import time
 from dataclasses import dataclass
 
 import numpy as np
@@ -322,6 +323,55 @@ class FrameStream:
         e0.tune()
         for f in self.frames[1:]:
             f.engine.set_tuning(e0.bands, e0.caps, e0.policies)
+
+    SCHEDULES = ("pipeline", "overlap", "serial")
+
+    def set_schedule(self, name: str):
+        """Halo schedule of every frame ("serial" | "overlap" | "pipeline")."""
+        for f in self.frames:
+            f.engine.halo_schedule = name
+
+    @property
+    def schedule(self) -> str:
+        return self.head.engine.halo_schedule
+
+    def pick_schedule(self, reduce_max=None, barrier=None, steps: int = 0, rounds: int = 2) -> dict:
+        """Time every halo schedule that differs on this engine (interior /
+        boundary overlap, the three-stream pipeline, the plain serial one) on
+        the real transport and keep the fastest; returns {"chosen", "ms"}.
+        Which one wins depends on the link and RCCL's per-exchange cost, which
+        one GPU cannot show, so the job measures it where it runs.
+        reduce_max(ms) -> max over ranks and barrier() keep every rank on the
+        same choice (each rank times the same steps; collective order holds)."""
+        reduce_max = reduce_max or (lambda v: v)
+        barrier = barrier or (lambda: None)
+        cands = []
+        for s in self.SCHEDULES:
+            self.set_schedule(s)
+            eff = self.schedule
+            if eff not in cands:
+                cands.append(eff)
+        if len(cands) == 1:
+            self.set_schedule(cands[0])
+            return {"chosen": cands[0], "ms": {}}
+        n = steps if steps > 0 else max(60, 4 * len(self.frames))
+        best = {}
+        for _ in range(rounds):
+            for s in cands:
+                self.set_schedule(s)
+                for i in range(2 * len(self.frames)):
+                    self.step(i)
+                self.synchronize()
+                barrier()
+                t0 = time.perf_counter()
+                for i in range(n):
+                    self.step(i)
+                self.synchronize()
+                ms = reduce_max((time.perf_counter() - t0) * 1e3 / n)
+                best[s] = min(best.get(s, float("inf")), ms)
+        chosen = min(cands, key=lambda s: best[s])
+        self.set_schedule(chosen)
+        return {"chosen": chosen, "ms": {s: round(v, 5) for s, v in best.items()}}
 
     def stream_of(self, i: int):
         return self.streams[(i % len(self.frames)) % self.nstreams] if self.streams else None

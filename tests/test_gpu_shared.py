@@ -47,6 +47,10 @@ def test_bench_gloo_gpu_processes(tmp_path, n):
     rec = recs[0]
     assert rec["n_gpus"] == n and rec["value"] > 0 and rec["verified_vs_golden"] is True
     assert sum(rec["stripe_rows"]) == 1536
+    # the three halo schedules differ on device engines: each was timed on the
+    # real transport and the verified headline ran the fastest
+    hs = rec["halo_schedule"]
+    assert set(hs["ms"]) == {"serial", "overlap", "pipeline"} and hs["chosen"] == min(hs["ms"], key=hs["ms"].get)
     for name, sc in rec["scopes"].items():
         assert "error" not in sc, (name, sc)
         if "verified" in sc:

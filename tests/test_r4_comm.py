@@ -238,6 +238,8 @@ def test_bench_budget_skips_extra_scopes(tmp_path):
     rec = json.loads(lines[0])
     assert set(rec["budget"]["skipped"]) >= {"dist", "resident_deep"}
     assert "partial" not in rec
+    # host engines have one halo schedule: nothing to time, the choice is recorded
+    assert rec["halo_schedule"]["chosen"] == "serial" and rec["halo_schedule"]["requested"] == "auto"
 
 
 # ------------------------------------------------------------------ GPU box
@@ -331,6 +333,33 @@ def test_frame_stream_host_each_frame_exact(C, monkeypatch):
         for _ in range(2):
             ref = C.golden_apply(ref, "gaussian5", "reflect101", True)
         assert (fs.frames[f].result_stripe() == ref).all(), f
+
+
+def test_halo_schedule_property(C):
+    # request vs effective schedule: a one-rank (or host) engine exchanges
+    # nothing, so every request runs as the serial schedule
+    import mpi_cuda_imagemanipulation_amd as m
+
+    e = C.Engine(m.models.Pipeline("gaussian5").config(64, 32, 3, "host"))
+    for s in ("pipeline", "overlap", "serial"):
+        e.halo_schedule = s
+        assert e.halo_schedule == "serial"
+    with pytest.raises(Exception, match="halo schedule"):
+        e.halo_schedule = "fastest"
+
+
+def test_frame_stream_pick_schedule_single_candidate(C, monkeypatch):
+    # only schedules that differ on this engine are timed; one candidate -> no timing
+    import mpi_cuda_imagemanipulation_amd as m
+    from mpi_cuda_imagemanipulation_amd import parallel
+
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    ctx = parallel.init("gloo")
+    fs = parallel.FrameStream(ctx, m.models.Pipeline("gaussian5", halo_depth=1), 64, 40, 3)
+    calls = []
+    got = fs.pick_schedule(lambda v: calls.append(v) or v)
+    assert got == {"chosen": "serial", "ms": {}} and not calls and fs.schedule == "serial"
 
 
 def test_frame_stream_auto_frames_rule(C, monkeypatch):
