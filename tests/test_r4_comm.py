@@ -362,6 +362,28 @@ def test_frame_stream_pick_schedule_single_candidate(C, monkeypatch):
     assert got == {"chosen": "serial", "ms": {}} and not calls and fs.schedule == "serial"
 
 
+def test_frame_stream_pick_schedule_takes_fastest_max_over_ranks():
+    # three schedules that differ: each is timed `rounds` times, the per-rank
+    # time goes through reduce_max (every rank must agree), the fastest wins
+    # and stays set on every frame
+    import time as _t
+    from types import SimpleNamespace
+
+    from mpi_cuda_imagemanipulation_amd import parallel
+
+    cost = {"pipeline": 0.004, "overlap": 0.001, "serial": 0.002}
+    frames = [SimpleNamespace(engine=SimpleNamespace(halo_schedule="pipeline")) for _ in range(2)]
+    fs = parallel.FrameStream.__new__(parallel.FrameStream)
+    fs.frames = frames
+    fs.step = lambda i=None: _t.sleep(cost[frames[0].engine.halo_schedule])
+    fs.synchronize = lambda: None
+    seen = []
+    got = fs.pick_schedule(lambda v: seen.append(v) or v, steps=3, rounds=2)
+    assert got["chosen"] == "overlap" and set(got["ms"]) == set(cost)
+    assert len(seen) == 6 and all(f.engine.halo_schedule == "overlap" for f in frames)
+    assert got["ms"]["overlap"] < got["ms"]["serial"] < got["ms"]["pipeline"]
+
+
 def test_frame_stream_auto_frames_rule(C, monkeypatch):
     # auto frame count: 1 on the host or when one stripe exceeds the cache
     import mpi_cuda_imagemanipulation_amd as m
