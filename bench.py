@@ -85,10 +85,12 @@ def parse():
                     help="halo schedule of the headline steps at N>1 (auto: time each on the real transport before "
                          "the timed region and keep the fastest, max over ranks)")
     ap.add_argument("--frames", type=int, default=0,
-                    help="frames the headline steps over (0: auto, enough to defeat the Infinity Cache; 1: one "
-                         "frame iterated in place)")
+                    help="frames the headline steps over (0: auto -- enough to defeat the Infinity Cache when a "
+                         "stripe fits it, else 2 at N>1 so one frame's exchange runs beside the other's filter, "
+                         "else 1; 1: one frame iterated in place)")
     ap.add_argument("--streams", type=int, default=0,
-                    help="streams the headline frames alternate over (0: auto -- 2 when frames rotate, so one frame's "
+                    help="streams the headline frames alternate over (0: auto -- at N>1 the probe times 1 and 2, else 2 "
+                         "when frames rotate, so one frame's "
                          "kernel boundary overlaps the next frame's step; 1: strictly serial steps)")
     ap.add_argument("--deep-steps", type=int, default=-1, help="steps of the deep-halo scope (-1: --steps; 0: skip)")
     ap.add_argument("--halo-depth", type=int, default=0,
@@ -266,7 +268,8 @@ def main():
         sched = {"chosen": fs.schedule, "ms": {}, "requested": a.halo_schedule}
     else:
         sched = dict(fs.pick_schedule(max_over_ranks, barrier), requested="auto")
-    log.info("halo schedule: %s %s", sched["chosen"], sched["ms"])
+    nstreams = fs.nstreams  # the probe may have settled on one stream
+    log.info("halo schedule: %s on %d stream(s) %s", sched["chosen"], nstreams, sched["ms"])
     step = fs.step
     sync_frames = fs.synchronize
     frame_stream = fs.stream_of
@@ -396,7 +399,8 @@ def main():
             "seq_len": H,
             "parallelism": f"rowpart{world}+halo",
             "scope": ("resident: halo exchange every step + full-frame filter per step"
-                      + (f", round-robin over {nframes} frames so every step reads HBM-cold data" if cold else "")
+                      + (f", round-robin over {nframes} frames so every step reads HBM-cold data" if cold else
+                         (f", round-robin over {nframes} independent frames" if nframes > 1 else ""))
                       + (f", consecutive frames on {nstreams} alternating streams" if nstreams > 1 else "")),
         },
         "verified_vs_golden": verify,

@@ -289,20 +289,35 @@ class FrameStream:
         self.ws_max = max(r for _, r in part) * W * (info["cin"] + info["cout"])  # per-GPU bytes of one step
         self.fits_mall = self.ws_max <= MALL_BYTES
         if frames <= 0:
-            frames = (min(8, -(-2 * MALL_BYTES // max(1, self.ws_max)) + 1)
-                      if (self.fits_mall and self.iterable and ctx.device) else 1)
+            if self.fits_mall and self.iterable and ctx.device:
+                frames = min(8, -(-2 * MALL_BYTES // max(1, self.ws_max)) + 1)
+            elif ctx.device and ctx.world > 1 and self.iterable:
+                frames = 2  # one frame's halo exchange can run beside the other's filter
+            else:
+                frames = 1
         self.cold = frames > 1 and self.fits_mall
-        streams = streams if streams > 0 else (2 if frames > 1 else 1)
-        self.nstreams = max(1, min(streams, frames)) if ctx.device else 1
+        nmax = max(1, min(streams if streams > 0 else 2, frames)) if ctx.device else 1
+        # stream counts pick_schedule may choose between (a fixed --streams: that one)
+        self.stream_options = [nmax] if (streams > 0 or nmax == 1) else [1, nmax]
         self.frames = [DistributedPipeline(ctx, pipeline, W, H, Cc, autotune=autotune and i == 0, cold=self.cold)
                        for i in range(frames)]
         self.streams = []
+        self.nstreams = 1
         if ctx.device:
-            self.streams = [torch.cuda.Stream() for _ in range(self.nstreams)]
-            for i, f in enumerate(self.frames):
-                f.use_stream(self.streams[i % self.nstreams].cuda_stream)
+            self.streams = [torch.cuda.Stream() for _ in range(nmax)]
+            for f in self.frames:
                 f.engine.stage_timing = stage_timing
+        self.set_streams(nmax)
         self._i = 0
+
+    def set_streams(self, n: int):
+        """Queue frame f on stream f mod n (n <= the streams created)."""
+        if not self.streams:
+            return
+        n = max(1, min(n, len(self.streams)))
+        for i, f in enumerate(self.frames):
+            f.use_stream(self.streams[i % n].cuda_stream)
+        self.nstreams = n
 
     def __len__(self):
         return len(self.frames)
@@ -337,28 +352,36 @@ class FrameStream:
 
     def pick_schedule(self, reduce_max=None, barrier=None, steps: int = 0, rounds: int = 2) -> dict:
         """Time every halo schedule that differs on this engine (interior /
-        boundary overlap, the three-stream pipeline, the plain serial one) on
-        the real transport and keep the fastest; returns {"chosen", "ms"}.
+        boundary overlap, the three-stream pipeline, the plain serial one),
+        with the frames on one stream or alternating over two, on the real
+        transport, and keep the fastest; returns {"chosen", "streams", "ms"}
+        ("ms" keys: schedule, or schedule@streams when both counts are tried).
         Which one wins depends on the link and RCCL's per-exchange cost, which
         one GPU cannot show, so the job measures it where it runs.
         reduce_max(ms) -> max over ranks and barrier() keep every rank on the
         same choice (each rank times the same steps; collective order holds)."""
         reduce_max = reduce_max or (lambda v: v)
         barrier = barrier or (lambda: None)
-        cands = []
+        scheds = []
         for s in self.SCHEDULES:
             self.set_schedule(s)
             eff = self.schedule
-            if eff not in cands:
-                cands.append(eff)
+            if eff not in scheds:
+                scheds.append(eff)
+        opts = list(self.stream_options)
+        cands = [(s, ns) for ns in opts for s in scheds]
+        key = (lambda c: f"{c[0]}@{c[1]}") if len(opts) > 1 else (lambda c: c[0])
         if len(cands) == 1:
-            self.set_schedule(cands[0])
-            return {"chosen": cands[0], "ms": {}}
+            self.set_schedule(scheds[0])
+            self.set_streams(opts[0])
+            return {"chosen": scheds[0], "streams": self.nstreams, "ms": {}}
         n = steps if steps > 0 else max(60, 4 * len(self.frames))
         best = {}
         for _ in range(rounds):
-            for s in cands:
-                self.set_schedule(s)
+            for c in cands:
+                self.synchronize()
+                self.set_schedule(c[0])
+                self.set_streams(c[1])
                 for i in range(2 * len(self.frames)):
                     self.step(i)
                 self.synchronize()
@@ -368,10 +391,12 @@ class FrameStream:
                     self.step(i)
                 self.synchronize()
                 ms = reduce_max((time.perf_counter() - t0) * 1e3 / n)
-                best[s] = min(best.get(s, float("inf")), ms)
-        chosen = min(cands, key=lambda s: best[s])
-        self.set_schedule(chosen)
-        return {"chosen": chosen, "ms": {s: round(v, 5) for s, v in best.items()}}
+                best[c] = min(best.get(c, float("inf")), ms)
+        chosen = min(cands, key=lambda c: best[c])
+        self.synchronize()
+        self.set_schedule(chosen[0])
+        self.set_streams(chosen[1])
+        return {"chosen": chosen[0], "streams": self.nstreams, "ms": {key(c): round(v, 5) for c, v in best.items()}}
 
     def stream_of(self, i: int):
         return self.streams[(i % len(self.frames)) % self.nstreams] if self.streams else None

@@ -359,7 +359,7 @@ def test_frame_stream_pick_schedule_single_candidate(C, monkeypatch):
     fs = parallel.FrameStream(ctx, m.models.Pipeline("gaussian5", halo_depth=1), 64, 40, 3)
     calls = []
     got = fs.pick_schedule(lambda v: calls.append(v) or v)
-    assert got == {"chosen": "serial", "ms": {}} and not calls and fs.schedule == "serial"
+    assert got == {"chosen": "serial", "streams": 1, "ms": {}} and not calls and fs.schedule == "serial"
 
 
 def test_frame_stream_pick_schedule_takes_fastest_max_over_ranks():
@@ -375,6 +375,7 @@ def test_frame_stream_pick_schedule_takes_fastest_max_over_ranks():
     frames = [SimpleNamespace(engine=SimpleNamespace(halo_schedule="pipeline")) for _ in range(2)]
     fs = parallel.FrameStream.__new__(parallel.FrameStream)
     fs.frames = frames
+    fs.streams, fs.stream_options, fs.nstreams = [], [1], 1  # host: no streams to alternate
     fs.step = lambda i=None: _t.sleep(cost[frames[0].engine.halo_schedule])
     fs.synchronize = lambda: None
     seen = []
