@@ -392,7 +392,8 @@ std::vector<std::unique_ptr<Comm>> make_rccl_comms_all(const std::vector<int>& d
         raw[(size_t)r]->wait(raw[(size_t)r]->side_stream());
       }
     } catch (...) {
-      free_all();
+      // the buffers stay allocated: a flagged (not yet aborted) communicator's
+      // kernel may still reference them, and hipFree would wait for it
       for (auto* c : raw) c->abort("in-process pre-connect failed");
       throw;
     }
