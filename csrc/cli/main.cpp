@@ -7,6 +7,8 @@
 // or N logical ranks on fewer GPUs / on the CPU), all parameters are flags:
 //
 //   stripe run   --input in.ppm --output out.ppm --chain gray:ref,contrast:3.5,emboss3
+//                (input PPM/PGM or baseline JPEG, read by content; output .jpg/.jpeg
+//                 -> JPEG at --quality Q (95), anything else -> PPM/PGM)
 //                (multi-process: --backend rccl --world N --rank r --rendezvous FILE [--device d])
 //                [--preset ref-gpu|ref-cpu] [--ranks N] [--backend rccl|local|host]
 //                [--devices 0,1,..] [--border reflect101|replicate|constant|skip]
@@ -214,7 +216,7 @@ int cmd_run_rank(const Args& a) {
   EngineConfig cfg;
   if (rank == 0) {
     STRIPE_CHECK(a.has("input") && a.has("output"), "rank 0 needs --input and --output");
-    img = read_pnm(a.get("input"));
+    img = read_image(a.get("input"));
     cfg = config_from(a, img.W, img.H, img.C);
   } else {
     cfg = config_from(a, 1, 1, 3);  // geometry arrives with the metadata broadcast
@@ -233,7 +235,7 @@ int cmd_run_rank(const Args& a) {
   }
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (rank == 0) {
-    write_pnm(a.get("output"), out);
+    write_image(a.get("output"), out, a.geti("quality", 95));
     std::printf("{\"cmd\":\"run\",\"W\":%d,\"H\":%d,\"C\":%d,\"ranks\":%d,\"backend\":\"rccl\",\"processes\":%d,"
                 "\"chain\":\"%s\",\"wall_ms\":%.3f,\"kernel_ms\":%.4f,\"scatter_ms\":%.4f,\"gather_ms\":%.4f}\n",
                 img.W, img.H, img.C, world, world, cfg.chain.c_str(), ms, t.run, t.scatter, t.gather);
@@ -244,7 +246,7 @@ int cmd_run_rank(const Args& a) {
 int cmd_run(const Args& a) {
   if (a.has("world")) return cmd_run_rank(a);
   STRIPE_CHECK(a.has("input") && a.has("output"), "run needs --input and --output");
-  Image img = read_pnm(a.get("input"));
+  Image img = read_image(a.get("input"));
   EngineConfig cfg = config_from(a, img.W, img.H, img.C);
   const int N = a.geti("ranks", 1);
   const std::string backend = a.get("backend", cfg.backend == BackendKind::Host ? "host" : "local");
@@ -259,7 +261,7 @@ int cmd_run(const Args& a) {
   const auto t0 = std::chrono::steady_clock::now();
   Image out = run_group(cfg, g.comms, g.devices, img, iters, &t);
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  write_pnm(a.get("output"), out);
+  write_image(a.get("output"), out, a.geti("quality", 95));
   std::printf("{\"cmd\":\"run\",\"W\":%d,\"H\":%d,\"C\":%d,\"ranks\":%d,\"backend\":\"%s\",\"chain\":\"%s\","
               "\"wall_ms\":%.3f,\"kernel_ms\":%.4f,\"scatter_ms\":%.4f,\"gather_ms\":%.4f}\n",
               img.W, img.H, img.C, N, backend.c_str(), cfg.chain.c_str(), ms, t.run, t.scatter, t.gather);
@@ -268,7 +270,7 @@ int cmd_run(const Args& a) {
 
 int cmd_cmp(const Args& a) {
   STRIPE_CHECK(a.pos.size() == 2, "cmp needs two files");
-  Image x = read_pnm(a.pos[0]), y = read_pnm(a.pos[1]);
+  Image x = read_image(a.pos[0]), y = read_image(a.pos[1]);
   CmpResult r = compare_images(x, y);
   const int tol = a.geti("tol", 0);
   if (!r.same_shape) {
@@ -288,7 +290,7 @@ int cmd_gen(const Args& a) {
   parse_shape(a.get("synthetic", "512x512x3"), &W, &H, &C);
   Image img = synth_image((uint64_t)std::stoull(a.get("seed", "1")), W, H, C);
   STRIPE_CHECK(a.has("output"), "gen needs --output");
-  write_pnm(a.get("output"), img);
+  write_image(a.get("output"), img, a.geti("quality", 95));
   return 0;
 }
 
@@ -486,7 +488,8 @@ int cmd_bench(const Args& a) {
 void usage() {
   std::fprintf(stderr,
                "usage: stripe <run|bench|cmp|gen|info> [options]\n"
-               "  run   --input in.ppm --output out.ppm [--chain C | --preset ref-gpu|ref-cpu] [--ranks N]\n"
+               "  run   --input in.ppm|in.jpg --output out.ppm|out.jpg [--quality 95]\n"
+               "        [--chain C | --preset ref-gpu|ref-cpu] [--ranks N]\n"
                "        [--backend rccl|local|host] [--devices 0,1,..] [--border MODE] [--no-halo]\n"
                "        [--expand-gray] [--legacy-partition] [--iterations K] [--no-fuse] [--no-overlap]\n"
                "        [--dist-chunks K]  (> 1 ranks, single-pass chains: pipelined scatter/filter/gather)\n"

@@ -4,6 +4,7 @@
 // validated headers; other formats go through the Python front end (Pillow).
 #include "stripe/image.h"
 
+#include <cctype>
 #include <cmath>
 #include <cstdio>
 #include <fstream>
@@ -109,6 +110,43 @@ void write_pnm(const std::string& path, const Image& img) {
     STRIPE_CHECK(f.good(), "write failed for '" << tmp << "'");
   }
   STRIPE_CHECK(std::rename(tmp.c_str(), path.c_str()) == 0, "rename to '" << path << "' failed");
+}
+
+namespace {
+std::string slurp(const std::string& path) {
+  std::ifstream f(path, std::ios::binary);
+  STRIPE_CHECK(f.good(), "cannot open '" << path << "'");
+  return std::string((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+}
+
+void write_atomic(const std::string& path, const std::string& bytes) {
+  const std::string tmp = path + ".tmp." + std::to_string(getpid());
+  {
+    std::ofstream f(tmp, std::ios::binary | std::ios::trunc);
+    STRIPE_CHECK(f.good(), "cannot write '" << tmp << "'");
+    f.write(bytes.data(), (std::streamsize)bytes.size());
+    f.flush();
+    STRIPE_CHECK(f.good(), "write failed for '" << tmp << "'");
+  }
+  STRIPE_CHECK(std::rename(tmp.c_str(), path.c_str()) == 0, "rename to '" << path << "' failed");
+}
+
+bool jpeg_path(const std::string& path) {
+  std::string ext = path.substr(path.find_last_of('.') == std::string::npos ? path.size() : path.find_last_of('.'));
+  for (auto& ch : ext) ch = (char)std::tolower((unsigned char)ch);
+  return ext == ".jpg" || ext == ".jpeg" || ext == ".jfif";
+}
+}  // namespace
+
+Image read_image(const std::string& path) {
+  const std::string bytes = slurp(path);
+  if (bytes.size() >= 2 && (uint8_t)bytes[0] == 0xFF && (uint8_t)bytes[1] == 0xD8) return decode_jpeg(bytes);
+  return decode_pnm(bytes);
+}
+
+void write_image(const std::string& path, const Image& img, int quality) {
+  if (jpeg_path(path)) write_atomic(path, encode_jpeg(img, quality));
+  else write_atomic(path, encode_pnm(img));
 }
 
 void synth_rows(uint64_t seed, int W, int C, int row0, int rows, uint8_t* dst) {

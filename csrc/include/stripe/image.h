@@ -38,6 +38,20 @@ void write_pnm(const std::string& path, const Image& img);
 Image decode_pnm(const std::string& bytes);
 std::string encode_pnm(const Image& img);
 
+// Baseline JPEG (csrc/core/jpeg.cpp): the reference's own input / output
+// format (cv::imread / imwrite, kernel.cu:110,236).  decode: sequential
+// Huffman, 1 or 3 components, any sampling, restart intervals; encode: JFIF,
+// 4:2:0 (subsample) or 4:4:4 YCbCr, quality 1..100 on the Annex K tables,
+// Huffman tables fitted to the image, optional restart interval (MCUs).
+Image decode_jpeg(const std::string& bytes);
+std::string encode_jpeg(const Image& img, int quality = 95, bool subsample = true, int restart_interval = 0);
+
+// By content on read (JPEG SOI or PNM magic), by extension on write
+// (.jpg/.jpeg -> JPEG at `quality`, anything else -> PNM); writes are atomic
+// (temp file + rename).
+Image read_image(const std::string& path);
+void write_image(const std::string& path, const Image& img, int quality = 95);
+
 // ---- synthetic random-pixel frames ----
 // Counter-based: byte (y, b) of a W*C row is a pure function of (seed, y, b), so
 // every rank generates its own stripe with no root copy and no host round trip.

@@ -79,6 +79,17 @@ PYBIND11_MODULE(_C, m) {
   m.def("write_pnm", [](const std::string& p, const U8Array& a) { write_pnm(p, image_from_numpy(a)); });
   m.def("decode_pnm", [](py::bytes b) { return image_to_numpy(decode_pnm(std::string(b))); });
   m.def("encode_pnm", [](const U8Array& a) { return py::bytes(encode_pnm(image_from_numpy(a))); });
+  m.def("decode_jpeg", [](py::bytes b) { return image_to_numpy(decode_jpeg(std::string(b))); });
+  m.def(
+      "encode_jpeg",
+      [](const U8Array& a, int quality, bool subsample, int restart) {
+        return py::bytes(encode_jpeg(image_from_numpy(a), quality, subsample, restart));
+      },
+      py::arg("img"), py::arg("quality") = 95, py::arg("subsample") = true, py::arg("restart_interval") = 0);
+  m.def("read_image", [](const std::string& p) { return image_to_numpy(read_image(p)); });
+  m.def(
+      "write_image", [](const std::string& p, const U8Array& a, int q) { write_image(p, image_from_numpy(a), q); },
+      py::arg("path"), py::arg("img"), py::arg("quality") = 95);
   m.def("synth_image", [](uint64_t seed, int W, int H, int C) { return image_to_numpy(synth_image(seed, W, H, C)); });
   m.def("synth_rows", [](uint64_t seed, int W, int C, int row0, int rows) {
     Image img(W, rows, C);

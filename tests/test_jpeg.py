@@ -1,0 +1,161 @@
+"""Native baseline JPEG codec (csrc/core/jpeg.cpp): the reference's own I/O
+format (cv::imread of a JPEG, kernel.cu:110; imwrite JPEG, kernel.cu:236).
+
+Oracle: Pillow (libjpeg-turbo) where it is importable.  Decoders may differ by
+the IDCT's arithmetic and the colour conversion's fixed point: ours (float
+IDCT, float YCbCr) stays within 3 levels of libjpeg-turbo's integer path, with
+a mean difference well under 0.1 level.
+"""
+import io
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PIL = pytest.importorskip("PIL.Image")
+
+
+def _smooth(h, w, c, noise=6.0, seed=0):
+    rng = np.random.default_rng(seed)
+    y, x = np.mgrid[0:h, 0:w]
+    base = np.stack([128 + 100 * np.sin(x / 17.0 + k) * np.cos(y / 23.0 - k) for k in range(c)], -1)
+    img = np.clip(base + rng.normal(0, noise, base.shape), 0, 255).astype(np.uint8)
+    return img[..., 0] if c == 1 else img
+
+
+def _pil_encode(img, **kw):
+    b = io.BytesIO()
+    PIL.fromarray(img).save(b, "JPEG", **kw)
+    return b.getvalue()
+
+
+def _pil_decode(data, gray):
+    return np.asarray(PIL.open(io.BytesIO(data)).convert("L" if gray else "RGB"))
+
+
+def _psnr(a, b):
+    mse = ((a.astype(np.float64) - b.astype(np.float64)) ** 2).mean()
+    return 10 * np.log10(255.0 ** 2 / max(mse, 1e-12))
+
+
+@pytest.mark.parametrize("shape", [(64, 64, 3), (67, 93, 3), (200, 301, 3), (57, 41, 1), (1, 1, 3), (9, 300, 1)])
+@pytest.mark.parametrize("subsampling", [0, 1, 2])  # Pillow: 4:4:4, 4:2:2, 4:2:0
+def test_decode_matches_libjpeg(C, shape, subsampling):
+    h, w, c = shape
+    if c == 1 and subsampling:
+        pytest.skip("gray has one sampling")
+    img = _smooth(h, w, c)
+    data = _pil_encode(img, quality=90, subsampling=subsampling)
+    ours = C.decode_jpeg(data)
+    ref = _pil_decode(data, c == 1)
+    assert ours.shape == ref.shape
+    d = np.abs(ours.astype(int) - ref.astype(int))
+    assert d.max() <= 3 and d.mean() < 0.1, (d.max(), d.mean())
+
+
+@pytest.mark.parametrize("quality", [10, 50, 95, 100])
+def test_decode_across_quality(C, quality):
+    img = _smooth(48, 80, 3, seed=quality)
+    data = _pil_encode(img, quality=quality)
+    d = np.abs(C.decode_jpeg(data).astype(int) - _pil_decode(data, False).astype(int))
+    assert d.max() <= 3 and d.mean() < 0.15
+
+
+@pytest.mark.parametrize("subsample", [True, False])
+@pytest.mark.parametrize("shape", [(64, 64, 3), (67, 93, 3), (33, 17, 1)])
+def test_encode_decodes_in_libjpeg(C, shape, subsample):
+    # our files are valid JFIF: libjpeg-turbo decodes them to what we decode,
+    # and the picture survives (a smooth frame at quality 95)
+    h, w, c = shape
+    img = _smooth(h, w, c, noise=0.0)
+    enc = C.encode_jpeg(img, 95, subsample, 0)
+    theirs = _pil_decode(enc, c == 1)
+    ours = C.decode_jpeg(enc)
+    assert np.abs(theirs.astype(int) - ours.astype(int)).max() <= 3
+    assert _psnr(theirs, img) > (36.0 if (subsample and c == 3) else 40.0)
+
+
+def test_encode_quality_orders_size_and_error(C):
+    img = _smooth(96, 128, 3)
+    sizes, errs = [], []
+    for q in (20, 60, 95):
+        enc = C.encode_jpeg(img, q)
+        sizes.append(len(enc))
+        errs.append(_psnr(C.decode_jpeg(enc), img))
+    assert sizes[0] < sizes[1] < sizes[2] and errs[0] < errs[1] < errs[2]
+
+
+def test_restart_interval_round_trip(C):
+    img = _smooth(120, 170, 3)
+    for ri in (1, 3, 7):
+        enc = C.encode_jpeg(img, 90, True, ri)
+        assert b"\xff\xdd" in enc and b"\xff\xd0" in enc
+        ours = C.decode_jpeg(enc)
+        assert np.abs(ours.astype(int) - _pil_decode(enc, False).astype(int)).max() <= 3
+        assert np.array_equal(ours, C.decode_jpeg(C.encode_jpeg(img, 90, True, ri)))
+
+
+def test_extreme_statistics_huffman_tables(C):
+    # pure noise at quality 100 (every AC symbol class) and a flat frame (a
+    # handful of symbols): the fitted Huffman tables stay valid JPEG (<= 16-bit
+    # codes, no all-ones code)
+    rng = np.random.default_rng(3)
+    for img in (rng.integers(0, 256, (64, 96, 3), dtype=np.uint8), np.full((40, 40, 3), 77, np.uint8),
+                np.zeros((16, 16), np.uint8)):
+        enc = C.encode_jpeg(img, 100, False, 0)
+        theirs = _pil_decode(enc, img.ndim == 2)
+        assert np.abs(theirs.astype(int) - C.decode_jpeg(enc).astype(int)).max() <= 3
+
+
+def test_progressive_refused_with_message(C):
+    data = _pil_encode(_smooth(32, 32, 3), quality=80, progressive=True)
+    with pytest.raises(RuntimeError, match="progressive"):
+        C.decode_jpeg(data)
+
+
+def test_corrupt_input_raises(C):
+    with pytest.raises(RuntimeError, match="JPEG"):
+        C.decode_jpeg(b"\xff\xd8\xff\xc0\x00")
+    good = C.encode_jpeg(_smooth(16, 16, 3), 90)
+    with pytest.raises(RuntimeError):
+        C.decode_jpeg(good[: len(good) // 3])  # truncated: header fine, tables / scan cut
+
+
+def test_read_image_sniffs_content_and_python_io(C, tmp_path):
+    import mpi_cuda_imagemanipulation_amd as m
+
+    img = _smooth(40, 50, 3)
+    p = tmp_path / "x.jpg"
+    m.utils.write_image(str(p), img, quality=92)
+    assert open(p, "rb").read(2) == b"\xff\xd8"
+    back = m.utils.read_image(str(p))
+    assert back.shape == img.shape and _psnr(back, img) > 30
+    # content, not extension, decides on read
+    q = tmp_path / "y.ppm"
+    q.write_bytes(p.read_bytes())
+    assert np.array_equal(C.read_image(str(q)), back)
+
+
+def test_cli_runs_on_jpeg_input_and_output(C, tmp_path):
+    # the reference's flow: JPEG in, filtered, JPEG out (kernel.cu:110,236)
+    import mpi_cuda_imagemanipulation_amd as m
+
+    img = _smooth(70, 90, 3)
+    src = tmp_path / "in.jpg"
+    src.write_bytes(_pil_encode(img, quality=92))
+    decoded = C.decode_jpeg(src.read_bytes())
+    cli = os.path.join(ROOT, "bin", "stripe")
+    if not os.path.exists(cli):
+        pytest.skip("bin/stripe not built")
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+    out_ppm, out_jpg = tmp_path / "out.ppm", tmp_path / "out.jpg"
+    for out in (out_ppm, out_jpg):
+        r = subprocess.run([cli, "run", "--input", str(src), "--output", str(out), "--chain", "gaussian5",
+                            "--backend", "host", "--quality", "97"], capture_output=True, text=True, env=env,
+                           timeout=120)
+        assert r.returncode == 0, r.stderr
+    ref = C.golden_apply(decoded, "gaussian5", "reflect101", True)
+    assert np.array_equal(m.utils.read_image(str(out_ppm)), ref)
+    assert _psnr(C.read_image(str(out_jpg)), ref) > 38

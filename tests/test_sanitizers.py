@@ -55,3 +55,28 @@ def test_asan_malformed_ppm(asan_cli, tmp_path, payload):
              "--backend", "host")
     assert "AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-3000:]
     assert r.returncode in (0, 1), (r.returncode, r.stderr[-2000:])
+
+
+def test_asan_jpeg_round_trip_and_mutations(asan_cli, tmp_path):
+    # JPEG in / out through the instrumented CLI, then corrupted JPEGs: each
+    # either decodes or fails with an error exit, never a sanitizer report
+    import random
+
+    src, out = str(tmp_path / "a.jpg"), str(tmp_path / "b.jpg")
+    assert _run(asan_cli, "gen", "--synthetic", "45x29x3", "--seed", "4", "--output", src).returncode == 0
+    r = _run(asan_cli, "run", "--input", src, "--output", out, "--chain", "gaussian5", "--backend", "host")
+    assert r.returncode == 0, r.stderr[-3000:]
+    good = open(src, "rb").read()
+    rnd = random.Random(11)
+    for k in range(24):
+        b = bytearray(good)
+        for _ in range(rnd.randint(1, 4)):
+            b[rnd.randrange(2, len(b))] = rnd.randrange(256)
+        if k % 4 == 3:
+            b = b[:rnd.randrange(2, len(b))]
+        f = tmp_path / f"bad{k}.jpg"
+        f.write_bytes(bytes(b))
+        r = _run(asan_cli, "run", "--input", str(f), "--output", str(tmp_path / "o.ppm"), "--chain", "gaussian5",
+                 "--backend", "host")
+        assert "AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-3000:]
+        assert r.returncode in (0, 1), (r.returncode, r.stderr[-2000:])

@@ -45,6 +45,7 @@ CORE_SOURCES = [
     "core/chain.cpp",
     "core/partition.cpp",
     "core/image.cpp",
+    "core/jpeg.cpp",
     "core/golden.cpp",
     "core/cpu_exec.cpp",
     "hip/pointwise.hip",
