@@ -159,3 +159,26 @@ def test_cli_runs_on_jpeg_input_and_output(C, tmp_path):
     ref = C.golden_apply(decoded, "gaussian5", "reflect101", True)
     assert np.array_equal(m.utils.read_image(str(out_ppm)), ref)
     assert _psnr(C.read_image(str(out_jpg)), ref) > 38
+
+
+@pytest.mark.gpu
+def test_cli_jpeg_on_gpu_ref_preset(C, tmp_path):
+    # the reference's whole flow on the GPU: JPEG in, gray -> contrast 3.5 ->
+    # emboss3 on 3 ranks (legacy split, stripes independent), expand, JPEG and
+    # PPM out; the PPM equals the golden path on the decoded frame
+    import numpy as np_
+
+    img = _smooth(211, 157, 3)
+    src = tmp_path / "in.jpg"
+    src.write_bytes(_pil_encode(img, quality=90))
+    cli = os.path.join(ROOT, "bin", "stripe")
+    out = tmp_path / "out.ppm"
+    r = subprocess.run([cli, "run", "--input", str(src), "--output", str(out), "--preset", "ref-gpu", "--ranks", "3",
+                        "--backend", "local"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-3000:]
+    got = C.read_image(str(out))
+    dec = C.decode_jpeg(src.read_bytes())
+    rows = 211 // 3
+    for k in range(3):
+        ref = C.golden_apply(dec[k * rows:(k + 1) * rows], "gray:ref,contrast:3.5,emboss3@skip,expand", "skip", True)
+        assert np_.array_equal(got[k * rows:(k + 1) * rows], ref), k
