@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round-4 refresh of the five BASELINE configs (tools/gpu_configs.sh) plus the
+# Round-4 refresh of the five BASELINE configs (tools/gpu/gpu_configs.sh) plus the
 # config-3 local-rank schedules side by side.  Output: gpurun_out/r4/configs.
 set -o pipefail
 export O=gpurun_out/r4/configs
 mkdir -p $O
-timeout -k 10 900 bash tools/gpu_configs.sh || exit 1
+timeout -k 10 900 bash tools/gpu/gpu_configs.sh || exit 1
 for d in 1 4 8; do
   echo "== cfg3 sobel 4 local ranks, halo depth $d" >> $O/configs.txt
   timeout -k 10 200 bin/stripe bench --synthetic 8192x8192x1 --chain sobel --ranks 4 --iters 48 --warmup 8 \
