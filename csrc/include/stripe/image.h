@@ -40,11 +40,13 @@ std::string encode_pnm(const Image& img);
 
 // Baseline JPEG (csrc/core/jpeg.cpp): the reference's own input / output
 // format (cv::imread / imwrite, kernel.cu:110,236).  decode: sequential
-// Huffman, 1 or 3 components, any sampling, restart intervals; encode: JFIF,
-// 4:2:0 (subsample) or 4:4:4 YCbCr, quality 1..100 on the Annex K tables,
-// Huffman tables fitted to the image, optional restart interval (MCUs).
+// Huffman, 1 or 3 components, any sampling, restart intervals (decoded in
+// parallel when every marker is in place); encode: JFIF, 4:2:0 (subsample)
+// or 4:4:4 YCbCr, quality 1..100 on the Annex K tables, Huffman tables fitted
+// to the image, restart interval in MCUs (-1: one MCU row, coded in parallel;
+// 0: none).
 Image decode_jpeg(const std::string& bytes);
-std::string encode_jpeg(const Image& img, int quality = 95, bool subsample = true, int restart_interval = 0);
+std::string encode_jpeg(const Image& img, int quality = 95, bool subsample = true, int restart_interval = -1);
 
 // By content on read (JPEG SOI or PNM magic), by extension on write
 // (.jpg/.jpeg -> JPEG at `quality`, anything else -> PNM); writes are atomic

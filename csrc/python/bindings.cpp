@@ -85,7 +85,7 @@ PYBIND11_MODULE(_C, m) {
       [](const U8Array& a, int quality, bool subsample, int restart) {
         return py::bytes(encode_jpeg(image_from_numpy(a), quality, subsample, restart));
       },
-      py::arg("img"), py::arg("quality") = 95, py::arg("subsample") = true, py::arg("restart_interval") = 0);
+      py::arg("img"), py::arg("quality") = 95, py::arg("subsample") = true, py::arg("restart_interval") = -1);
   m.def("read_image", [](const std::string& p) { return image_to_numpy(read_image(p)); });
   m.def(
       "write_image", [](const std::string& p, const U8Array& a, int q) { write_image(p, image_from_numpy(a), q); },

@@ -75,5 +75,6 @@ def decode_jpeg(data: bytes) -> np.ndarray:
     return C.decode_jpeg(data)
 
 
-def encode_jpeg(img, quality: int = 95, subsample: bool = True, restart_interval: int = 0) -> bytes:
+def encode_jpeg(img, quality: int = 95, subsample: bool = True, restart_interval: int = -1) -> bytes:
+    """restart_interval: MCUs per interval (-1: one MCU row, coded in parallel; 0: none)"""
     return C.encode_jpeg(np.ascontiguousarray(img, dtype=np.uint8), quality, subsample, restart_interval)

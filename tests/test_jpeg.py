@@ -182,3 +182,20 @@ def test_cli_jpeg_on_gpu_ref_preset(C, tmp_path):
     for k in range(3):
         ref = C.golden_apply(dec[k * rows:(k + 1) * rows], "gray:ref,contrast:3.5,emboss3@skip,expand", "skip", True)
         assert np_.array_equal(got[k * rows:(k + 1) * rows], ref), k
+
+
+def test_parallel_restart_intervals_decode_identically(C):
+    # the default encode puts a restart marker after every MCU row and both
+    # sides code the intervals in parallel: the coefficients do not depend on
+    # the intervals, so the decoded frames are bit-identical
+    img = _smooth(250, 333, 3, seed=5)
+    per_row, none, every3 = (C.encode_jpeg(img, 88, True, ri) for ri in (-1, 0, 3))
+    assert b"\xff\xdd" in per_row and b"\xff\xdd" not in none
+    ref = C.decode_jpeg(none)
+    assert np.array_equal(C.decode_jpeg(per_row), ref) and np.array_equal(C.decode_jpeg(every3), ref)
+    assert np.abs(_pil_decode(per_row, False).astype(int) - ref.astype(int)).max() <= 3
+    # a lost marker: the parallel split no longer matches, the sequential
+    # decoder resynchronises (no crash, same size)
+    k = per_row.index(b"\xff\xd3")
+    broken = per_row[:k] + per_row[k + 2:]
+    assert C.decode_jpeg(broken).shape == img.shape
