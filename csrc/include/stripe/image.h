@@ -48,6 +48,41 @@ std::string encode_pnm(const Image& img);
 Image decode_jpeg(const std::string& bytes);
 std::string encode_jpeg(const Image& img, int quality = 95, bool subsample = true, int restart_interval = -1);
 
+// The two stages of each direction, so the pixel stage can run on the GPU
+// (csrc/hip/jpeg_dev.hip) while the entropy stage stays on the host.
+// Decode: jpeg_entropy_decode() parses the file and Huffman-decodes every
+// block into dequantised DCT coefficients (natural order; block rows of the
+// MCU-padded component plane); jpeg_pixels() runs IDCT + upsampling + colour.
+struct JpegCoefs {
+  int W = 0, H = 0, hmax = 1, vmax = 1;
+  bool rgb = false;  // three components stored as R, G, B (no colour transform)
+  struct Comp {
+    int h = 1, v = 1, bw = 0, bh = 0;  // sampling factors, blocks per row / column
+    std::vector<int16_t> coef;         // bw * bh * 64
+  };
+  std::vector<Comp> comps;
+};
+JpegCoefs jpeg_entropy_decode(const std::string& bytes);
+Image jpeg_pixels(JpegCoefs&& jc);
+// Encode: jpeg_quantise() = colour conversion, chroma subsampling, forward DCT
+// and quantisation (zigzag order per block); jpeg_entropy_encode() = Huffman
+// tables fitted to the coefficients + the JFIF stream.
+struct JpegQuant {
+  int W = 0, H = 0, hs = 1;  // hs: luma sampling factor (2 = 4:2:0)
+  uint16_t q[2][64] = {};    // luma / chroma quantisation tables (natural order)
+  struct Comp {
+    int f = 1, bw = 0, bh = 0;  // sampling factor, blocks per row / column
+    std::vector<int16_t> coef;  // bw * bh * 64, zigzag order
+  };
+  std::vector<Comp> comps;
+};
+JpegQuant jpeg_quantise(const Image& img, int quality, bool subsample);
+std::string jpeg_entropy_encode(const JpegQuant& jq, int restart_interval = -1);
+// quantisation tables of a quality (natural order) and the zigzag map
+// (zigzag index -> natural index), shared with the device stages
+void jpeg_tables(int quality, uint16_t luma[64], uint16_t chroma[64]);
+const int* jpeg_zigzag();
+
 // By content on read (JPEG SOI or PNM magic), by extension on write
 // (.jpg/.jpeg -> JPEG at `quality`, anything else -> PNM); writes are atomic
 // (temp file + rename).
