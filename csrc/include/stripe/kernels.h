@@ -10,6 +10,7 @@
 #include <cstdint>
 
 #include "stripe/chain.h"
+#include "stripe/image.h"
 
 namespace stripe {
 
@@ -98,5 +99,15 @@ void launch_conv_small(const Pass& p, const PassLaunch& L, hipStream_t s);
 bool sep_supported(const Pass& p);
 void prepare_sep_consts(const Pass& p, PassConsts* pc, hipStream_t s);
 void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, hipStream_t s);
+
+// ---- JPEG pixel stages on the device (csrc/hip/jpeg_dev.hip) ----
+// IDCT + chroma upsampling + YCbCr -> RGB of entropy-decoded coefficients into
+// interleaved rows of `pitch` bytes at dst (device), queued on s.
+void jpeg_pixels_device(const JpegCoefs& jc, uint8_t* dst, int64_t pitch, hipStream_t s);
+// Colour conversion, chroma subsampling, forward DCT and quantisation of an
+// interleaved device frame; returns the coefficients (host) for
+// jpeg_entropy_encode (synchronises s).
+JpegQuant jpeg_quantise_device(const uint8_t* src, int64_t pitch, int W, int H, int C, int quality, bool subsample,
+                               hipStream_t s);
 
 }  // namespace stripe

@@ -86,6 +86,42 @@ PYBIND11_MODULE(_C, m) {
         return py::bytes(encode_jpeg(image_from_numpy(a), quality, subsample, restart));
       },
       py::arg("img"), py::arg("quality") = 95, py::arg("subsample") = true, py::arg("restart_interval") = -1);
+  // JPEG split at the entropy stage: Huffman on the host, pixels on the GPU
+  py::class_<JpegCoefs>(m, "JpegCoefs")
+      .def_readonly("W", &JpegCoefs::W)
+      .def_readonly("H", &JpegCoefs::H)
+      .def_property_readonly("C", [](const JpegCoefs& j) { return (int)j.comps.size(); })
+      .def(
+          "to_device",
+          [](const JpegCoefs& j, uintptr_t dst, int64_t pitch, uintptr_t stream) {
+            py::gil_scoped_release nogil;
+            jpeg_pixels_device(j, reinterpret_cast<uint8_t*>(dst), pitch, as_stream(stream));
+          },
+          py::arg("dst"), py::arg("pitch"), py::arg("stream") = 0)
+      .def("to_host", [](const JpegCoefs& j) {
+        JpegCoefs c = j;
+        return image_to_numpy(jpeg_pixels(std::move(c)));
+      });
+  m.def("jpeg_entropy_decode", [](py::bytes b) {
+    const std::string s(b);
+    py::gil_scoped_release nogil;
+    return jpeg_entropy_decode(s);
+  });
+  m.def(
+      "jpeg_encode_device",
+      [](uintptr_t src, int64_t pitch, int W, int H, int C, int quality, bool subsample, int restart, uintptr_t stream) {
+        std::string out;
+        {
+          py::gil_scoped_release nogil;
+          out = jpeg_entropy_encode(
+              jpeg_quantise_device(reinterpret_cast<const uint8_t*>(src), pitch, W, H, C, quality, subsample,
+                                   as_stream(stream)),
+              restart);
+        }
+        return py::bytes(out);
+      },
+      py::arg("src"), py::arg("pitch"), py::arg("W"), py::arg("H"), py::arg("C"), py::arg("quality") = 95,
+      py::arg("subsample") = true, py::arg("restart_interval") = -1, py::arg("stream") = 0);
   m.def("read_image", [](const std::string& p) { return image_to_numpy(read_image(p)); });
   m.def(
       "write_image", [](const std::string& p, const U8Array& a, int q) { write_image(p, image_from_numpy(a), q); },

@@ -78,3 +78,43 @@ def decode_jpeg(data: bytes) -> np.ndarray:
 def encode_jpeg(img, quality: int = 95, subsample: bool = True, restart_interval: int = -1) -> bytes:
     """restart_interval: MCUs per interval (-1: one MCU row, coded in parallel; 0: none)"""
     return C.encode_jpeg(np.ascontiguousarray(img, dtype=np.uint8), quality, subsample, restart_interval)
+
+
+def read_image_device(path: str, device=None):
+    """Decode an image straight into a CUDA uint8 tensor (HxW or HxWx3).
+    Baseline JPEG: Huffman decoding on the host, IDCT + upsampling + colour on
+    the GPU (csrc/hip/jpeg_dev.hip) -- only the coefficients cross the link.
+    Other formats: host decode, then one upload."""
+    import torch
+
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    data = open(str(path), "rb").read()
+    if data[:2] != b"\xff\xd8":
+        return torch.from_numpy(read_image(path)).to(dev)
+    jc = C.jpeg_entropy_decode(data)
+    shape = (jc.H, jc.W) if jc.C == 1 else (jc.H, jc.W, jc.C)
+    out = torch.empty(shape, dtype=torch.uint8, device=dev)
+    with torch.cuda.device(dev):
+        jc.to_device(out.data_ptr(), jc.W * jc.C, torch.cuda.current_stream(dev).cuda_stream)
+    return out
+
+
+def write_image_device(path: str, img, quality: int = 95) -> None:
+    """Write a CUDA uint8 tensor: JPEG paths encode with colour conversion,
+    DCT and quantisation on the GPU and Huffman coding on the host (restart
+    interval per MCU row, coded in parallel); other formats via the host."""
+    import torch
+
+    if not _is_jpeg(path) or not (hasattr(img, "is_cuda") and img.is_cuda):
+        write_image(path, img, quality)
+        return
+    x = img.contiguous()
+    H, W = int(x.shape[0]), int(x.shape[1])
+    Cc = 1 if x.dim() == 2 else int(x.shape[2])
+    with torch.cuda.device(x.device):
+        data = C.jpeg_encode_device(x.data_ptr(), W * Cc, W, H, Cc, quality, True, -1,
+                                    torch.cuda.current_stream(x.device).cuda_stream)
+    tmp = f"{path}.tmp{os.getpid()}"
+    with open(tmp, "wb") as f:
+        f.write(data)
+    os.replace(tmp, str(path))

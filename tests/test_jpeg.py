@@ -199,3 +199,59 @@ def test_parallel_restart_intervals_decode_identically(C):
     k = per_row.index(b"\xff\xd3")
     broken = per_row[:k] + per_row[k + 2:]
     assert C.decode_jpeg(broken).shape == img.shape
+
+
+# ---- pixel stages on the GPU (csrc/hip/jpeg_dev.hip) ----
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,subsampling", [((211, 157, 3), 0), ((211, 157, 3), 1), ((211, 157, 3), 2),
+                                               ((64, 99, 1), 0), ((1, 1, 3), 2)])
+def test_device_decode_matches_host(C, tmp_path, shape, subsampling):
+    import mpi_cuda_imagemanipulation_amd as m
+
+    h, w, c = shape
+    img = _smooth(h, w, c)
+    data = _pil_encode(img, quality=90, **({"subsampling": subsampling} if c == 3 else {}))
+    p = tmp_path / "x.jpg"
+    p.write_bytes(data)
+    got = m.utils.read_image_device(str(p))
+    assert got.is_cuda and tuple(got.shape) == img.shape
+    d = np.abs(got.cpu().numpy().astype(int) - C.decode_jpeg(data).astype(int))
+    assert d.max() <= 1 and (d > 0).mean() < 0.01, (d.max(), (d > 0).mean())
+
+
+@pytest.mark.gpu
+def test_device_decode_restart_intervals_and_rgb_output_pitch(C):
+    import torch
+
+    img = _smooth(300, 401, 3, seed=2)
+    data = C.encode_jpeg(img, 85, True, -1)
+    jc = C.jpeg_entropy_decode(data)
+    assert (jc.W, jc.H, jc.C) == (401, 300, 3)
+    pitch = 401 * 3 + 64  # a padded destination (e.g. an engine stripe row)
+    buf = torch.full((300, pitch), 7, dtype=torch.uint8, device="cuda")
+    jc.to_device(buf.data_ptr(), pitch, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    out = buf.cpu().numpy()
+    assert (out[:, 401 * 3:] == 7).all()  # nothing written past the row
+    d = np.abs(out[:, :401 * 3].reshape(300, 401, 3).astype(int) - jc.to_host().astype(int))
+    assert d.max() <= 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c", [3, 1])
+def test_device_encode_matches_host(C, tmp_path, c):
+    import torch
+
+    import mpi_cuda_imagemanipulation_amd as m
+
+    img = _smooth(250, 333, c, seed=4)
+    p = tmp_path / "o.jpg"
+    m.utils.write_image_device(str(p), torch.from_numpy(img).cuda(), quality=90)
+    enc = p.read_bytes()
+    ours = C.decode_jpeg(enc)
+    ref = C.decode_jpeg(C.encode_jpeg(img, 90, True, -1))
+    # a coefficient on a quantisation tie may round the other way: tiny differences only
+    d = np.abs(ours.astype(int) - ref.astype(int))
+    assert d.mean() < 0.05 and _psnr(ours, ref) > 45
+    assert np.abs(_pil_decode(enc, c == 1).astype(int) - ours.astype(int)).max() <= 3
+    assert _psnr(ours, img) > 30
