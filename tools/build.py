@@ -56,6 +56,7 @@ CORE_SOURCES = [
     "hip/stencil_inst_d.hip",
     "hip/conv.hip",
     "hip/blur_sep.hip",
+    "hip/jpeg_dev.hip",
     "hip/dispatch.cpp",
     "runtime/comm_rccl.cpp",
     "runtime/comm_local.cpp",
