@@ -203,6 +203,38 @@ UniqueId file_rendezvous(const std::string& path, int rank) {
   }
 }
 
+// Rank 0's input.  A baseline JPEG bound for a device run stays as its
+// entropy-decoded coefficients: the pixel stage (IDCT, upsampling, colour)
+// then runs on the GPU straight into the root buffer (csrc/hip/jpeg_dev.hip);
+// any other input, or a host run, decodes here.
+struct Input {
+  Image img;
+  JpegCoefs jpeg;
+  bool coefs = false;
+  int W = 0, H = 0, C = 0;
+};
+
+Input read_input(const std::string& path, bool device) {
+  std::ifstream f(path, std::ios::binary);
+  STRIPE_CHECK(f.good(), "cannot open '" << path << "'");
+  const std::string bytes((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+  const bool jpeg = bytes.size() >= 2 && (uint8_t)bytes[0] == 0xFF && (uint8_t)bytes[1] == 0xD8;
+  Input in;
+  if (jpeg && device) {
+    in.jpeg = jpeg_entropy_decode(bytes);
+    in.coefs = true;
+    in.W = in.jpeg.W;
+    in.H = in.jpeg.H;
+    in.C = (int)in.jpeg.comps.size();
+    return in;
+  }
+  in.img = jpeg ? decode_jpeg(bytes) : decode_pnm(bytes);
+  in.W = in.img.W;
+  in.H = in.img.H;
+  in.C = in.img.C;
+  return in;
+}
+
 // One rank of a multi-process job: `stripe run --backend rccl --world N --rank r
 // --rendezvous FILE [--device d]` (like the reference's `mpiexec -n N`, one
 // process per rank; only rank 0 reads the input and writes the output).
@@ -212,12 +244,12 @@ int cmd_run_rank(const Args& a) {
   STRIPE_CHECK(a.has("rendezvous"), "multi-process runs need --rendezvous FILE (shared by all ranks)");
   const int ndev = device_count();
   const int device = a.geti("device", ndev > 0 ? rank % ndev : 0);
-  Image img;
+  Input in;
   EngineConfig cfg;
   if (rank == 0) {
     STRIPE_CHECK(a.has("input") && a.has("output"), "rank 0 needs --input and --output");
-    img = read_image(a.get("input"));
-    cfg = config_from(a, img.W, img.H, img.C);
+    in = read_input(a.get("input"), true);
+    cfg = config_from(a, in.W, in.H, in.C);
   } else {
     cfg = config_from(a, 1, 1, 3);  // geometry arrives with the metadata broadcast
   }
@@ -228,7 +260,9 @@ int cmd_run_rank(const Args& a) {
   const auto t0 = std::chrono::steady_clock::now();
   Image out;
   try {
-    out = run_rank(cfg, comm.get(), device, rank == 0 ? &img : nullptr, a.geti("iterations", 1), &t);
+    out = rank == 0 && in.coefs ? run_rank(cfg, comm.get(), device, &in.jpeg, a.geti("iterations", 1), &t)
+                                : run_rank(cfg, comm.get(), device, rank == 0 ? &in.img : nullptr,
+                                           a.geti("iterations", 1), &t);
   } catch (...) {
     comm->abort("rank failed");
     throw;
@@ -238,7 +272,7 @@ int cmd_run_rank(const Args& a) {
     write_image(a.get("output"), out, a.geti("quality", 95));
     std::printf("{\"cmd\":\"run\",\"W\":%d,\"H\":%d,\"C\":%d,\"ranks\":%d,\"backend\":\"rccl\",\"processes\":%d,"
                 "\"chain\":\"%s\",\"wall_ms\":%.3f,\"kernel_ms\":%.4f,\"scatter_ms\":%.4f,\"gather_ms\":%.4f}\n",
-                img.W, img.H, img.C, world, world, cfg.chain.c_str(), ms, t.run, t.scatter, t.gather);
+                in.W, in.H, in.C, world, world, cfg.chain.c_str(), ms, t.run, t.scatter, t.gather);
   }
   return 0;
 }
@@ -246,8 +280,9 @@ int cmd_run_rank(const Args& a) {
 int cmd_run(const Args& a) {
   if (a.has("world")) return cmd_run_rank(a);
   STRIPE_CHECK(a.has("input") && a.has("output"), "run needs --input and --output");
-  Image img = read_image(a.get("input"));
-  EngineConfig cfg = config_from(a, img.W, img.H, img.C);
+  const bool host_run = a.get("backend", device_count() > 0 ? "local" : "host") == "host";
+  const Input in = read_input(a.get("input"), !host_run);
+  EngineConfig cfg = config_from(a, in.W, in.H, in.C);
   const int N = a.geti("ranks", 1);
   const std::string backend = a.get("backend", cfg.backend == BackendKind::Host ? "host" : "local");
   const int iters = a.geti("iterations", 1);
@@ -259,12 +294,13 @@ int cmd_run(const Args& a) {
   Group g = make_group(backend, N, parse_int_list(a.get("devices")));
   PhaseTimes t;
   const auto t0 = std::chrono::steady_clock::now();
-  Image out = run_group(cfg, g.comms, g.devices, img, iters, &t);
+  Image out = in.coefs ? run_group(cfg, g.comms, g.devices, in.jpeg, iters, &t)
+                       : run_group(cfg, g.comms, g.devices, in.img, iters, &t);
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   write_image(a.get("output"), out, a.geti("quality", 95));
   std::printf("{\"cmd\":\"run\",\"W\":%d,\"H\":%d,\"C\":%d,\"ranks\":%d,\"backend\":\"%s\",\"chain\":\"%s\","
               "\"wall_ms\":%.3f,\"kernel_ms\":%.4f,\"scatter_ms\":%.4f,\"gather_ms\":%.4f}\n",
-              img.W, img.H, img.C, N, backend.c_str(), cfg.chain.c_str(), ms, t.run, t.scatter, t.gather);
+              in.W, in.H, in.C, N, backend.c_str(), cfg.chain.c_str(), ms, t.run, t.scatter, t.gather);
   return 0;
 }
 

@@ -141,6 +141,9 @@ class Engine {
   void load_synthetic(uint64_t seed);                     // own stripe, generated in place
   void load_packed(const void* src, bool src_device);     // own stripe, packed rows
   void load_root(const void* full, bool src_device);      // rank 0: full frame into root buffer
+  // rank 0: a baseline JPEG's entropy-decoded coefficients into the root
+  // buffer; a device engine runs IDCT / upsampling / colour on the GPU
+  void load_root_jpeg(const JpegCoefs& jc);
   void load_root_synthetic(uint64_t seed);                // rank 0: synthetic full frame on device
   void scatter();                                         // root buffer -> every rank's stripe
 
@@ -310,6 +313,10 @@ class Engine {
 // `input` is read on rank 0 only; `device` is this rank's GPU (-1: keep).
 Image run_rank(const EngineConfig& cfg, Comm* comm, int device, const Image* input, int iterations,
                PhaseTimes* times = nullptr);
+// Same, rank 0's input a baseline JPEG decoded as far as its coefficients
+// (jpeg_entropy_decode): the pixels are made where the root buffer lives.
+Image run_rank(const EngineConfig& cfg, Comm* comm, int device, const JpegCoefs* input, int iterations,
+               PhaseTimes* times = nullptr);
 // Small host buffer broadcast over a communicator (metadata, <= 256 bytes).
 void broadcast_small(Comm* comm, void* host, size_t bytes, int root, int device);
 
@@ -328,5 +335,7 @@ Image run_local_group(const EngineConfig& cfg, int world, const Image& input, in
 // devices[r] is rank r's HIP device (empty: keep cfg.device).
 Image run_group(const EngineConfig& cfg, const std::vector<Comm*>& comms, const std::vector<int>& devices,
                 const Image& input, int iterations, PhaseTimes* times = nullptr);
+Image run_group(const EngineConfig& cfg, const std::vector<Comm*>& comms, const std::vector<int>& devices,
+                const JpegCoefs& input, int iterations, PhaseTimes* times = nullptr);
 
 }  // namespace stripe

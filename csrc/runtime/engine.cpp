@@ -374,6 +374,24 @@ void Engine::load_root(const void* full, bool src_device) {
   fill_margins(org, C, 0, cfg_.H, plan_.in_margin_px, plan_.in_margin_border, s_compute_);
 }
 
+void Engine::load_root_jpeg(const JpegCoefs& jc) {
+  if (rank_ != 0) return;
+  STRIPE_CHECK(root_in_.data() != nullptr, "root buffers not allocated (EngineConfig::root_buffers)");
+  const int C = plan_.cin;
+  STRIPE_CHECK(jc.W == cfg_.W && jc.H == cfg_.H && (int)jc.comps.size() == C,
+               "JPEG " << jc.W << "x" << jc.H << "x" << jc.comps.size() << " does not match the engine's " << cfg_.W
+                       << "x" << cfg_.H << "x" << C);
+  if (!device()) {
+    JpegCoefs copy = jc;
+    const Image img = jpeg_pixels(std::move(copy));
+    load_root(img.data.data(), false);
+    return;
+  }
+  uint8_t* org = root_origin(root_in_, C);
+  jpeg_pixels_device(jc, org, pitch(C), s_compute_);
+  fill_margins(org, C, 0, cfg_.H, plan_.in_margin_px, plan_.in_margin_border, s_compute_);
+}
+
 void Engine::load_root_synthetic(uint64_t seed) {
   if (rank_ != 0) return;
   STRIPE_CHECK(root_in_.data() != nullptr, "root buffers not allocated (EngineConfig::root_buffers)");
@@ -1724,18 +1742,19 @@ double probe_link_rate(Comm* comm, int device, size_t bytes, int reps) {
   return rate;
 }
 
-Image run_rank(const EngineConfig& cfg_in, Comm* comm, int device, const Image* input, int iterations,
-               PhaseTimes* times) {
+namespace {
+Image run_rank_impl(const EngineConfig& cfg_in, Comm* comm, int device, const Image* input, const JpegCoefs* jpeg,
+                    int iterations, PhaseTimes* times) {
   const int rank = comm ? comm->rank() : 0;
   EngineConfig c = cfg_in;
   // the root knows the geometry (it read the image); everyone else learns it
   // from the metadata broadcast
   int meta[4] = {c.W, c.H, c.C, 0};
   if (rank == 0) {
-    STRIPE_CHECK(input != nullptr, "rank 0 needs the input image");
-    meta[0] = input->W;
-    meta[1] = input->H;
-    meta[2] = input->C;
+    STRIPE_CHECK(input != nullptr || jpeg != nullptr, "rank 0 needs the input image");
+    meta[0] = input ? input->W : jpeg->W;
+    meta[1] = input ? input->H : jpeg->H;
+    meta[2] = input ? input->C : (int)jpeg->comps.size();
   }
   broadcast_small(comm, meta, sizeof meta, 0, device);
   c.W = meta[0];
@@ -1744,7 +1763,10 @@ Image run_rank(const EngineConfig& cfg_in, Comm* comm, int device, const Image* 
   c.root_buffers = true;
   if (device >= 0) c.device = device;
   Engine e(c, comm);
-  if (rank == 0) e.load_root(input->data.data(), false);
+  if (rank == 0) {
+    if (input) e.load_root(input->data.data(), false);
+    else e.load_root_jpeg(*jpeg);
+  }
   if (iterations == 1 && c.dist_chunks > 1 && (e.dist_chunks(c.dist_chunks) > 0 || e.dist_direct())) {
     e.run_dist(c.dist_chunks);
   } else {
@@ -1762,10 +1784,22 @@ Image run_rank(const EngineConfig& cfg_in, Comm* comm, int device, const Image* 
   if (comm) comm->barrier();
   return out;
 }
+}  // namespace
 
-Image run_group(const EngineConfig& cfg, const std::vector<Comm*>& comms, const std::vector<int>& devices,
-                const Image& input, int iterations, PhaseTimes* times) {
-  STRIPE_CHECK(input.W == cfg.W && input.H == cfg.H && input.C == cfg.C, "input does not match the config");
+Image run_rank(const EngineConfig& cfg, Comm* comm, int device, const Image* input, int iterations,
+               PhaseTimes* times) {
+  return run_rank_impl(cfg, comm, device, input, nullptr, iterations, times);
+}
+
+Image run_rank(const EngineConfig& cfg, Comm* comm, int device, const JpegCoefs* input, int iterations,
+               PhaseTimes* times) {
+  return run_rank_impl(cfg, comm, device, nullptr, input, iterations, times);
+}
+
+namespace {
+template <class In>
+Image run_group_impl(const EngineConfig& cfg, const std::vector<Comm*>& comms, const std::vector<int>& devices,
+                     const In& input, int iterations, PhaseTimes* times) {
   const int world = (int)comms.size();
   Image out;
   std::mutex mu;
@@ -1798,6 +1832,20 @@ Image run_group(const EngineConfig& cfg, const std::vector<Comm*>& comms, const 
   for (auto& t : th) t.join();
   if (err) std::rethrow_exception(err);
   return out;
+}
+}  // namespace
+
+Image run_group(const EngineConfig& cfg, const std::vector<Comm*>& comms, const std::vector<int>& devices,
+                const Image& input, int iterations, PhaseTimes* times) {
+  STRIPE_CHECK(input.W == cfg.W && input.H == cfg.H && input.C == cfg.C, "input does not match the config");
+  return run_group_impl(cfg, comms, devices, input, iterations, times);
+}
+
+Image run_group(const EngineConfig& cfg, const std::vector<Comm*>& comms, const std::vector<int>& devices,
+                const JpegCoefs& input, int iterations, PhaseTimes* times) {
+  STRIPE_CHECK(input.W == cfg.W && input.H == cfg.H && (int)input.comps.size() == cfg.C,
+               "input does not match the config");
+  return run_group_impl(cfg, comms, devices, input, iterations, times);
 }
 
 Image run_local_group(const EngineConfig& cfg, int world, const Image& input, int iterations, PhaseTimes* times) {
