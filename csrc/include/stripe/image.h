@@ -9,7 +9,9 @@
 #pragma once
 
 #include <cstdint>
+#include <memory>
 #include <string>
+#include <utility>
 #include <vector>
 
 #if defined(__HIPCC__)
@@ -53,12 +55,34 @@ std::string encode_jpeg(const Image& img, int quality = 95, bool subsample = tru
 // Decode: jpeg_entropy_decode() parses the file and Huffman-decodes every
 // block into dequantised DCT coefficients (natural order; block rows of the
 // MCU-padded component plane); jpeg_pixels() runs IDCT + upsampling + colour.
+// Vector storage that does not zero on resize (large coefficient planes are
+// first touched by parallel workers instead of one thread's value-init).
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = NoInitAlloc<U>;
+  };
+  NoInitAlloc() = default;
+  template <class U>
+  NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
+  template <class U>
+  void construct(U* p) noexcept {
+    ::new ((void*)p) U;
+  }
+  template <class U, class... A>
+  void construct(U* p, A&&... a) {
+    ::new ((void*)p) U(std::forward<A>(a)...);
+  }
+};
+using CoefVec = std::vector<int16_t, NoInitAlloc<int16_t>>;
+
 struct JpegCoefs {
   int W = 0, H = 0, hmax = 1, vmax = 1;
   bool rgb = false;  // three components stored as R, G, B (no colour transform)
   struct Comp {
     int h = 1, v = 1, bw = 0, bh = 0;  // sampling factors, blocks per row / column
-    std::vector<int16_t> coef;         // bw * bh * 64
+    CoefVec coef;                      // bw * bh * 64
   };
   std::vector<Comp> comps;
 };
@@ -72,7 +96,7 @@ struct JpegQuant {
   uint16_t q[2][64] = {};    // luma / chroma quantisation tables (natural order)
   struct Comp {
     int f = 1, bw = 0, bh = 0;  // sampling factor, blocks per row / column
-    std::vector<int16_t> coef;  // bw * bh * 64, zigzag order
+    CoefVec coef;               // bw * bh * 64, zigzag order
   };
   std::vector<Comp> comps;
 };
