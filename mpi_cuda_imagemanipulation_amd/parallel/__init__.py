@@ -351,8 +351,8 @@ class FrameStream:
         return self.head.engine.halo_schedule
 
     def pick_schedule(self, reduce_max=None, barrier=None, steps: int = 0, rounds: int = 2) -> dict:
-        """Time every halo schedule that differs on this engine (interior /
-        boundary overlap, the three-stream pipeline, the plain serial one),
+        """Time every halo schedule (interior / boundary overlap, the
+        three-stream pipeline, the plain serial one),
         with the frames on one stream or alternating over two, on the real
         transport, and keep the fastest; returns {"chosen", "streams", "ms"}
         ("ms" keys: schedule, or schedule@streams when both counts are tried).
@@ -362,19 +362,18 @@ class FrameStream:
         same choice (each rank times the same steps; collective order holds)."""
         reduce_max = reduce_max or (lambda v: v)
         barrier = barrier or (lambda: None)
-        scheds = []
-        for s in self.SCHEDULES:
-            self.set_schedule(s)
-            eff = self.schedule
-            if eff not in scheds:
-                scheds.append(eff)
+        # the candidate list must be the same on every rank (each timing is a
+        # collective reduce_max): device engines try every schedule, even one a
+        # rank's own stripe runs another way (e.g. a thin stripe without the
+        # pipeline); host engines have one schedule and time nothing
+        scheds = list(self.SCHEDULES) if self.streams else ["serial"]
         opts = list(self.stream_options)
         cands = [(s, ns) for ns in opts for s in scheds]
         key = (lambda c: f"{c[0]}@{c[1]}") if len(opts) > 1 else (lambda c: c[0])
         if len(cands) == 1:
             self.set_schedule(scheds[0])
             self.set_streams(opts[0])
-            return {"chosen": scheds[0], "streams": self.nstreams, "ms": {}}
+            return {"chosen": self.schedule, "streams": self.nstreams, "ms": {}}
         n = steps if steps > 0 else max(60, 4 * len(self.frames))
         best = {}
         for _ in range(rounds):

@@ -363,7 +363,8 @@ def test_frame_stream_pick_schedule_single_candidate(C, monkeypatch):
 
 
 def test_frame_stream_pick_schedule_takes_fastest_max_over_ranks():
-    # three schedules that differ: each is timed `rounds` times, the per-rank
+    # device engines: all three schedules are timed `rounds` times (the same
+    # list on every rank, whatever each rank's stripe runs), the per-rank
     # time goes through reduce_max (every rank must agree), the fastest wins
     # and stays set on every frame
     import time as _t
@@ -375,7 +376,8 @@ def test_frame_stream_pick_schedule_takes_fastest_max_over_ranks():
     frames = [SimpleNamespace(engine=SimpleNamespace(halo_schedule="pipeline")) for _ in range(2)]
     fs = parallel.FrameStream.__new__(parallel.FrameStream)
     fs.frames = frames
-    fs.streams, fs.stream_options, fs.nstreams = [], [1], 1  # host: no streams to alternate
+    fs.streams, fs.stream_options, fs.nstreams = [object()], [1], 1  # a device stream stand-in
+    fs.set_streams = lambda n: None
     fs.step = lambda i=None: _t.sleep(cost[frames[0].engine.halo_schedule])
     fs.synchronize = lambda: None
     seen = []
