@@ -259,17 +259,21 @@ int cmd_run_rank(const Args& a) {
   PhaseTimes t;
   const auto t0 = std::chrono::steady_clock::now();
   Image out;
+  JpegOut jo;
   try {
-    out = rank == 0 && in.coefs ? run_rank(cfg, comm.get(), device, &in.jpeg, a.geti("iterations", 1), &t)
+    jo.quality = a.geti("quality", 95);
+    JpegOut* jp = rank == 0 && is_jpeg_path(a.get("output")) ? &jo : nullptr;
+    out = rank == 0 && in.coefs ? run_rank(cfg, comm.get(), device, &in.jpeg, a.geti("iterations", 1), &t, jp)
                                 : run_rank(cfg, comm.get(), device, rank == 0 ? &in.img : nullptr,
-                                           a.geti("iterations", 1), &t);
+                                           a.geti("iterations", 1), &t, jp);
   } catch (...) {
     comm->abort("rank failed");
     throw;
   }
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (rank == 0) {
-    write_image(a.get("output"), out, a.geti("quality", 95));
+    if (is_jpeg_path(a.get("output"))) write_file_atomic(a.get("output"), jo.bytes);  // encoded from the root buffer
+    else write_image(a.get("output"), out, a.geti("quality", 95));
     std::printf("{\"cmd\":\"run\",\"W\":%d,\"H\":%d,\"C\":%d,\"ranks\":%d,\"backend\":\"rccl\",\"processes\":%d,"
                 "\"chain\":\"%s\",\"wall_ms\":%.3f,\"kernel_ms\":%.4f,\"scatter_ms\":%.4f,\"gather_ms\":%.4f}\n",
                 in.W, in.H, in.C, world, world, cfg.chain.c_str(), ms, t.run, t.scatter, t.gather);
@@ -294,10 +298,16 @@ int cmd_run(const Args& a) {
   Group g = make_group(backend, N, parse_int_list(a.get("devices")));
   PhaseTimes t;
   const auto t0 = std::chrono::steady_clock::now();
-  Image out = in.coefs ? run_group(cfg, g.comms, g.devices, in.jpeg, iters, &t)
-                       : run_group(cfg, g.comms, g.devices, in.img, iters, &t);
+  // a JPEG output is encoded from the root buffer (device: colour + DCT +
+  // quantisation on the GPU), not from a host copy of the frame
+  JpegOut jo;
+  jo.quality = a.geti("quality", 95);
+  JpegOut* jp = is_jpeg_path(a.get("output")) ? &jo : nullptr;
+  Image out = in.coefs ? run_group(cfg, g.comms, g.devices, in.jpeg, iters, &t, jp)
+                       : run_group(cfg, g.comms, g.devices, in.img, iters, &t, jp);
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  write_image(a.get("output"), out, a.geti("quality", 95));
+  if (jp) write_file_atomic(a.get("output"), jo.bytes);
+  else write_image(a.get("output"), out, a.geti("quality", 95));
   std::printf("{\"cmd\":\"run\",\"W\":%d,\"H\":%d,\"C\":%d,\"ranks\":%d,\"backend\":\"%s\",\"chain\":\"%s\","
               "\"wall_ms\":%.3f,\"kernel_ms\":%.4f,\"scatter_ms\":%.4f,\"gather_ms\":%.4f}\n",
               in.W, in.H, in.C, N, backend.c_str(), cfg.chain.c_str(), ms, t.run, t.scatter, t.gather);

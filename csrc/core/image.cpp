@@ -119,7 +119,9 @@ std::string slurp(const std::string& path) {
   return std::string((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
 }
 
-void write_atomic(const std::string& path, const std::string& bytes) {
+}  // namespace
+
+void write_file_atomic(const std::string& path, const std::string& bytes) {
   const std::string tmp = path + ".tmp." + std::to_string(getpid());
   {
     std::ofstream f(tmp, std::ios::binary | std::ios::trunc);
@@ -131,12 +133,11 @@ void write_atomic(const std::string& path, const std::string& bytes) {
   STRIPE_CHECK(std::rename(tmp.c_str(), path.c_str()) == 0, "rename to '" << path << "' failed");
 }
 
-bool jpeg_path(const std::string& path) {
+bool is_jpeg_path(const std::string& path) {
   std::string ext = path.substr(path.find_last_of('.') == std::string::npos ? path.size() : path.find_last_of('.'));
   for (auto& ch : ext) ch = (char)std::tolower((unsigned char)ch);
   return ext == ".jpg" || ext == ".jpeg" || ext == ".jfif";
 }
-}  // namespace
 
 Image read_image(const std::string& path) {
   const std::string bytes = slurp(path);
@@ -145,8 +146,8 @@ Image read_image(const std::string& path) {
 }
 
 void write_image(const std::string& path, const Image& img, int quality) {
-  if (jpeg_path(path)) write_atomic(path, encode_jpeg(img, quality));
-  else write_atomic(path, encode_pnm(img));
+  if (is_jpeg_path(path)) write_file_atomic(path, encode_jpeg(img, quality));
+  else write_file_atomic(path, encode_pnm(img));
 }
 
 void synth_rows(uint64_t seed, int W, int C, int row0, int rows, uint8_t* dst) {

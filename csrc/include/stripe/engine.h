@@ -191,6 +191,10 @@ class Engine {
   // scatter / gather copies; the stripe buffers then hold no output)
   bool dist_direct() const;
   void store_root(void* full, bool dst_device);           // rank 0: root output buffer, packed
+  // rank 0: the root output as a baseline JPEG; a device engine runs colour
+  // conversion, DCT and quantisation on the GPU (only the coefficients come
+  // back), the Huffman coding runs on the host
+  std::string store_root_jpeg(int quality);
   // The reference's timed window ends in rank 0's host memory (kernel.cu:190-226:
   // kernels, D2H, gray->BGR, MPI_Gather).  One step of it from the resident
   // stripe: the chain (halo exchange included), its output rows downloaded in
@@ -308,15 +312,22 @@ class Engine {
   int out_c_ = 0;
 };
 
+// Rank 0's output as a JPEG stream instead of an Image (run_rank / run_group
+// fill `bytes` and return an empty Image when one is passed).
+struct JpegOut {
+  int quality = 95;
+  std::string bytes;
+};
+
 // One rank's whole pipeline (one process or thread per rank): metadata
 // broadcast from rank 0, scatter, chain, gather; returns the image on rank 0.
 // `input` is read on rank 0 only; `device` is this rank's GPU (-1: keep).
 Image run_rank(const EngineConfig& cfg, Comm* comm, int device, const Image* input, int iterations,
-               PhaseTimes* times = nullptr);
+               PhaseTimes* times = nullptr, JpegOut* jpeg_out = nullptr);
 // Same, rank 0's input a baseline JPEG decoded as far as its coefficients
 // (jpeg_entropy_decode): the pixels are made where the root buffer lives.
 Image run_rank(const EngineConfig& cfg, Comm* comm, int device, const JpegCoefs* input, int iterations,
-               PhaseTimes* times = nullptr);
+               PhaseTimes* times = nullptr, JpegOut* jpeg_out = nullptr);
 // Small host buffer broadcast over a communicator (metadata, <= 256 bytes).
 void broadcast_small(Comm* comm, void* host, size_t bytes, int root, int device);
 
@@ -334,8 +345,8 @@ Image run_local_group(const EngineConfig& cfg, int world, const Image& input, in
 // Same driver over caller-provided communicators (one host thread per rank);
 // devices[r] is rank r's HIP device (empty: keep cfg.device).
 Image run_group(const EngineConfig& cfg, const std::vector<Comm*>& comms, const std::vector<int>& devices,
-                const Image& input, int iterations, PhaseTimes* times = nullptr);
+                const Image& input, int iterations, PhaseTimes* times = nullptr, JpegOut* jpeg_out = nullptr);
 Image run_group(const EngineConfig& cfg, const std::vector<Comm*>& comms, const std::vector<int>& devices,
-                const JpegCoefs& input, int iterations, PhaseTimes* times = nullptr);
+                const JpegCoefs& input, int iterations, PhaseTimes* times = nullptr, JpegOut* jpeg_out = nullptr);
 
 }  // namespace stripe

@@ -112,6 +112,10 @@ const int* jpeg_zigzag();
 // (temp file + rename).
 Image read_image(const std::string& path);
 void write_image(const std::string& path, const Image& img, int quality = 95);
+// bytes to a temp file, then rename over `path`
+void write_file_atomic(const std::string& path, const std::string& bytes);
+// .jpg / .jpeg / .jfif (any case)
+bool is_jpeg_path(const std::string& path);
 
 // ---- synthetic random-pixel frames ----
 // Counter-based: byte (y, b) of a W*C row is a pure function of (seed, y, b), so

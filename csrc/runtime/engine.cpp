@@ -1630,6 +1630,22 @@ void Engine::store_root(void* full, bool dst_device) {
   stage_end(Stage::Store, s_compute_);
 }
 
+std::string Engine::store_root_jpeg(int quality) {
+  if (rank_ != 0) return {};
+  const int C = out_c_ > 0 ? out_c_ : plan_.cout;
+  if (!device()) {
+    Image img(cfg_.W, cfg_.H, C);
+    store_root(img.data.data(), false);
+    return encode_jpeg(img, quality);
+  }
+  TraceRange tr("stripe.store_jpeg");
+  stage_begin(Stage::Store, s_compute_);
+  JpegQuant jq = jpeg_quantise_device(root_origin(root_out_, C), pitch(C), cfg_.W, cfg_.H, C, quality, true,
+                                      s_compute_);
+  stage_end(Stage::Store, s_compute_);
+  return jpeg_entropy_encode(jq, -1);
+}
+
 void Engine::synchronize() {
   if (!device()) return;
   TraceRange tr("stripe.synchronize");
@@ -1744,7 +1760,7 @@ double probe_link_rate(Comm* comm, int device, size_t bytes, int reps) {
 
 namespace {
 Image run_rank_impl(const EngineConfig& cfg_in, Comm* comm, int device, const Image* input, const JpegCoefs* jpeg,
-                    int iterations, PhaseTimes* times) {
+                    int iterations, PhaseTimes* times, JpegOut* jpeg_out) {
   const int rank = comm ? comm->rank() : 0;
   EngineConfig c = cfg_in;
   // the root knows the geometry (it read the image); everyone else learns it
@@ -1775,7 +1791,9 @@ Image run_rank_impl(const EngineConfig& cfg_in, Comm* comm, int device, const Im
     e.gather();
   }
   Image out;
-  if (rank == 0) {
+  if (rank == 0 && jpeg_out) {
+    jpeg_out->bytes = e.store_root_jpeg(jpeg_out->quality);
+  } else if (rank == 0) {
     out = Image(c.W, c.H, e.out_channels());
     e.store_root(out.data.data(), false);
   }
@@ -1787,19 +1805,19 @@ Image run_rank_impl(const EngineConfig& cfg_in, Comm* comm, int device, const Im
 }  // namespace
 
 Image run_rank(const EngineConfig& cfg, Comm* comm, int device, const Image* input, int iterations,
-               PhaseTimes* times) {
-  return run_rank_impl(cfg, comm, device, input, nullptr, iterations, times);
+               PhaseTimes* times, JpegOut* jpeg_out) {
+  return run_rank_impl(cfg, comm, device, input, nullptr, iterations, times, jpeg_out);
 }
 
 Image run_rank(const EngineConfig& cfg, Comm* comm, int device, const JpegCoefs* input, int iterations,
-               PhaseTimes* times) {
-  return run_rank_impl(cfg, comm, device, nullptr, input, iterations, times);
+               PhaseTimes* times, JpegOut* jpeg_out) {
+  return run_rank_impl(cfg, comm, device, nullptr, input, iterations, times, jpeg_out);
 }
 
 namespace {
 template <class In>
 Image run_group_impl(const EngineConfig& cfg, const std::vector<Comm*>& comms, const std::vector<int>& devices,
-                     const In& input, int iterations, PhaseTimes* times) {
+                     const In& input, int iterations, PhaseTimes* times, JpegOut* jpeg_out) {
   const int world = (int)comms.size();
   Image out;
   std::mutex mu;
@@ -1808,7 +1826,7 @@ Image run_group_impl(const EngineConfig& cfg, const std::vector<Comm*>& comms, c
     try {
       PhaseTimes t;
       Image o = run_rank(cfg, comms[r], devices.empty() ? cfg.device : devices[r], r == 0 ? &input : nullptr,
-                         iterations, &t);
+                         iterations, &t, r == 0 ? jpeg_out : nullptr);
       if (r == 0) {
         std::lock_guard<std::mutex> lk(mu);
         out = std::move(o);
@@ -1836,16 +1854,16 @@ Image run_group_impl(const EngineConfig& cfg, const std::vector<Comm*>& comms, c
 }  // namespace
 
 Image run_group(const EngineConfig& cfg, const std::vector<Comm*>& comms, const std::vector<int>& devices,
-                const Image& input, int iterations, PhaseTimes* times) {
+                const Image& input, int iterations, PhaseTimes* times, JpegOut* jpeg_out) {
   STRIPE_CHECK(input.W == cfg.W && input.H == cfg.H && input.C == cfg.C, "input does not match the config");
-  return run_group_impl(cfg, comms, devices, input, iterations, times);
+  return run_group_impl(cfg, comms, devices, input, iterations, times, jpeg_out);
 }
 
 Image run_group(const EngineConfig& cfg, const std::vector<Comm*>& comms, const std::vector<int>& devices,
-                const JpegCoefs& input, int iterations, PhaseTimes* times) {
+                const JpegCoefs& input, int iterations, PhaseTimes* times, JpegOut* jpeg_out) {
   STRIPE_CHECK(input.W == cfg.W && input.H == cfg.H && (int)input.comps.size() == cfg.C,
                "input does not match the config");
-  return run_group_impl(cfg, comms, devices, input, iterations, times);
+  return run_group_impl(cfg, comms, devices, input, iterations, times, jpeg_out);
 }
 
 Image run_local_group(const EngineConfig& cfg, int world, const Image& input, int iterations, PhaseTimes* times) {

@@ -260,3 +260,25 @@ def test_device_encode_matches_host(C, tmp_path, c):
     assert d.mean() < 0.05 and _psnr(ours, ref) > 45
     assert np.abs(_pil_decode(enc, c == 1).astype(int) - ours.astype(int)).max() <= 3
     assert _psnr(ours, img) > 30
+
+
+@pytest.mark.gpu
+def test_cli_jpeg_to_jpeg_on_gpu(C, tmp_path):
+    # JPEG in and out of a device run: the input's pixels are made on the GPU
+    # into the root buffer, the output is encoded from the root buffer on the
+    # GPU (colour + DCT + quantisation) and Huffman-coded on the host
+    import mpi_cuda_imagemanipulation_amd as m
+
+    img = _smooth(301, 203, 3, seed=8)
+    src = tmp_path / "in.jpg"
+    src.write_bytes(_pil_encode(img, quality=92))
+    out = tmp_path / "out.jpg"
+    cli = os.path.join(ROOT, "bin", "stripe")
+    r = subprocess.run([cli, "run", "--input", str(src), "--output", str(out), "--chain", "gaussian5", "--ranks", "2",
+                        "--backend", "local", "--quality", "97"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-3000:]
+    dec = m.utils.read_image_device(str(src)).cpu().numpy()
+    ref = C.golden_apply(dec, "gaussian5", "reflect101", True)
+    got = C.read_image(str(out))
+    assert got.shape == ref.shape and _psnr(got, ref) > 40
+    assert np.abs(_pil_decode(out.read_bytes(), False).astype(int) - got.astype(int)).max() <= 3
