@@ -36,3 +36,33 @@ def test_reference_flow_example(C, tmp_path):
 def test_frame_stream_example():
     out = _run("examples/frame_stream.py", "--backend", "gloo", "--shape", "96x64x3", "--frames", "4")
     assert "frames/s" in out and "schedule serial" in out
+
+
+def _run_gpu(*args):
+    r = subprocess.run([sys.executable, *args], capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stdout + r.stderr[-3000:]
+    return r.stdout
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.gpu
+def test_reference_flow_example_gpu(C, tmp_path):
+    import mpi_cuda_imagemanipulation_amd as m
+
+    y, x = np.mgrid[0:200, 0:260]
+    img = np.stack([128 + 100 * np.sin(x / 17 + k) * np.cos(y / 23 - k) for k in range(3)], -1).astype(np.uint8)
+    src = tmp_path / "in.jpg"
+    m.utils.write_image(str(src), img, 92)
+    out = tmp_path / "out.ppm"
+    assert "on GPU" in _run_gpu("examples/reference_flow.py", str(src), str(out))
+    dec = m.utils.read_image_device(str(src)).cpu().numpy()
+    ref = C.golden_apply(dec, "gray:ref,contrast:3.5,emboss3@skip,expand", "reflect101", True)
+    assert np.array_equal(m.utils.read_image(str(out)), ref)
+
+
+@pytest.mark.gpu
+def test_frame_stream_example_gpu():
+    out = _run_gpu("examples/frame_stream.py", "--backend", "rccl", "--shape", "2048x1024x3", "--frames", "16")
+    assert "frames/s" in out and "1 rank(s) (rccl)" in out
