@@ -80,3 +80,24 @@ def test_asan_jpeg_round_trip_and_mutations(asan_cli, tmp_path):
                  "--backend", "host")
         assert "AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-3000:]
         assert r.returncode in (0, 1), (r.returncode, r.stderr[-2000:])
+
+
+def test_asan_jpeg_decoder_fuzz(tmp_path):
+    # the decoder alone, host ASan + UBSan (g++), random and header-targeted
+    # mutations: every input decodes or raises, no sanitizer report
+    import shutil
+
+    if not shutil.which("g++"):
+        pytest.skip("g++ not available")
+    exe = tmp_path / "jpeg_fuzz"
+    src = [os.path.join(ROOT, "tests", "native", "jpeg_fuzz.cpp"), os.path.join(ROOT, "csrc", "core", "jpeg.cpp"),
+           os.path.join(ROOT, "csrc", "core", "image.cpp")]
+    b = subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
+                        "-I" + os.path.join(ROOT, "csrc", "include"), *src, "-o", str(exe), "-lpthread"],
+                       capture_output=True, text=True, timeout=300)
+    if b.returncode != 0 and "sanitizer" in b.stderr.lower():
+        pytest.skip("sanitizer runtimes unavailable: " + b.stderr[-300:])
+    assert b.returncode == 0, b.stderr[-3000:]
+    r = _run(str(exe), "1500")
+    assert r.returncode == 0 and "jpeg fuzz:" in r.stdout, (r.stdout + r.stderr)[-3000:]
+    assert "AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-3000:]
