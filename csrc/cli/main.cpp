@@ -19,6 +19,7 @@
 //                [--frames F] [--json out.json]     (F: stream of F frames, resident scope)
 //   stripe cmp   a.ppm b.ppm [--tol 0]
 //   stripe gen   --synthetic WxHxC --seed S --output x.ppm
+//   stripe convert --input a.jpg --output b.ppm [--quality 95]
 //   stripe info  [--chain ...] [--channels C] [--format json]
 #include <hip/hip_runtime.h>
 
@@ -340,6 +341,15 @@ int cmd_gen(const Args& a) {
   return 0;
 }
 
+// PPM/PGM <-> JPEG (input by content, output by extension)
+int cmd_convert(const Args& a) {
+  STRIPE_CHECK(a.has("input") && a.has("output"), "convert needs --input and --output");
+  const Image img = read_image(a.get("input"));
+  write_image(a.get("output"), img, a.geti("quality", 95));
+  std::printf("{\"cmd\":\"convert\",\"W\":%d,\"H\":%d,\"C\":%d}\n", img.W, img.H, img.C);
+  return 0;
+}
+
 int cmd_info(const Args& a) {
   const int n = device_count();
   if (a.get("format") == "json") {
@@ -545,7 +555,8 @@ void usage() {
                "        [--no-overlap] [--no-pipeline] [--graphs] [--band ROWS] [--halo-depth K] [--dist-chunks K]\n"
                "        [--frames F]  (resident: a stream of F independent frames, cache-cold tuning)\n"
                "  cmp   a.ppm b.ppm [--tol T]\n"
-               "  gen   --synthetic WxHxC [--seed S] --output out.ppm\n"
+               "  gen   --synthetic WxHxC [--seed S] --output out.ppm|out.jpg\n"
+               "  convert --input in.ppm|in.jpg --output out.ppm|out.jpg [--quality 95]\n"
                "  info  [--chain C] [--channels C] [--format json]\n");
 }
 
@@ -558,6 +569,7 @@ int main(int argc, char** argv) {
     if (a.cmd == "bench") return cmd_bench(a);
     if (a.cmd == "cmp") return cmd_cmp(a);
     if (a.cmd == "gen") return cmd_gen(a);
+    if (a.cmd == "convert") return cmd_convert(a);
     if (a.cmd == "info") return cmd_info(a);
     usage();
     return a.cmd.empty() || a.cmd == "help" || a.cmd == "--help" ? 0 : 2;

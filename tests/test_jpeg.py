@@ -282,3 +282,22 @@ def test_cli_jpeg_to_jpeg_on_gpu(C, tmp_path):
     got = C.read_image(str(out))
     assert got.shape == ref.shape and _psnr(got, ref) > 40
     assert np.abs(_pil_decode(out.read_bytes(), False).astype(int) - got.astype(int)).max() <= 3
+
+
+def test_cli_convert_and_cmp(C, tmp_path):
+    cli = os.path.join(ROOT, "bin", "stripe")
+    if not os.path.exists(cli):
+        pytest.skip("bin/stripe not built")
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+    img = _smooth(50, 70, 3)
+    src = tmp_path / "a.ppm"
+    C.write_pnm(str(src), img)
+    jpg, back = tmp_path / "b.jpg", tmp_path / "c.ppm"
+    for a, b in ((src, jpg), (jpg, back)):
+        r = subprocess.run([cli, "convert", "--input", str(a), "--output", str(b), "--quality", "93"],
+                           capture_output=True, text=True, env=env, timeout=60)
+        assert r.returncode == 0 and '"cmd":"convert"' in r.stdout, r.stderr
+    assert jpg.read_bytes()[:2] == b"\xff\xd8"
+    assert np.array_equal(C.read_image(str(back)), C.decode_jpeg(jpg.read_bytes()))
+    r = subprocess.run([cli, "cmp", str(back), str(jpg)], capture_output=True, text=True, env=env, timeout=60)
+    assert r.returncode == 0 and '"max_abs":0' in r.stdout
