@@ -6,18 +6,24 @@ row-partitioned over N MI355X (one process per GPU, RCCL over xGMI).
     (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
 
 One step = one full-frame gaussian5 pass over the distributed frame: every rank
-exchanges its 2 halo rows with its neighbours (ncclSend/ncclRecv on a side
-stream, every step: halo depth 1) while its interior rows are filtered, then
-filters its boundary rows.  Steps are iterated (ping-pong), so each step's halo
-rows are required work.
+exchanges its 2 halo rows with its neighbours (ncclSend/ncclRecv, every step:
+halo depth 1) and filters its stripe.  How the exchange meets the filter is
+measured, not assumed: at N > 1 the three halo schedules (exchange then filter;
+interior rows beside the exchange, boundary rows after it; core / rim / edge
+on three streams), each with frames on one stream or alternating over two, are
+timed on the real transport before the timed region and the fastest is kept
+(max over ranks; `halo_schedule` in the record).  Steps are iterated
+(ping-pong), so each step's halo rows are required work.
 
 Cache temperature of the headline.  A step's per-GPU working set is its stripe
 in + out: 1.61 GB on one GPU, 201 MB on each of 8.  When it fits the 256 MiB
 Infinity Cache (N=8), iterating one frame would read every step's input from
 the cache, not HBM; the headline then steps round-robin over F independent
-frames (F engines, each its own stripe pair, sharing one stream) with
-F x working set > 2 x 256 MiB, so every step reads data evicted long before --
-a stream of distinct frames, the way a video-rate workload sees the GPUs.  The
+frames (F engines, each its own stripe pair; consecutive frames may alternate
+over two streams) with F x working set > 2 x 256 MiB, so every step reads data
+evicted long before -- a stream of distinct frames, the way a video-rate
+workload sees the GPUs.  Stripes too big for the cache (N = 2, 4) get two
+frames, so one frame's exchange can run beside the other's filter.  The
 warm single-frame number (resident_warm) and the communication-avoiding deep
 halo (resident_deep: k*2 rows exchanged once per k steps, bit-identical) are
 reported beside it as named scopes, never as `value`.
@@ -25,7 +31,7 @@ reported beside it as named scopes, never as `value`.
 Order of work (the timed region holds nothing but the K steps):
   identity (what RCCL and the runtime report, gathered to rank 0) -> autotune
   (band height x occupancy cap x memory policy, on cold data when the frames
-  rotate; also ramps the clock) -> W warmup steps -> K timed steps (barrier +
+  rotate; also ramps the clock) -> halo-schedule probe (N > 1) -> W warmup steps -> K timed steps (barrier +
   device sync on both sides, max over ranks) -> per-step device events of
   max(K, 20) more steps -> golden verification -> copy roofline -> the other
   scopes, each skipped once the wall-time budget is spent.
