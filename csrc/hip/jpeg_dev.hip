@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <mutex>
 
 #include "stripe/image.h"
 #include "stripe/kernels.h"
@@ -172,9 +173,12 @@ __global__ __launch_bounds__(256) void k_jpeg_fdct(const float* __restrict__ pla
 namespace {
 
 void upload_jpeg_constants() {
+  // once per device (several host threads may decode / encode at once)
+  static std::mutex mu;
   static bool done[64] = {};
   int d = 0;
   HIP_CHECK(hipGetDevice(&d));
+  std::lock_guard<std::mutex> lk(mu);
   if (d < 64 && done[d]) return;
   float B[64];
   for (int x = 0; x < 8; ++x)
