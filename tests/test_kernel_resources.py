@@ -28,7 +28,7 @@ def report():
 def test_every_kernel_family_reported(report):
     names = " ".join(report)
     for fam in ["k_pointwise", "k_fill_margins", "k_synth", "k_copy_rows", "k_sep", "k_direct", "k_blur_pl",
-                "k_conv_mfma"]:
+                "k_conv_mfma", "k_conv_i8", "k_jpeg_idct", "k_jpeg_color", "k_jpeg_planes", "k_jpeg_fdct"]:
         assert fam in names, fam
 
 
