@@ -84,3 +84,52 @@ def test_cli_gloo_gpu_4_processes(tmp_path, C, extra):
             assert (got[r * rows:(r + 1) * rows] == np_ref.expand(e)).all(), r
     else:
         assert (got == C.golden_apply(img, "gaussian5", "reflect101", True)).all()
+
+
+SCHED_WORKER = r'''
+import json, os, sys
+sys.path.insert(0, os.environ["STRIPE_ROOT"])
+from mpi_cuda_imagemanipulation_amd import parallel, models
+from mpi_cuda_imagemanipulation_amd._native import C
+ctx = parallel.init("gloo-gpu")
+W, H, Cc, chain = 700, 256, 3, "gaussian5"
+fs = parallel.FrameStream(ctx, models.Pipeline(chain, halo_depth=1), W, H, Cc, frames=2, streams=2)
+row0, rows = fs.head.stripe
+fs.tune()
+refs = []
+for f in range(2):
+    ref = C.synth_image(5 + f, W, H, Cc)
+    for _ in range(3):
+        ref = C.golden_apply(ref, chain, "reflect101", True)
+    refs.append(ref[row0:row0 + rows])
+bad = []
+for sched in ("serial", "overlap", "pipeline"):
+    for ns in (1, 2):
+        fs.set_schedule(sched)
+        fs.set_streams(ns)
+        fs.load_synthetic(5)
+        for _ in range(6):
+            fs.step()
+        fs.synchronize()
+        for f in range(2):
+            if not (fs.frames[f].result_stripe() == refs[f]).all():
+                bad.append([sched, ns, f])
+print("RESULT", ctx.rank, json.dumps(bad), flush=True)
+'''
+
+
+def test_frame_stream_every_schedule_exact_gloo_gpu(tmp_path):
+    # pick_schedule may choose any schedule x stream count on the real
+    # transport, so every combination must be exact across ranks: 2 processes,
+    # 2 frames, 3 iterated steps each, vs the golden path
+    script = tmp_path / "w.py"
+    script.write_text(SCHED_WORKER)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(script)]
+    env = dict(os.environ, STRIPE_ROOT=ROOT, OMP_NUM_THREADS="2")
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+    assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
+    res = [l for l in r.stdout.splitlines() if l.startswith("RESULT")]
+    assert len(res) == 2, r.stdout[-2000:]
+    for l in res:
+        assert json.loads(l.split(" ", 2)[2]) == [], l
