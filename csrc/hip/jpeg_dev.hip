@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <mutex>
 
 #include "stripe/image.h"
@@ -193,8 +194,23 @@ unsigned blocks_for(int64_t n, int per) { return (unsigned)((n + per - 1) / per)
 
 }  // namespace
 
+namespace {
+// STRIPE_JPEG_PIN=0 keeps the pageable coefficient upload (A/B switch)
+bool pin_uploads() {
+  static const bool on = [] {
+    const char* e = std::getenv("STRIPE_JPEG_PIN");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
+}  // namespace
+
 void jpeg_pixels_device(const JpegCoefs& jc, uint8_t* dst, int64_t pitch, hipStream_t s) {
   const int nc = (int)jc.comps.size();
+  // large coefficient planes are page-locked for the upload (a pageable copy
+  // is staged through the runtime's bounce buffers at a fraction of the link
+  // rate); they are unregistered once the copies have run
+  std::vector<void*> pinned;
   STRIPE_CHECK(nc == 1 || nc == 3, "JPEG: 1 or 3 components");
   STRIPE_CHECK(pitch >= (int64_t)jc.W * nc, "JPEG: destination pitch " << pitch << " < row bytes " << jc.W * nc);
   upload_jpeg_constants();
@@ -207,7 +223,13 @@ void jpeg_pixels_device(const JpegCoefs& jc, uint8_t* dst, int64_t pitch, hipStr
     int16_t* dcoef = nullptr;
     HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&dcoef), (size_t)nb * 64 * sizeof(int16_t), s));
     HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&planes[(size_t)ci]), (size_t)ps * c.bh * 8, s));
-    HIP_CHECK(hipMemcpyAsync(dcoef, c.coef.data(), (size_t)nb * 64 * sizeof(int16_t), hipMemcpyHostToDevice, s));
+    const size_t cbytes = (size_t)nb * 64 * sizeof(int16_t);
+    if (pin_uploads() && cbytes >= ((size_t)8 << 20)) {
+      void* hp = const_cast<int16_t*>(c.coef.data());
+      if (hipHostRegister(hp, cbytes, hipHostRegisterDefault) == hipSuccess) pinned.push_back(hp);
+      else (void)hipGetLastError();  // not registrable: the pageable copy below still works
+    }
+    HIP_CHECK(hipMemcpyAsync(dcoef, c.coef.data(), cbytes, hipMemcpyHostToDevice, s));
     dev::k_jpeg_idct<<<blocks_for(nb, 4), 256, 0, s>>>(dcoef, nb, c.bw, planes[(size_t)ci], ps);
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipFreeAsync(dcoef, s));
@@ -219,6 +241,10 @@ void jpeg_pixels_device(const JpegCoefs& jc, uint8_t* dst, int64_t pitch, hipStr
                                                           jc.rgb, jc.W, jc.H, dst, pitch);
   HIP_CHECK(hipGetLastError());
   for (uint8_t* p : planes) HIP_CHECK(hipFreeAsync(p, s));
+  if (!pinned.empty()) {
+    HIP_CHECK(hipStreamSynchronize(s));  // the copies from the registered pages are done
+    for (void* hp : pinned) (void)hipHostUnregister(hp);
+  }
 }
 
 JpegQuant jpeg_quantise_device(const uint8_t* src, int64_t pitch, int W, int H, int C, int quality, bool subsample,
