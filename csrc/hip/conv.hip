@@ -279,9 +279,12 @@ constexpr int kQPS = 96;  // i8 plane row bytes (>= kCWin)
 
 template <int C>
 // m-tiles (16 output rows) per wave: measured 16K conv:31, RGB 2 / 3: 2.059 /
-// 2.037 ms on one box, 2.145-2.165 / 2.186-2.191 on another (4 spills: the
-// 3-occupancy MT = 2 stays), gray 4 / 6 / 8: 0.771 / 0.683 / 0.717 ms
-constexpr int convq_mt() { return C == 3 ? 2 : 6; }
+// 2.037 ms on one box, 2.145-2.165 / 2.186-2.191 on another while MT = 3
+// spilled 4 registers (round 3); spill-free since, MT = 3 is 1-2 % ahead on
+// both precisions (round 4, profiles/r4/blur/conv_mt.txt: exact 2.122-2.163
+// vs 2.157-2.177 ms, lsb 1.575-1.590 vs 1.610-1.616); gray 4 / 6 / 8: 0.771 /
+// 0.683 / 0.717 ms
+constexpr int convq_mt() { return C == 3 ? 3 : 6; }
 
 template <int C, int MT>
 __host__ __device__ constexpr int convq_rows_staged(int nq) {
