@@ -179,9 +179,11 @@ class RcclComm final : public Comm {
       if (el > limit)
         abort("rank " + std::to_string(rank_) + ": collective did not complete within " + std::to_string(limit) +
               " s (STRIPE_COMM_TIMEOUT_S)");
-      // spin for the first millisecond (a step's tail: the caller times it),
-      // then back off
-      if (el > 1e-3) std::this_thread::sleep_for(std::chrono::microseconds(20));
+      // poll without sleeping for the first 50 ms (the tail of a timed run of
+      // steps: a sleep wakes ~50-70 us late under Linux timer slack, ~1 % of a
+      // 20-step 16K run), then back off
+      if (el > 0.05) std::this_thread::sleep_for(std::chrono::microseconds(20));
+      else std::this_thread::yield();
     }
   }
 
