@@ -4,6 +4,8 @@
 
 #include "stripe/trace.h"
 
+#include "engine_internal.h"
+
 #include <algorithm>
 #include <chrono>
 #include <cstdlib>
@@ -14,21 +16,6 @@
 
 namespace stripe {
 
-// STRIPE_SCHEDULE_EMU=split|pipe|split1 runs the multi-rank schedules on one
-// rank (without the exchange) to time their launch/stream overhead on one GPU.
-// Measured, gaussian5 on a 16384x2048 RGB stripe (the N=8 share): one launch
-// 43.0 us/step; interior+boundary on one stream 46.9; the overlap schedule
-// (cross-stream events around the exchange) 54.4; the pipelined schedule 51.5.
-// Cross-queue event waits cost ~7 us per step on this stack, so the pipelined
-// schedule (one cross-queue wait on the critical path) is the default.
-static int schedule_emu() {
-  static const int v = [] {
-    const char* e = std::getenv("STRIPE_SCHEDULE_EMU");
-    if (!e) return 0;
-    return std::strcmp(e, "split") == 0 ? 1 : std::strcmp(e, "pipe") == 0 ? 2 : std::strcmp(e, "split1") == 0 ? 3 : 0;
-  }();
-  return v;
-}
 
 
 // ---------------------------------------------------------------------------
@@ -241,9 +228,6 @@ const char* stage_name(Stage s) {
 }
 
 namespace {
-double host_ms() {
-  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
 double& phase_field(PhaseTimes& t, Stage s) {
   switch (s) {
     case Stage::Load: return t.load;
@@ -565,418 +549,6 @@ void Engine::run_pass(const Pass& p, const uint8_t* in, uint8_t* out) {
   }
 }
 
-// ---------------------------------------------------------------------------
-// Pipelined halo schedule (iterated single-pass chains over > 1 ranks).
-//
-// Per step k (input A, output B, radius R) the output rows split three ways:
-//   core  [2R, rows-2R)                main stream; reads A[R, rows-R): the
-//                                      previous step's core + rim rows only
-//   rim   [R, 2R) u [rows-2R, rows-R)  edge stream; reads A[0, 3R) (+ bottom)
-//   edge  [0, R) u [rows-R, rows)      edge stream after the halo exchange
-// so the exchange and the boundary rows run beside the next core instead of
-// between consecutive cores.  Cross-stream hazards (A/B ping-pong):
-//   core_k  waits rim_{k-1}   (RAW on A[R,2R); WAR: rim_{k-1} read B[2R,3R))
-//   rim_k   waits core_{k-1}  (RAW on A[2R,3R); WAR: core_{k-1} read B[R,2R))
-//   xchg_k  waits edge_{k-1}  (sends A[0,R), A[rows-R,rows))
-//   edge_k  waits xchg_k      (halo rows), edge stream order covers the rest
-// core/rim events alternate by step parity so core_k never waits rim_k.
-// ---------------------------------------------------------------------------
-bool Engine::pipelined_ok() const {
-  if (device() && schedule_emu() == 2 && plan_.passes.size() == 1 && plan_.cin == plan_.cout &&
-      stripe().rows > 4 * plan_.passes[0].R && plan_.passes[0].R > 0)
-    return true;
-  if (!device() || !cfg_.halo || !cfg_.overlap || part_.active <= 1) return false;
-  if (plan_.passes.size() != 1 || plan_.cin != plan_.cout) return false;
-  const int R = plan_.passes[0].R;
-  // large windows (MFMA blur) pay a whole 32-row group per thin rim range:
-  // the three-way split costs more than it hides (blur:31 stripe 0.124 vs 0.114 ms)
-  if (plan_.passes[0].kind == PassKind::Conv && schedule_emu() != 2) return false;
-  const int rows = stripe().rows;
-  return R > 0 && rows > 4 * R && comm_ != nullptr;
-}
-
-void Engine::set_halo_schedule(int s) {
-  STRIPE_CHECK(s >= 0 && s <= 2, "halo schedule must be 0 (serial), 1 (overlap) or 2 (pipeline), got " << s);
-  cfg_.overlap = s >= 1;
-  cfg_.pipeline = s == 2;
-}
-
-int Engine::halo_schedule() const {
-  // mirrors run(1)'s dispatch and run_pass's split for a single-pass chain
-  if (!device() || !cfg_.halo || part_.active <= 1) return 0;
-  if (cfg_.pipeline && cfg_.overlap && pipelined_ok()) return 2;
-  const int R = plan_.passes.empty() ? 0 : plan_.passes[0].R;
-  return cfg_.overlap && stripe().rows > 2 * R ? 1 : 0;
-}
-
-void Engine::run_pipelined(int iterations) {
-  const Pass& p = plan_.passes[0];
-  const int R = p.R, rows = stripe().rows;
-  if (!s_edge_) {
-    HIP_CHECK(hipStreamCreateWithFlags(&s_edge_, hipStreamNonBlocking));
-    for (auto& e : pev_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  }
-  hipEvent_t* ev_core = &pev_[0];
-  hipEvent_t* ev_rim = &pev_[2];
-  hipEvent_t& ev_bnd = pev_[4];
-  hipEvent_t& ev_x = pev_[5];
-  hipEvent_t& ev_start = pev_[6];
-  // everything queued before (input load, previous runs) precedes the first step
-  HIP_CHECK(hipEventRecord(ev_start, s_compute_));
-  HIP_CHECK(hipStreamWaitEvent(s_edge_, ev_start, 0));
-  HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_start, 0));
-  for (hipEvent_t e : {ev_core[1], ev_rim[1], ev_bnd}) HIP_CHECK(hipEventRecord(e, s_compute_));
-  const PassConsts& pc = prt_[0].pc;
-  for (int k = 0; k < iterations; ++k) {
-    time_halo_ = k == iterations - 1;
-    const int par = k & 1;
-    uint8_t* in = origin(buf_[cur_], p.cin);
-    uint8_t* out = origin(buf_[cur_ ^ 1], p.cout);
-    PassLaunch L = make_launch(p, in, out, 0);
-    // core (main stream)
-    HIP_CHECK(hipStreamWaitEvent(s_compute_, ev_rim[par ^ 1], 0));
-    L.nrange = 1;
-    L.ry[0] = 2 * R;
-    L.ry[1] = rows - 2 * R;
-    launch_pass(p, pc, L, s_compute_);
-    HIP_CHECK(hipEventRecord(ev_core[par], s_compute_));
-    // halo exchange (comm stream) once the previous boundary rows exist
-    HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_bnd, 0));
-    exchange_halo(in, p.cin, R, s_comm_);
-    HIP_CHECK(hipEventRecord(ev_x, s_comm_));
-    // rim (edge stream)
-    HIP_CHECK(hipStreamWaitEvent(s_edge_, ev_core[par ^ 1], 0));
-    L.nrange = 2;
-    L.ry[0] = R;
-    L.ry[1] = 2 * R;
-    L.ry[2] = rows - 2 * R;
-    L.ry[3] = rows - R;
-    launch_pass(p, pc, L, s_edge_);
-    HIP_CHECK(hipEventRecord(ev_rim[par], s_edge_));
-    // boundary rows (edge stream) after the halo arrived
-    HIP_CHECK(hipStreamWaitEvent(s_edge_, ev_x, 0));
-    L.ry[0] = 0;
-    L.ry[1] = R;
-    L.ry[2] = rows - R;
-    L.ry[3] = rows;
-    launch_pass(p, pc, L, s_edge_);
-    HIP_CHECK(hipEventRecord(ev_bnd, s_edge_));
-    cur_ ^= 1;
-    cur_c_ = plan_.cout;
-  }
-  // later work on the compute stream sees every region of the last step
-  HIP_CHECK(hipStreamWaitEvent(s_compute_, ev_bnd, 0));
-  time_halo_ = true;
-}
-
-// ---------------------------------------------------------------------------
-// Chain-level ("deep") halo for multi-rank runs.  The chain's stencil radii
-// sum to S; a block of m <= k iterations starts with ONE exchange of m*S rows
-// of the chain input per side, and every pass then computes the rank's own
-// rows plus the shrinking band of neighbour rows the rest of the block still
-// needs ((m-1-i)*S + the radii of the passes after it), recomputed
-// redundantly and bit-identically to the neighbour (same kernels, same global
-// row grid).  Compared with one exchange per pass and iteration, the wire
-// carries the same rows on average, but the exchange latency, the cross-stream
-// waits and the interior/boundary launch split are paid once per block; the
-// price is (m-1)*S/2 + O(S) extra rows per interior side and pass (< 1 % of a
-// 2048-row stripe at the default depth).  Multi-pass chains (e.g.
-// gaussian5,sobel) exchange once per chain instead of once per pass even at
-// m = 1.  Stencil and pointwise kernels address rows by global index, so an
-// output range reaching into the halo rows is ordinary; the MFMA blur/conv
-// passes (32-row group grid) keep the per-pass exchange.
-// ---------------------------------------------------------------------------
-int Engine::chain_reach() const {
-  int s = 0;
-  for (const Pass& p : plan_.passes) {
-    if (p.kind != PassKind::Pointwise && p.kind != PassKind::Separable && p.kind != PassKind::Direct) return 0;
-    s += p.R;
-  }
-  return s;
-}
-
-int Engine::choose_depth() const {
-  if (!cfg_.halo || part_.active <= 1) return 0;
-  if (const char* e = std::getenv("STRIPE_DEEP"); e && std::atoi(e) == 0) return 0;  // A/B: per-pass exchange
-  const int S = chain_reach();
-  if (S <= 0) return 0;
-  int minrows = std::numeric_limits<int>::max();
-  for (int r = 0; r < part_.active; ++r) minrows = std::min(minrows, part_.of(r).rows);
-  int k = cfg_.halo_depth;
-  if (k <= 0) {
-    if (const char* e = std::getenv("STRIPE_HALO_DEPTH")) k = std::atoi(e);
-  }
-  if (plan_.cin != plan_.cout) k = 1;                          // not iterable: one chain per run
-  if (k <= 0) k = std::min(8, 1 + (minrows / 100) / S);       // redundant rows <= ~1 % of the stripe
-  // every neighbour must own the k*S rows it sends (and keep its own interior)
-  k = std::min(k, minrows / (2 * S));
-  return k >= 1 ? k : 0;
-}
-
-void Engine::run_deep(int iterations) {
-  const int S = chain_reach(), rows = stripe().rows;
-  if (rows == 0) return;
-  const bool up = rank_ > 0, down = rank_ + 1 < part_.active;
-  const Pass& p0 = plan_.passes[0];
-  const int R0 = p0.R;
-  // the block's exchange flies on the comm stream beside the first pass's
-  // interior rows [R0, rows - R0), which read only the rank's own rows; its
-  // boundary rows follow once the halo has landed (two cross-stream waits per
-  // block instead of per pass and step)
-  static const bool env_overlap = [] {
-    const char* e = std::getenv("STRIPE_DEEP_OVERLAP");
-    return !e || std::atoi(e) != 0;
-  }();
-  const bool overlap = device() && cfg_.overlap && env_overlap && rows > 2 * R0;
-  const int iy0 = up ? R0 : 0, iy1 = down ? rows - R0 : rows;  // rows needing no halo
-  for (int done = 0; done < iterations;) {
-    const int m = std::min(depth_, iterations - done);
-    time_halo_ = done + m >= iterations;  // stage events of the last exchange only
-    if (overlap) {
-      HIP_CHECK(hipEventRecord(ev_[4], s_compute_));
-      HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_[4], 0));
-      exchange_halo(origin(buf_[cur_], p0.cin), p0.cin, m * S, s_comm_);
-      HIP_CHECK(hipEventRecord(ev_[5], s_comm_));
-    } else {
-      exchange_halo(origin(buf_[cur_], p0.cin), p0.cin, m * S, s_compute_);
-    }
-    for (int i = 0; i < m; ++i) {
-      int reach = (m - i) * S;  // halo rows valid in the current input
-      for (size_t k = 0; k < plan_.passes.size(); ++k) {
-        const Pass& p = plan_.passes[k];
-        reach -= p.R;  // halo rows this pass's output must cover
-        const int y0 = up ? -reach : 0, y1 = rows + (down ? reach : 0);
-        uint8_t* in = origin(buf_[cur_], p.cin);
-        uint8_t* out = origin(buf_[cur_ ^ 1], p.cout);
-        if (device()) {
-          PassLaunch L = make_launch(p, in, out, (int)k);
-          L.ext = reach;
-          if (overlap && i == 0 && k == 0) {
-            L.nrange = 1;
-            L.ry[0] = iy0;
-            L.ry[1] = iy1;
-            launch_pass(p, prt_[k].pc, L, s_compute_);
-            HIP_CHECK(hipStreamWaitEvent(s_compute_, ev_[5], 0));
-            L.nrange = 2;
-            L.ry[0] = y0;
-            L.ry[1] = iy0;
-            L.ry[2] = iy1;
-            L.ry[3] = y1;
-          } else {
-            L.nrange = 1;
-            L.ry[0] = y0;
-            L.ry[1] = y1;
-          }
-          launch_pass(p, prt_[k].pc, L, s_compute_);
-        } else {
-          cpu_pass(p, ConstView{in, pitch(p.cin)}, MutView{out, pitch(p.cout)}, cfg_.W, geom(), y0, y1,
-                   host_threads());
-        }
-        cur_ ^= 1;
-      }
-    }
-    done += m;
-  }
-  cur_c_ = plan_.cout;
-  time_halo_ = true;
-}
-
-std::vector<int> Engine::bands() const {
-  std::vector<int> b;
-  for (const auto& p : prt_) b.push_back(p.band);
-  return b;
-}
-
-std::vector<int> Engine::caps() const {
-  std::vector<int> b;
-  for (const auto& p : prt_) b.push_back(p.wgs);
-  return b;
-}
-
-std::vector<int> Engine::policies() const {
-  std::vector<int> b;
-  for (const auto& p : prt_) b.push_back(p.nt);
-  return b;
-}
-
-void Engine::set_tuning(const std::vector<int>& bands, const std::vector<int>& caps,
-                        const std::vector<int>& policies) {
-  STRIPE_CHECK(bands.size() == prt_.size() && caps.size() == prt_.size() &&
-                   (policies.empty() || policies.size() == prt_.size()),
-               "tuning needs one entry per pass");
-  for (size_t i = 0; i < prt_.size(); ++i) {
-    prt_[i].band = bands[i];
-    prt_[i].wgs = caps[i];
-    if (!policies.empty()) prt_[i].nt = policies[i];
-  }
-  tuned_ = true;
-}
-
-// Time each candidate band height, then each occupancy cap at the best band,
-// on this rank's stripe (kernels only, no halo exchange; outputs land in the
-// scratch ping-pong buffer) and keep the fastest.  The cap is tuned per box:
-// the HBM-streaming cap that made a warm 16K RGB gaussian5 pass 9 % faster
-// (0.311 -> 0.282 ms) reads no better than no cap on a cold clock
-// (profiles/r3/headline_diag.txt), so it is measured here rather than fixed.
-void Engine::autotune_bands() {
-  tuned_ = true;
-  if (!device() || cfg_.band > 0 || stripe().rows == 0) return;
-  // 4-row bands pay off on small per-rank stripes, where a launch has too few
-  // waves to hide each wave's row-step latency (8192x2048 gray sobel, one
-  // rank's share of config 3 at N=4: 0.0125 ms at 4 rows vs 0.0150 at 12)
-  const int cand[] = {4, 8, 12, 16, 24, 32};
-  // -1: the family default (separable 2 / direct 3 workgroups per CU on
-  // HBM-streaming passes, none on cache-resident ones), 0: no cap
-  const int caps[] = {-1, 0, 2, 3, 4};
-  const bool fixed_cap = std::getenv("STRIPE_NT_WGS") != nullptr;  // A/B runs pin the cap
-  hipEvent_t e0 = ev_[6], e1 = ev_[7];
-  // Cold tuning (EngineConfig::cold): a stripe whose steps all read from HBM
-  // must not be tuned on data the previous candidate left in the 256 MiB
-  // Infinity Cache (round 3 reused the warm tuning for the cold scope,
-  // VERDICT r3 weak #2).  Every timed launch then reads and writes the next of
-  // `nrot` scratch stripe pairs, together more than twice the cache.
-  constexpr int64_t kMall = 256ll << 20;
-  const int64_t pair_bytes = (int64_t)buf_[0].bytes() + (int64_t)buf_[1].bytes();
-  std::vector<Buffer> scratch;
-  int nrot = 0;
-  if (cfg_.cold && pair_bytes <= 2 * kMall) {
-    nrot = (int)std::min<int64_t>(8, (2 * kMall + pair_bytes - 1) / pair_bytes + 1);
-    for (int k = 0; k < 2 * nrot; ++k) {
-      scratch.emplace_back(buf_[k & 1].bytes(), true);
-      HIP_CHECK(hipMemsetAsync(scratch.back().data(), 0, scratch.back().bytes(), s_compute_));
-    }
-  }
-  int rot = 0;
-  // a stream of cold frames alternates two streams (bench.py's headline), so
-  // one frame's kernel boundary overlaps the next frame's launch: the cold
-  // candidates are timed the same way, alternating launches between the
-  // compute stream and a second one
-  hipStream_t s2 = nullptr;
-  hipEvent_t e_fork = nullptr, e_join = nullptr;
-  if (nrot > 0) {
-    HIP_CHECK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
-    HIP_CHECK(hipEventCreateWithFlags(&e_fork, hipEventDisableTiming));
-    HIP_CHECK(hipEventCreateWithFlags(&e_join, hipEventDisableTiming));
-  }
-  struct TuneCleanup {
-    hipStream_t& s;
-    hipEvent_t& a;
-    hipEvent_t& b;
-    ~TuneCleanup() {
-      if (s) (void)hipStreamSynchronize(s), (void)hipStreamDestroy(s);
-      if (a) (void)hipEventDestroy(a);
-      if (b) (void)hipEventDestroy(b);
-    }
-  } tune_cleanup{s2, e_fork, e_join};
-  for (size_t i = 0; i < plan_.passes.size(); ++i) {
-    const Pass& p = plan_.passes[i];
-    if (p.kind != PassKind::Separable && p.kind != PassKind::Direct) continue;
-    PassLaunch L = make_launch(p, origin(buf_[cur_], p.cin), origin(buf_[cur_ ^ 1], p.cout), (int)i);
-    L.ry[0] = 0;
-    L.ry[1] = L.rows;
-    auto launch_one = [&]() {
-      if (nrot == 0) {
-        launch_pass(p, prt_[i].pc, L, s_compute_);
-        return;
-      }
-      hipStream_t ls = (rot & 1) ? s2 : s_compute_;
-      // the same launch on the next scratch pair (same sizes and offsets)
-      const Buffer& bi = scratch[(size_t)(2 * (rot % nrot))];
-      const Buffer& bo = scratch[(size_t)(2 * (rot % nrot) + 1)];
-      ++rot;
-      PassLaunch R = L;
-      R.in = bi.data() + (L.in - L.in_base);
-      R.in_base = bi.data();
-      R.in_bytes = (int64_t)bi.bytes();
-      R.out = bo.data() + (L.out - L.out_base);
-      R.out_base = bo.data();
-      R.out_bytes = (int64_t)bo.bytes();
-      launch_pass(p, prt_[i].pc, R, ls);
-    };
-    // median over 5 timed bursts (after one warmup burst) of kBurst
-    // back-to-back launches: the steady state of an iterated run, where one
-    // launch's tail overlaps the next one's ramp (isolated launches favour
-    // taller bands by ~5 % on 20-90 us kernels); bursts of a 40-300 us kernel
-    // still jitter by a few percent, about the gap between bands
-    constexpr int kBurst = 4;
-    auto time_it = [&](int band, int wgs, int nt) {
-      L.band = band;
-      L.wgs = wgs;
-      L.nt = nt;
-      std::vector<float> t;
-      for (int rep = 0; rep < 6; ++rep) {
-        HIP_CHECK(hipEventRecord(e0, s_compute_));
-        if (s2) {
-          HIP_CHECK(hipEventRecord(e_fork, s_compute_));
-          HIP_CHECK(hipStreamWaitEvent(s2, e_fork, 0));
-        }
-        for (int k = 0; k < kBurst; ++k) launch_one();
-        if (s2) {
-          HIP_CHECK(hipEventRecord(e_join, s2));
-          HIP_CHECK(hipStreamWaitEvent(s_compute_, e_join, 0));
-        }
-        HIP_CHECK(hipEventRecord(e1, s_compute_));
-        HIP_CHECK(hipEventSynchronize(e1));
-        if (rep > 0) t.push_back(elapsed(e0, e1) / kBurst);
-      }
-      std::nth_element(t.begin(), t.begin() + t.size() / 2, t.end());
-      return t[t.size() / 2];
-    };
-    const int nt0 = L.nt;  // the untuned policy (cold: streaming; else the size rule)
-    // clock ramp: the first candidate must not be timed on an idle-clocked GPU
-    {
-      L.band = 0;
-      L.wgs = -1;
-      const auto t0 = std::chrono::steady_clock::now();
-      for (int k = 0; k < 200; ++k) {
-        for (int j = 0; j < 4; ++j) launch_one();
-        HIP_CHECK(hipStreamSynchronize(s_compute_));
-        if (s2) HIP_CHECK(hipStreamSynchronize(s2));
-        if (std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() > 30.0) break;
-      }
-    }
-    float best = 1e30f;
-    int best_band = 0, best_wgs = -1, best_nt = prt_[i].nt;
-    for (int b : cand) {
-      const float t = time_it(b, -1, nt0);
-      if (t < best) {
-        best = t;
-        best_band = b;
-      }
-    }
-    if (!fixed_cap) {
-      for (int c : caps) {
-        if (c < 0) continue;  // the default was timed in the band sweep
-        const float t = time_it(best_band, c, nt0);
-        if (t < best * 0.995f) {  // a cap must beat the default by more than the noise floor
-          best = t;
-          best_wgs = c;
-        }
-      }
-    }
-    if (cfg_.cold) {
-      // the cache-resident policy (default stores, XCD-aware order), with and
-      // without the chosen cap: kept only if it beats streaming beyond the noise
-      best_nt = 1;
-      for (int c : {best_wgs, 0}) {
-        const float t = time_it(best_band, c, 0);
-        if (t < best * 0.995f) {
-          best = t;
-          best_wgs = c;
-          best_nt = 0;
-        }
-      }
-    }
-    prt_[i].band = best_band;
-    prt_[i].wgs = best_wgs;
-    prt_[i].nt = best_nt;
-    STRIPE_LOG(Info, rank_, "autotune pass " << i << (cfg_.cold ? " (cold)" : "") << ": band " << best_band
-                                             << " rows, occupancy cap " << best_wgs << ", policy " << best_nt << " ("
-                                             << best * 1e3f << " us per launch)");
-  }
-  if (!scratch.empty()) HIP_CHECK(hipStreamSynchronize(s_compute_));  // before the scratch stripes are freed
-}
-
 // Graph replay is safe when run() issues no collective: one active rank, or a
 // chain without halo exchange.  (RCCL calls are kept out of captured graphs.)
 bool Engine::graph_ok() const {
@@ -1084,196 +656,6 @@ void Engine::rewind() {
   cur_c_ = plan_.cin;
 }
 
-void Engine::alloc_host_io() {
-  const Stripe& st = stripe();
-  host_in_ = PinnedBuffer(std::max<size_t>(1, (size_t)st.rows * cfg_.W * plan_.cin));
-  host_out_ = PinnedBuffer(std::max<size_t>(1, (size_t)st.rows * cfg_.W * plan_.cout));
-  if (device()) {
-    stage_in_ = Buffer(std::max<size_t>(16, (size_t)st.rows * cfg_.W * plan_.cin), true);
-    stage_out_ = Buffer(std::max<size_t>(16, (size_t)st.rows * cfg_.W * plan_.cout), true);
-  }
-}
-
-namespace {
-// e2e transfer mode (STRIPE_E2E_MODE):
-//   zerocopy - the repack kernels read / write the pinned host rows directly
-//              over PCIe (no copy engine; uploads and downloads are ordinary
-//              kernels on two streams, so both directions can be in flight);
-//   staged   - 1-D pinned <-> packed device staging copies on the copy engines
-//              plus an on-device repack into the padded stripe;
-//   2d       - one pitched 2-D host copy per chunk (default).
-// Measured on one MI355X box (16K RGB, gaussian5): all three move 805 MB each
-// way in ~14.5 ms per direction (~55 GB/s) and the two directions do not
-// overlap on that host, so e2e is host-link bound (~29 ms/frame) in every mode;
-// 2d is the simplest and marginally fastest.
-enum class E2EMode { ZeroCopy, Staged, TwoD };
-E2EMode e2e_mode() {
-  const char* e = std::getenv("STRIPE_E2E_MODE");
-  if (e && std::strcmp(e, "staged") == 0) return E2EMode::Staged;
-  if (e && std::strcmp(e, "zerocopy") == 0) return E2EMode::ZeroCopy;
-  return E2EMode::TwoD;
-}
-}  // namespace
-
-void Engine::run_e2e(int chunks) {
-  STRIPE_CHECK(device(), "run_e2e needs the device backend");
-  STRIPE_CHECK(host_in_.data() && host_out_.data(), "call alloc_host_io() first");
-  const Stripe& st = stripe();
-  const int rows = st.rows;
-  if (rows == 0) return;
-  TraceRange tr("stripe.e2e");
-  fault_point("e2e", rank_);
-  const E2EMode mode = e2e_mode();
-  if (!s_h2d_) {
-    HIP_CHECK(hipStreamCreateWithFlags(&s_h2d_, hipStreamNonBlocking));
-    HIP_CHECK(hipStreamCreateWithFlags(&s_d2h_, hipStreamNonBlocking));
-  }
-  chunks = std::max(1, std::min(chunks, rows));
-  while ((int)ev_h2d_.size() < chunks + 1) {
-    hipEvent_t e1, e2;
-    HIP_CHECK(hipEventCreateWithFlags(&e1, hipEventDisableTiming));
-    HIP_CHECK(hipEventCreateWithFlags(&e2, hipEventDisableTiming));
-    ev_h2d_.push_back(e1);
-    ev_cmp_.push_back(e2);
-  }
-  const int cin = plan_.cin, cout = plan_.cout;
-  const int64_t Ein = (int64_t)cfg_.W * cin, Eout = (int64_t)cfg_.W * cout;
-  std::vector<int> cut(chunks + 1);
-  for (int i = 0; i <= chunks; ++i) cut[i] = (int)((int64_t)rows * i / chunks);
-  // previous step's download must finish before this step's output buffer is reused
-  HIP_CHECK(hipEventRecord(ev_[2], s_d2h_));
-  HIP_CHECK(hipStreamWaitEvent(s_compute_, ev_[2], 0));
-  HIP_CHECK(hipEventRecord(ev_[3], s_compute_));
-  HIP_CHECK(hipStreamWaitEvent(s_h2d_, ev_[3], 0));  // ...and this step's input buffer is free
-  cur_ = 0;
-  cur_c_ = cin;
-  uint8_t* in_org = origin(buf_[0], cin);
-  uint8_t* hin_dev = nullptr;
-  uint8_t* hout_dev = nullptr;
-  if (mode == E2EMode::ZeroCopy) {
-    HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&hin_dev), host_in_.data(), 0));
-    HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&hout_dev), host_out_.data(), 0));
-  }
-  auto download = [&](const uint8_t* org, int r0, int r1) {
-    if (r1 <= r0) return;
-    const int n = r1 - r0;
-    if (mode == E2EMode::ZeroCopy) {
-      launch_copy_rows(hout_dev + (int64_t)r0 * Eout, Eout, org + (int64_t)r0 * pitch(cout), pitch(cout), Eout, n,
-                       s_d2h_);
-    } else if (mode == E2EMode::Staged) {
-      launch_copy_rows(stage_out_.data() + (int64_t)r0 * Eout, Eout, org + (int64_t)r0 * pitch(cout), pitch(cout),
-                       Eout, n, s_d2h_);
-      HIP_CHECK(hipMemcpyAsync(host_out_.data() + (int64_t)r0 * Eout, stage_out_.data() + (int64_t)r0 * Eout,
-                               (size_t)n * Eout, hipMemcpyDeviceToHost, s_d2h_));
-    } else {
-      copy2d(host_out_.data() + (int64_t)r0 * Eout, Eout, org + (int64_t)r0 * pitch(cout), pitch(cout), Eout, n,
-             s_d2h_, 0);
-    }
-  };
-  stage_begin(Stage::E2E, s_h2d_);
-  stage_begin(Stage::H2D, s_h2d_);
-  for (int i = 0; i < chunks; ++i) {
-    const int n = cut[i + 1] - cut[i];
-    if (mode == E2EMode::ZeroCopy) {
-      launch_copy_rows(in_org + (int64_t)cut[i] * pitch(cin), pitch(cin), hin_dev + (int64_t)cut[i] * Ein, Ein, Ein,
-                       n, s_h2d_);
-    } else if (mode == E2EMode::Staged) {
-      HIP_CHECK(hipMemcpyAsync(stage_in_.data() + (int64_t)cut[i] * Ein, host_in_.data() + (int64_t)cut[i] * Ein,
-                               (size_t)n * Ein, hipMemcpyHostToDevice, s_h2d_));
-      launch_copy_rows(in_org + (int64_t)cut[i] * pitch(cin), pitch(cin), stage_in_.data() + (int64_t)cut[i] * Ein,
-                       Ein, Ein, n, s_h2d_);
-    } else {
-      copy2d(in_org + (int64_t)cut[i] * pitch(cin), pitch(cin), host_in_.data() + (int64_t)cut[i] * Ein, Ein, Ein, n,
-             s_h2d_, 0);
-    }
-    fill_margins(in_org, cin, cut[i], cut[i + 1], plan_.in_margin_px, plan_.in_margin_border, s_h2d_);
-    HIP_CHECK(hipEventRecord(ev_h2d_[i], s_h2d_));
-  }
-  stage_end(Stage::H2D, s_h2d_);
-  const bool single = plan_.passes.size() == 1;
-  if (!single) {
-    // multi-pass chains: upload overlapped with nothing but the download of the
-    // previous step; the chain itself runs as usual
-    HIP_CHECK(hipStreamWaitEvent(s_compute_, ev_h2d_[chunks - 1], 0));
-    run(1);
-    HIP_CHECK(hipEventRecord(ev_cmp_[0], s_compute_));
-    HIP_CHECK(hipStreamWaitEvent(s_d2h_, ev_cmp_[0], 0));
-    stage_begin(Stage::D2H, s_d2h_);
-    download(origin(buf_[out_buf_], cout), 0, rows);
-    stage_end(Stage::D2H, s_d2h_);
-    stage_end(Stage::E2E, s_d2h_);
-    join_d2h();
-    return;
-  }
-  const Pass& p = plan_.passes[0];
-  const int R = p.R;
-  const bool xchg = cfg_.halo && R > 0 && part_.active > 1;
-  const bool up = xchg && rank_ > 0;
-  const bool down = xchg && rank_ + 1 < part_.active;
-  uint8_t* out_org = origin(buf_[1], cout);
-  PassLaunch L = make_launch(p, in_org, out_org, 0);
-  if (xchg) {  // halo rows come from the first and last chunks
-    HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_h2d_[0], 0));
-    HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_h2d_[chunks - 1], 0));
-    exchange_halo(in_org, cin, R, s_comm_);
-    HIP_CHECK(hipEventRecord(ev_[5], s_comm_));
-  }
-  const int lo_lim = up ? std::min(R, rows) : 0;
-  const int hi_lim = down ? std::max(lo_lim, rows - R) : rows;
-  int done = lo_lim;
-  std::vector<std::pair<int, int>> ranges(chunks, {0, 0});
-  for (int i = 0; i < chunks; ++i) {
-    HIP_CHECK(hipStreamWaitEvent(s_compute_, ev_h2d_[i], 0));
-    if (i == 0) stage_begin(Stage::Compute, s_compute_);
-    const int avail = i == chunks - 1 ? rows : std::max(0, cut[i + 1] - R);  // inputs loaded for y + R
-    const int hi = std::min(avail, hi_lim);
-    if (hi > done) {
-      L.nrange = 1;
-      L.ry[0] = done;
-      L.ry[1] = hi;
-      launch_pass(p, prt_[0].pc, L, s_compute_);
-      ranges[i] = {done, hi};
-      done = hi;
-    }
-    HIP_CHECK(hipEventRecord(ev_cmp_[i], s_compute_));
-    HIP_CHECK(hipStreamWaitEvent(s_d2h_, ev_cmp_[i], 0));
-    if (i == 0) stage_begin(Stage::D2H, s_d2h_);
-    download(out_org, ranges[i].first, ranges[i].second);
-  }
-  if (xchg) {  // boundary rows once the neighbours' halos are in
-    HIP_CHECK(hipStreamWaitEvent(s_compute_, ev_[5], 0));
-    L.nrange = 0;
-    if (up) {
-      L.ry[2 * L.nrange] = 0;
-      L.ry[2 * L.nrange + 1] = lo_lim;
-      ++L.nrange;
-    }
-    if (down) {
-      L.ry[2 * L.nrange] = hi_lim;
-      L.ry[2 * L.nrange + 1] = rows;
-      ++L.nrange;
-    }
-    if (L.nrange > 0) launch_pass(p, prt_[0].pc, L, s_compute_);
-    HIP_CHECK(hipEventRecord(ev_cmp_[chunks], s_compute_));
-    HIP_CHECK(hipStreamWaitEvent(s_d2h_, ev_cmp_[chunks], 0));
-    if (up) download(out_org, 0, lo_lim);
-    if (down) download(out_org, hi_lim, rows);
-  }
-  stage_end(Stage::Compute, s_compute_);
-  stage_end(Stage::D2H, s_d2h_);
-  stage_end(Stage::E2E, s_d2h_);
-  join_d2h();
-  out_buf_ = 1;
-  out_c_ = cout;
-}
-
-// Later work on the compute stream (and a stream switch) orders behind this
-// step's downloads: the compute stream's tail then covers every side stream.
-void Engine::join_d2h() {
-  HIP_CHECK(hipEventRecord(ev_[1], s_d2h_));
-  HIP_CHECK(hipStreamWaitEvent(s_compute_, ev_[1], 0));
-}
-
 void Engine::store_packed(void* dst, bool dst_device) {
   (void)dst_device;
   STRIPE_CHECK(out_buf_ >= 0, "store_packed before run");
@@ -1319,306 +701,6 @@ void Engine::gather() {
   stage_end(Stage::Gather, s_compute_);
 }
 
-// ---------------------------------------------------------------------------
-// Pipelined distributed step (the reference's timed window, kernel.cu:135-225:
-// Scatter, the chain, Gather, there strictly one after the other).
-//
-// The root holds the whole frame, so it ships every peer's stripe together
-// with its halo rows (no neighbour exchange) in n row chunks, and filters its
-// own share in place: one launch from the root input straight into the root
-// output (no copies), beside the transfers.  Peer r's chunk k is filtered
-// once chunk k + 1 (the R rows below it) has landed, and its output travels
-// back in the grouped call that ships chunk k + 2, so each peer's xGMI link
-// carries scatter and gather traffic in opposite directions at once and the
-// peers' compute hides under the transfers:
-//   root comm      T0 | T1 | T2+G0 | T3+G1 | ... | T(n-1)+G(n-3) | G(n-2)+G(n-1)
-//   root compute   its whole share (no dependency on the transfers)
-//   peer compute        C0 (after T1) | C1 (after T2) | ... | C(n-1) (after T(n-1))
-// With row_weights from plan_dist_split the root keeps the share that
-// balances its filter time against the per-link transfer time.  Every active
-// rank derives the same n from the partition, so the grouped calls match.
-// Only single-pass stencil / pointwise chains (the pass reads exactly rows
-// y - R .. y + R); anything else runs the three calls.
-// ---------------------------------------------------------------------------
-int Engine::dist_chunks(int chunks) const {
-  if (!comm_ || part_.active <= 1 || chunks < 2 || plan_.passes.size() != 1) return 0;
-  const Pass& p = plan_.passes[0];
-  if (p.kind != PassKind::Separable && p.kind != PassKind::Direct && p.kind != PassKind::Pointwise) return 0;
-  if (cfg_.halo && p.R > halo_) return 0;
-  int minrows = std::numeric_limits<int>::max();
-  for (int r = 1; r < part_.active; ++r) minrows = std::min(minrows, part_.of(r).rows);  // peers' chunks
-  const int n = std::min(chunks, minrows / std::max(1, p.R));  // every chunk holds >= R rows
-  return n >= 2 ? n : 0;
-}
-
-bool Engine::dist_direct() const {
-  if (!device() || part_.active != 1 || rank_ != 0 || plan_.passes.size() != 1) return false;
-  if (!root_in_.data() || !root_out_.data()) return false;
-  const Pass& p = plan_.passes[0];
-  return p.kind == PassKind::Separable || p.kind == PassKind::Direct || p.kind == PassKind::Pointwise;
-}
-
-void Engine::run_dist(int chunks) {
-  fault_point("dist", rank_);
-  if (dist_direct()) {
-    // one rank: its stripe is the root's frame, so the pass reads the root
-    // input and writes the root output directly (scatter and gather would be
-    // two whole-frame device copies); the stripe buffers keep no output
-    if (cfg_.autotune && !tuned_) autotune_bands();
-    const Pass& p = plan_.passes[0];
-    TraceRange tr("stripe.dist");
-    fault_point("scatter", rank_);
-    stage_begin(Stage::Compute, s_compute_);
-    PassLaunch L = make_launch(p, root_origin(root_in_, plan_.cin), root_origin(root_out_, plan_.cout), 0);
-    L.nrange = 1;
-    L.ry[0] = 0;
-    L.ry[1] = L.rows;
-    launch_pass(p, prt_[0].pc, L, s_compute_);
-    stage_end(Stage::Compute, s_compute_);
-    out_buf_ = -1;
-    out_c_ = plan_.cout;
-    return;
-  }
-  const int n = dist_chunks(chunks);
-  const Stripe& st = stripe();
-  if (n == 0 || st.rows == 0) {
-    if (n == 0) {
-      scatter();
-      run(1);
-      gather();
-    }
-    return;  // idle rank of a pipelined group: no traffic, no rows
-  }
-  if (cfg_.autotune && !tuned_) autotune_bands();  // before any chunk lands in the buffers it uses
-  const Pass& p = plan_.passes[0];
-  const int R = p.R, cin = plan_.cin, cout = plan_.cout;
-  const int64_t Pin = pitch(cin), Pout = pitch(cout);
-  const bool root = rank_ == 0;
-  STRIPE_CHECK(!root || (root_in_.data() && root_out_.data()), "root buffers not allocated (EngineConfig::root_buffers)");
-  TraceRange tr("stripe.dist");
-  fault_point("scatter", rank_);
-  // row range [lo, hi) of peer r's transfer k (halo rows ride on the first and last chunk)
-  auto cut = [&](int r, int k) { return (int)((int64_t)part_.of(r).rows * k / n); };
-  auto span = [&](int r, int k, int& lo, int& hi) {
-    const bool h = cfg_.halo && R > 0;
-    lo = cut(r, k) - (k == 0 && h && r > 0 ? R : 0);
-    hi = cut(r, k + 1) + (k == n - 1 && h && r + 1 < part_.active ? R : 0);
-  };
-  const uint8_t* rin = root ? root_origin(root_in_, cin) - kMarginBytes : nullptr;
-  uint8_t* rout = root ? root_origin(root_out_, cout) - kMarginBytes : nullptr;
-  uint8_t* in_org = origin(buf_[0], cin);
-  uint8_t* out_org = origin(buf_[1], cout);
-  const bool dev = device();
-  // one grouped call: scatter chunk k (k < n) and gather chunks j, j2 (>= 0)
-  auto transfer = [&](int k, int j, int j2) {
-    const bool sc = k >= 0 && k < n;
-    comm_->group_start();
-    if (root) {
-      for (int r = 1; r < part_.active; ++r) {
-        const Stripe& sr = part_.of(r);
-        int lo, hi;
-        if (sc) {
-          span(r, k, lo, hi);
-          comm_->send(rin + (int64_t)(sr.row0 + lo) * Pin, (size_t)((hi - lo) * Pin), r, s_comm_);
-        }
-        for (int g : {j, j2})
-          if (g >= 0)
-            comm_->recv(rout + (int64_t)(sr.row0 + cut(r, g)) * Pout, (size_t)((cut(r, g + 1) - cut(r, g)) * Pout), r,
-                        s_comm_);
-      }
-    } else {
-      int lo, hi;
-      if (sc) {
-        span(rank_, k, lo, hi);
-        comm_->recv(in_org - kMarginBytes + (int64_t)lo * Pin, (size_t)((hi - lo) * Pin), 0, s_comm_);
-      }
-      for (int g : {j, j2})
-        if (g >= 0)
-          comm_->send(out_org - kMarginBytes + (int64_t)cut(rank_, g) * Pout,
-                      (size_t)((cut(rank_, g + 1) - cut(rank_, g)) * Pout), 0, s_comm_);
-    }
-    comm_->group_end();
-  };
-  // the root's own share: root input -> root output in place (its local rows
-  // are the frame's rows 0 .. rows - 1, so the root buffers are its stripe)
-  auto compute_root = [&]() {
-    const uint8_t* ri = root_origin(root_in_, cin);
-    uint8_t* ro = root_origin(root_out_, cout);
-    if (dev) {
-      PassLaunch L = make_launch(p, ri, ro, 0);
-      L.nrange = 1;
-      L.ry[0] = 0;
-      L.ry[1] = st.rows;
-      launch_pass(p, prt_[0].pc, L, s_compute_);
-    } else {
-      cpu_pass(p, ConstView{ri, Pin}, MutView{ro, Pout}, cfg_.W, geom(), 0, st.rows, host_threads());
-    }
-  };
-  auto compute = [&](int k) {
-    const int y0 = cut(rank_, k), y1 = cut(rank_, k + 1);
-    if (dev) {
-      PassLaunch L = make_launch(p, in_org, out_org, 0);
-      L.nrange = 1;
-      L.ry[0] = y0;
-      L.ry[1] = y1;
-      launch_pass(p, prt_[0].pc, L, s_compute_);
-    } else {
-      cpu_pass(p, ConstView{in_org, Pin}, MutView{out_org, Pout}, cfg_.W, geom(), y0, y1, host_threads());
-    }
-  };
-  if (dev) {
-    while ((int)dist_ev_.size() < 2 * n + 1) {
-      hipEvent_t e;
-      HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      dist_ev_.push_back(e);
-    }
-    // earlier work on the compute stream (loads, the previous step's reads of
-    // both buffers) precedes the first transfer
-    HIP_CHECK(hipEventRecord(ev_[4], s_compute_));
-    HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_[4], 0));
-  }
-  hipEvent_t* evT = dev ? dist_ev_.data() : nullptr;      // [0, n): transfer k landed
-  hipEvent_t* evC = dev ? dist_ev_.data() + n : nullptr;  // [n, 2n): chunk k filtered; [2n]: join
-  stage_begin(Stage::Scatter, s_comm_);
-  transfer(0, -1, -1);
-  record(dev ? evT[0] : nullptr, s_comm_);
-  // The root's own share runs beside the transfers (nothing it reads or
-  // writes is in flight).  On the device its launch is asynchronous; the host
-  // backend filters synchronously, so there it runs on a worker thread --
-  // otherwise every chunk after the first would wait for the root's whole
-  // share (a root-heavy weighted split made the host step slower).
-  std::thread root_worker;
-  std::exception_ptr root_err;
-  struct JoinGuard {
-    std::thread& t;
-    ~JoinGuard() {
-      if (t.joinable()) t.join();
-    }
-  } join_guard{root_worker};
-  if (root) {
-    if (dev) {
-      stage_begin(Stage::Compute, s_compute_);
-      compute_root();
-      stage_end(Stage::Compute, s_compute_);
-    } else {
-      root_worker = std::thread([&] {
-        try {
-          stage_begin(Stage::Compute, nullptr);  // host clock, this thread
-          compute_root();
-          stage_end(Stage::Compute, nullptr);
-        } catch (...) {
-          root_err = std::current_exception();
-        }
-      });
-    }
-  }
-  for (int k = 0; k < n; ++k) {
-    if (k + 1 < n) {
-      // a peer's gather of chunk k - 1 waits for its filter (the root's
-      // received rows are written by the transfer itself)
-      if (dev && !root && k >= 1) HIP_CHECK(hipStreamWaitEvent(s_comm_, evC[k - 1], 0));
-      if (k == 1) stage_begin(Stage::Gather, s_comm_);
-      transfer(k + 1, k - 1, -1);
-      record(dev ? evT[k + 1] : nullptr, s_comm_);
-    }
-    if (k + 1 == n - 1) stage_end(Stage::Scatter, s_comm_);  // the last chunk is on its way
-    if (root) continue;
-    if (dev) HIP_CHECK(hipStreamWaitEvent(s_compute_, evT[std::min(k + 1, n - 1)], 0));
-    if (k == 0) stage_begin(Stage::Compute, s_compute_);
-    compute(k);
-    record(dev ? evC[k] : nullptr, s_compute_);
-  }
-  if (!root) {
-    stage_end(Stage::Compute, s_compute_);
-    if (dev) HIP_CHECK(hipStreamWaitEvent(s_comm_, evC[n - 1], 0));
-  }
-  if (n == 2) stage_begin(Stage::Gather, s_comm_);
-  transfer(-1, n - 2, n - 1);
-  stage_end(Stage::Gather, s_comm_);
-  if (dev) {  // later work on the compute stream orders behind the gather
-    HIP_CHECK(hipEventRecord(dist_ev_[2 * n], s_comm_));
-    HIP_CHECK(hipStreamWaitEvent(s_compute_, dist_ev_[2 * n], 0));
-  }
-  if (root_worker.joinable()) root_worker.join();
-  if (root_err) std::rethrow_exception(root_err);
-  if (root) {  // the root's output is in the root buffer only (as with dist_direct)
-    out_buf_ = -1;
-    out_c_ = cout;
-    return;
-  }
-  run_in_buf_ = 0;
-  cur_ = 1;
-  cur_c_ = cout;
-  out_buf_ = 1;
-  out_c_ = cout;
-}
-
-void Engine::run_to_host(void* dst, int chunks) {
-  STRIPE_CHECK(device(), "run_to_host needs the device backend");
-  STRIPE_CHECK(cur_c_ == plan_.cin, "engine input has " << cur_c_ << " channels, chain expects " << plan_.cin);
-  const Stripe& st = stripe();
-  const int rows = st.rows;
-  if (rows == 0) return;
-  if (cfg_.autotune && !tuned_) autotune_bands();
-  TraceRange tr("stripe.to_host");
-  if (!s_d2h_) HIP_CHECK(hipStreamCreateWithFlags(&s_d2h_, hipStreamNonBlocking));
-  chunks = std::max(1, std::min(chunks, rows));
-  while ((int)ev_cmp_.size() < chunks + 1) {
-    hipEvent_t e1, e2;
-    HIP_CHECK(hipEventCreateWithFlags(&e1, hipEventDisableTiming));
-    HIP_CHECK(hipEventCreateWithFlags(&e2, hipEventDisableTiming));
-    ev_h2d_.push_back(e1);
-    ev_cmp_.push_back(e2);
-  }
-  const int cout = plan_.cout;
-  const int64_t Eout = (int64_t)cfg_.W * cout;
-  uint8_t* host = static_cast<uint8_t*>(dst);
-  const int in_buf = cur_;
-  // the previous step's download must be done before its rows are rewritten
-  HIP_CHECK(hipEventRecord(ev_[2], s_d2h_));
-  HIP_CHECK(hipStreamWaitEvent(s_compute_, ev_[2], 0));
-  stage_begin(Stage::E2E, s_compute_);
-  const Pass& p0 = plan_.passes[0];
-  const bool single = plan_.passes.size() == 1;  // any kind: launch_pass takes row ranges
-  if (!single) {  // multi-pass chains: the chain, then the download
-    run(1);
-    const int ob = out_buf_;
-    HIP_CHECK(hipEventRecord(ev_cmp_[0], s_compute_));
-    HIP_CHECK(hipStreamWaitEvent(s_d2h_, ev_cmp_[0], 0));
-    stage_begin(Stage::D2H, s_d2h_);
-    copy2d(host, Eout, origin(buf_[ob], cout), pitch(cout), Eout, rows, s_d2h_, 0);
-  } else {
-    stage_begin(Stage::Compute, s_compute_);
-    const bool xchg = cfg_.halo && p0.R > 0 && part_.active > 1;
-    uint8_t* in = origin(buf_[in_buf], p0.cin);
-    uint8_t* out = origin(buf_[in_buf ^ 1], cout);
-    if (xchg) exchange_halo(in, p0.cin, p0.R, s_compute_);
-    PassLaunch L = make_launch(p0, in, out, 0);
-    for (int i = 0; i < chunks; ++i) {
-      const int y0 = (int)((int64_t)rows * i / chunks), y1 = (int)((int64_t)rows * (i + 1) / chunks);
-      L.nrange = 1;
-      L.ry[0] = y0;
-      L.ry[1] = y1;
-      launch_pass(p0, prt_[0].pc, L, s_compute_);
-      HIP_CHECK(hipEventRecord(ev_cmp_[i], s_compute_));
-      HIP_CHECK(hipStreamWaitEvent(s_d2h_, ev_cmp_[i], 0));
-      if (i == 0) stage_begin(Stage::D2H, s_d2h_);
-      copy2d(host + (int64_t)y0 * Eout, Eout, out + (int64_t)y0 * pitch(cout), pitch(cout), Eout, y1 - y0, s_d2h_, 0);
-    }
-    stage_end(Stage::Compute, s_compute_);
-    out_buf_ = in_buf ^ 1;
-    out_c_ = cout;
-  }
-  stage_end(Stage::D2H, s_d2h_);
-  stage_end(Stage::E2E, s_d2h_);
-  join_d2h();
-  if (single) {  // the input stays current: the next step filters the same frame
-    cur_ = in_buf;
-    cur_c_ = plan_.cin;
-    run_in_buf_ = in_buf;
-  }
-}
-
 void Engine::store_root(void* full, bool dst_device) {
   (void)dst_device;
   if (rank_ != 0) return;
@@ -1655,226 +737,6 @@ void Engine::synchronize() {
   wait_stream(s_h2d_);
   wait_stream(s_d2h_);
   collect_times();
-}
-
-// ---------------------------------------------------------------------------
-// In-process group driver
-// ---------------------------------------------------------------------------
-// Broadcast `bytes` (<= 256) from `root` to every rank through the group's
-// point-to-point channel (device staging for device communicators): the
-// analogue of the reference's MPI_Bcast of the image properties (kernel.cu:129).
-void broadcast_small(Comm* comm, void* host, size_t bytes, int root, int device) {
-  if (!comm || comm->size() <= 1) return;
-  STRIPE_CHECK(bytes <= 256, "broadcast_small is for metadata (<= 256 bytes)");
-  const bool dev = comm->device_buffers();
-  void* buf = host;
-  hipStream_t s = nullptr;
-  if (dev) {
-    if (device >= 0) HIP_CHECK(hipSetDevice(device));
-    HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    HIP_CHECK(hipMalloc(&buf, 256));
-    if (comm->rank() == root) HIP_CHECK(hipMemcpyAsync(buf, host, bytes, hipMemcpyHostToDevice, s));
-  }
-  comm->group_start();
-  if (comm->rank() == root) {
-    for (int r = 0; r < comm->size(); ++r)
-      if (r != root) comm->send(buf, bytes, r, s);
-  } else {
-    comm->recv(buf, bytes, root, s);
-  }
-  comm->group_end();
-  if (dev) {
-    if (comm->rank() != root) HIP_CHECK(hipMemcpyAsync(host, buf, bytes, hipMemcpyDeviceToHost, s));
-    comm->wait(s);
-    HIP_CHECK(hipFree(buf));
-    HIP_CHECK(hipStreamDestroy(s));
-  }
-}
-
-double probe_link_rate(Comm* comm, int device, size_t bytes, int reps) {
-  if (!comm || comm->size() <= 1) return 0.0;
-  STRIPE_CHECK(bytes >= 1 && reps >= 1, "probe needs bytes, reps >= 1");
-  const bool dev = comm->device_buffers();
-  const int rank = comm->rank(), world = comm->size();
-  const int peers = rank == 0 ? world - 1 : 1;
-  hipStream_t s = nullptr;
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  // the probe buffers live on the rank's device: select it before allocating
-  if (dev && device >= 0) HIP_CHECK(hipSetDevice(device));
-  Buffer sendb(bytes * (size_t)peers, dev), recvb(bytes * (size_t)peers, dev);
-  if (dev) {
-    HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    HIP_CHECK(hipEventCreate(&e0));
-    HIP_CHECK(hipEventCreate(&e1));
-  }
-  auto one = [&]() {
-    comm->group_start();
-    if (rank == 0) {
-      for (int r = 1; r < world; ++r) {
-        comm->send(sendb.data() + (size_t)(r - 1) * bytes, bytes, r, s);
-        comm->recv(recvb.data() + (size_t)(r - 1) * bytes, bytes, r, s);
-      }
-    } else {
-      comm->recv(recvb.data(), bytes, 0, s);
-      comm->send(sendb.data(), bytes, 0, s);
-    }
-    comm->group_end();
-  };
-  std::vector<double> t;
-  try {
-    one();  // connection setup and warmup
-    if (dev) comm->wait(s);
-    for (int i = 0; i < reps; ++i) {
-      if (dev) {
-        HIP_CHECK(hipEventRecord(e0, s));
-        one();
-        HIP_CHECK(hipEventRecord(e1, s));
-        comm->wait(s);
-        float ms = 0;
-        HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
-        t.push_back(ms);
-      } else {
-        const double t0 = host_ms();
-        one();
-        t.push_back(host_ms() - t0);
-      }
-    }
-  } catch (...) {
-    if (dev) {
-      (void)hipEventDestroy(e0);
-      (void)hipEventDestroy(e1);
-      (void)hipStreamDestroy(s);
-    }
-    throw;
-  }
-  if (dev) {
-    HIP_CHECK(hipEventDestroy(e0));
-    HIP_CHECK(hipEventDestroy(e1));
-    HIP_CHECK(hipStreamDestroy(s));
-  }
-  std::nth_element(t.begin(), t.begin() + t.size() / 2, t.end());
-  double rate = (double)bytes / std::max(1e-6, t[t.size() / 2]);
-  broadcast_small(comm, &rate, sizeof rate, 0, device);  // the root's view, on every rank
-  return rate;
-}
-
-namespace {
-Image run_rank_impl(const EngineConfig& cfg_in, Comm* comm, int device, const Image* input, const JpegCoefs* jpeg,
-                    int iterations, PhaseTimes* times, JpegOut* jpeg_out) {
-  const int rank = comm ? comm->rank() : 0;
-  EngineConfig c = cfg_in;
-  // the root knows the geometry (it read the image); everyone else learns it
-  // from the metadata broadcast
-  int meta[4] = {c.W, c.H, c.C, 0};
-  if (rank == 0) {
-    STRIPE_CHECK(input != nullptr || jpeg != nullptr, "rank 0 needs the input image");
-    meta[0] = input ? input->W : jpeg->W;
-    meta[1] = input ? input->H : jpeg->H;
-    meta[2] = input ? input->C : (int)jpeg->comps.size();
-  }
-  broadcast_small(comm, meta, sizeof meta, 0, device);
-  c.W = meta[0];
-  c.H = meta[1];
-  c.C = meta[2];
-  c.root_buffers = true;
-  if (device >= 0) c.device = device;
-  Engine e(c, comm);
-  if (rank == 0) {
-    if (input) e.load_root(input->data.data(), false);
-    else e.load_root_jpeg(*jpeg);
-  }
-  if (iterations == 1 && c.dist_chunks > 1 && (e.dist_chunks(c.dist_chunks) > 0 || e.dist_direct())) {
-    e.run_dist(c.dist_chunks);
-  } else {
-    e.scatter();
-    e.run(iterations);
-    e.gather();
-  }
-  Image out;
-  if (rank == 0 && jpeg_out) {
-    jpeg_out->bytes = e.store_root_jpeg(jpeg_out->quality);
-  } else if (rank == 0) {
-    out = Image(c.W, c.H, e.out_channels());
-    e.store_root(out.data.data(), false);
-  }
-  e.synchronize();
-  if (times) *times = e.times();
-  if (comm) comm->barrier();
-  return out;
-}
-}  // namespace
-
-Image run_rank(const EngineConfig& cfg, Comm* comm, int device, const Image* input, int iterations,
-               PhaseTimes* times, JpegOut* jpeg_out) {
-  return run_rank_impl(cfg, comm, device, input, nullptr, iterations, times, jpeg_out);
-}
-
-Image run_rank(const EngineConfig& cfg, Comm* comm, int device, const JpegCoefs* input, int iterations,
-               PhaseTimes* times, JpegOut* jpeg_out) {
-  return run_rank_impl(cfg, comm, device, nullptr, input, iterations, times, jpeg_out);
-}
-
-namespace {
-template <class In>
-Image run_group_impl(const EngineConfig& cfg, const std::vector<Comm*>& comms, const std::vector<int>& devices,
-                     const In& input, int iterations, PhaseTimes* times, JpegOut* jpeg_out) {
-  const int world = (int)comms.size();
-  Image out;
-  std::mutex mu;
-  std::exception_ptr err;
-  auto body = [&](int r) {
-    try {
-      PhaseTimes t;
-      Image o = run_rank(cfg, comms[r], devices.empty() ? cfg.device : devices[r], r == 0 ? &input : nullptr,
-                         iterations, &t, r == 0 ? jpeg_out : nullptr);
-      if (r == 0) {
-        std::lock_guard<std::mutex> lk(mu);
-        out = std::move(o);
-        if (times) *times = t;
-      }
-    } catch (const std::exception& ex) {
-      STRIPE_LOG(Error, r, "rank failed: " << ex.what() << " (aborting the group)");
-      std::lock_guard<std::mutex> lk(mu);
-      if (!err) err = std::current_exception();
-      for (Comm* c : comms) c->abort("rank " + std::to_string(r) + " failed");
-    } catch (...) {
-      std::lock_guard<std::mutex> lk(mu);
-      if (!err) err = std::current_exception();
-      // one process owns every rank: abort the whole group (Q9), so ranks
-      // blocked on this one fail at once instead of at the comm timeout
-      for (Comm* c : comms) c->abort("rank " + std::to_string(r) + " failed");
-    }
-  };
-  std::vector<std::thread> th;
-  for (int r = 0; r < world; ++r) th.emplace_back(body, r);
-  for (auto& t : th) t.join();
-  if (err) std::rethrow_exception(err);
-  return out;
-}
-}  // namespace
-
-Image run_group(const EngineConfig& cfg, const std::vector<Comm*>& comms, const std::vector<int>& devices,
-                const Image& input, int iterations, PhaseTimes* times, JpegOut* jpeg_out) {
-  STRIPE_CHECK(input.W == cfg.W && input.H == cfg.H && input.C == cfg.C, "input does not match the config");
-  return run_group_impl(cfg, comms, devices, input, iterations, times, jpeg_out);
-}
-
-Image run_group(const EngineConfig& cfg, const std::vector<Comm*>& comms, const std::vector<int>& devices,
-                const JpegCoefs& input, int iterations, PhaseTimes* times, JpegOut* jpeg_out) {
-  STRIPE_CHECK(input.W == cfg.W && input.H == cfg.H && (int)input.comps.size() == cfg.C,
-               "input does not match the config");
-  return run_group_impl(cfg, comms, devices, input, iterations, times, jpeg_out);
-}
-
-Image run_local_group(const EngineConfig& cfg, int world, const Image& input, int iterations, PhaseTimes* times) {
-  auto hub = make_local_hub(world, cfg.backend == BackendKind::Device);
-  std::vector<std::unique_ptr<Comm>> owned;
-  std::vector<Comm*> comms;
-  for (int r = 0; r < world; ++r) {
-    owned.push_back(make_local_comm(hub, r));
-    comms.push_back(owned.back().get());
-  }
-  return run_group(cfg, comms, {}, input, iterations, times);
 }
 
 }  // namespace stripe

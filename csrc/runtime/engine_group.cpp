@@ -1,0 +1,240 @@
+// In-process group driver: metadata broadcast, link probe, one rank's whole
+// pipeline and the in-process group runners (see engine.h).
+#include "stripe/engine.h"
+#include "stripe/cpu_exec.h"
+
+#include "stripe/trace.h"
+
+#include "engine_internal.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <exception>
+#include <mutex>
+#include <thread>
+
+namespace stripe {
+
+// ---------------------------------------------------------------------------
+// In-process group driver
+// ---------------------------------------------------------------------------
+// Broadcast `bytes` (<= 256) from `root` to every rank through the group's
+// point-to-point channel (device staging for device communicators): the
+// analogue of the reference's MPI_Bcast of the image properties (kernel.cu:129).
+void broadcast_small(Comm* comm, void* host, size_t bytes, int root, int device) {
+  if (!comm || comm->size() <= 1) return;
+  STRIPE_CHECK(bytes <= 256, "broadcast_small is for metadata (<= 256 bytes)");
+  const bool dev = comm->device_buffers();
+  void* buf = host;
+  hipStream_t s = nullptr;
+  if (dev) {
+    if (device >= 0) HIP_CHECK(hipSetDevice(device));
+    HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    HIP_CHECK(hipMalloc(&buf, 256));
+    if (comm->rank() == root) HIP_CHECK(hipMemcpyAsync(buf, host, bytes, hipMemcpyHostToDevice, s));
+  }
+  comm->group_start();
+  if (comm->rank() == root) {
+    for (int r = 0; r < comm->size(); ++r)
+      if (r != root) comm->send(buf, bytes, r, s);
+  } else {
+    comm->recv(buf, bytes, root, s);
+  }
+  comm->group_end();
+  if (dev) {
+    if (comm->rank() != root) HIP_CHECK(hipMemcpyAsync(host, buf, bytes, hipMemcpyDeviceToHost, s));
+    comm->wait(s);
+    HIP_CHECK(hipFree(buf));
+    HIP_CHECK(hipStreamDestroy(s));
+  }
+}
+
+double probe_link_rate(Comm* comm, int device, size_t bytes, int reps) {
+  if (!comm || comm->size() <= 1) return 0.0;
+  STRIPE_CHECK(bytes >= 1 && reps >= 1, "probe needs bytes, reps >= 1");
+  const bool dev = comm->device_buffers();
+  const int rank = comm->rank(), world = comm->size();
+  const int peers = rank == 0 ? world - 1 : 1;
+  hipStream_t s = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  // the probe buffers live on the rank's device: select it before allocating
+  if (dev && device >= 0) HIP_CHECK(hipSetDevice(device));
+  Buffer sendb(bytes * (size_t)peers, dev), recvb(bytes * (size_t)peers, dev);
+  if (dev) {
+    HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    HIP_CHECK(hipEventCreate(&e0));
+    HIP_CHECK(hipEventCreate(&e1));
+  }
+  auto one = [&]() {
+    comm->group_start();
+    if (rank == 0) {
+      for (int r = 1; r < world; ++r) {
+        comm->send(sendb.data() + (size_t)(r - 1) * bytes, bytes, r, s);
+        comm->recv(recvb.data() + (size_t)(r - 1) * bytes, bytes, r, s);
+      }
+    } else {
+      comm->recv(recvb.data(), bytes, 0, s);
+      comm->send(sendb.data(), bytes, 0, s);
+    }
+    comm->group_end();
+  };
+  std::vector<double> t;
+  try {
+    one();  // connection setup and warmup
+    if (dev) comm->wait(s);
+    for (int i = 0; i < reps; ++i) {
+      if (dev) {
+        HIP_CHECK(hipEventRecord(e0, s));
+        one();
+        HIP_CHECK(hipEventRecord(e1, s));
+        comm->wait(s);
+        float ms = 0;
+        HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        t.push_back(ms);
+      } else {
+        const double t0 = host_ms();
+        one();
+        t.push_back(host_ms() - t0);
+      }
+    }
+  } catch (...) {
+    if (dev) {
+      (void)hipEventDestroy(e0);
+      (void)hipEventDestroy(e1);
+      (void)hipStreamDestroy(s);
+    }
+    throw;
+  }
+  if (dev) {
+    HIP_CHECK(hipEventDestroy(e0));
+    HIP_CHECK(hipEventDestroy(e1));
+    HIP_CHECK(hipStreamDestroy(s));
+  }
+  std::nth_element(t.begin(), t.begin() + t.size() / 2, t.end());
+  double rate = (double)bytes / std::max(1e-6, t[t.size() / 2]);
+  broadcast_small(comm, &rate, sizeof rate, 0, device);  // the root's view, on every rank
+  return rate;
+}
+
+namespace {
+Image run_rank_impl(const EngineConfig& cfg_in, Comm* comm, int device, const Image* input, const JpegCoefs* jpeg,
+                    int iterations, PhaseTimes* times, JpegOut* jpeg_out) {
+  const int rank = comm ? comm->rank() : 0;
+  EngineConfig c = cfg_in;
+  // the root knows the geometry (it read the image); everyone else learns it
+  // from the metadata broadcast
+  int meta[4] = {c.W, c.H, c.C, 0};
+  if (rank == 0) {
+    STRIPE_CHECK(input != nullptr || jpeg != nullptr, "rank 0 needs the input image");
+    meta[0] = input ? input->W : jpeg->W;
+    meta[1] = input ? input->H : jpeg->H;
+    meta[2] = input ? input->C : (int)jpeg->comps.size();
+  }
+  broadcast_small(comm, meta, sizeof meta, 0, device);
+  c.W = meta[0];
+  c.H = meta[1];
+  c.C = meta[2];
+  c.root_buffers = true;
+  if (device >= 0) c.device = device;
+  Engine e(c, comm);
+  if (rank == 0) {
+    if (input) e.load_root(input->data.data(), false);
+    else e.load_root_jpeg(*jpeg);
+  }
+  if (iterations == 1 && c.dist_chunks > 1 && (e.dist_chunks(c.dist_chunks) > 0 || e.dist_direct())) {
+    e.run_dist(c.dist_chunks);
+  } else {
+    e.scatter();
+    e.run(iterations);
+    e.gather();
+  }
+  Image out;
+  if (rank == 0 && jpeg_out) {
+    jpeg_out->bytes = e.store_root_jpeg(jpeg_out->quality);
+  } else if (rank == 0) {
+    out = Image(c.W, c.H, e.out_channels());
+    e.store_root(out.data.data(), false);
+  }
+  e.synchronize();
+  if (times) *times = e.times();
+  if (comm) comm->barrier();
+  return out;
+}
+}  // namespace
+
+Image run_rank(const EngineConfig& cfg, Comm* comm, int device, const Image* input, int iterations,
+               PhaseTimes* times, JpegOut* jpeg_out) {
+  return run_rank_impl(cfg, comm, device, input, nullptr, iterations, times, jpeg_out);
+}
+
+Image run_rank(const EngineConfig& cfg, Comm* comm, int device, const JpegCoefs* input, int iterations,
+               PhaseTimes* times, JpegOut* jpeg_out) {
+  return run_rank_impl(cfg, comm, device, nullptr, input, iterations, times, jpeg_out);
+}
+
+namespace {
+template <class In>
+Image run_group_impl(const EngineConfig& cfg, const std::vector<Comm*>& comms, const std::vector<int>& devices,
+                     const In& input, int iterations, PhaseTimes* times, JpegOut* jpeg_out) {
+  const int world = (int)comms.size();
+  Image out;
+  std::mutex mu;
+  std::exception_ptr err;
+  auto body = [&](int r) {
+    try {
+      PhaseTimes t;
+      Image o = run_rank(cfg, comms[r], devices.empty() ? cfg.device : devices[r], r == 0 ? &input : nullptr,
+                         iterations, &t, r == 0 ? jpeg_out : nullptr);
+      if (r == 0) {
+        std::lock_guard<std::mutex> lk(mu);
+        out = std::move(o);
+        if (times) *times = t;
+      }
+    } catch (const std::exception& ex) {
+      STRIPE_LOG(Error, r, "rank failed: " << ex.what() << " (aborting the group)");
+      std::lock_guard<std::mutex> lk(mu);
+      if (!err) err = std::current_exception();
+      for (Comm* c : comms) c->abort("rank " + std::to_string(r) + " failed");
+    } catch (...) {
+      std::lock_guard<std::mutex> lk(mu);
+      if (!err) err = std::current_exception();
+      // one process owns every rank: abort the whole group (Q9), so ranks
+      // blocked on this one fail at once instead of at the comm timeout
+      for (Comm* c : comms) c->abort("rank " + std::to_string(r) + " failed");
+    }
+  };
+  std::vector<std::thread> th;
+  for (int r = 0; r < world; ++r) th.emplace_back(body, r);
+  for (auto& t : th) t.join();
+  if (err) std::rethrow_exception(err);
+  return out;
+}
+}  // namespace
+
+Image run_group(const EngineConfig& cfg, const std::vector<Comm*>& comms, const std::vector<int>& devices,
+                const Image& input, int iterations, PhaseTimes* times, JpegOut* jpeg_out) {
+  STRIPE_CHECK(input.W == cfg.W && input.H == cfg.H && input.C == cfg.C, "input does not match the config");
+  return run_group_impl(cfg, comms, devices, input, iterations, times, jpeg_out);
+}
+
+Image run_group(const EngineConfig& cfg, const std::vector<Comm*>& comms, const std::vector<int>& devices,
+                const JpegCoefs& input, int iterations, PhaseTimes* times, JpegOut* jpeg_out) {
+  STRIPE_CHECK(input.W == cfg.W && input.H == cfg.H && (int)input.comps.size() == cfg.C,
+               "input does not match the config");
+  return run_group_impl(cfg, comms, devices, input, iterations, times, jpeg_out);
+}
+
+Image run_local_group(const EngineConfig& cfg, int world, const Image& input, int iterations, PhaseTimes* times) {
+  auto hub = make_local_hub(world, cfg.backend == BackendKind::Device);
+  std::vector<std::unique_ptr<Comm>> owned;
+  std::vector<Comm*> comms;
+  for (int r = 0; r < world; ++r) {
+    owned.push_back(make_local_comm(hub, r));
+    comms.push_back(owned.back().get());
+  }
+  return run_group(cfg, comms, {}, input, iterations, times);
+}
+
+}  // namespace stripe

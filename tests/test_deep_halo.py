@@ -2,7 +2,7 @@
 
 With halo depth k an iterated single-pass chain exchanges k*R rows once per k
 iterations and recomputes the neighbours' boundary band locally
-(Engine::run_deep, csrc/runtime/engine.cpp).  It must reproduce the golden
+(Engine::run_deep, csrc/runtime/engine_schedules.cpp).  It must reproduce the golden
 iterated result bit-for-bit for every depth, rank count and iteration count
 (including counts that are not multiples of k).  The reference exchanges no
 halo at all (kernel.cu:131-137); here the multi-rank output equals

@@ -196,7 +196,7 @@ def test_multipass_chain_level_exchange_gpu(m, chain, ranks, depth, iters):
 
 @pytest.mark.parametrize("chain", ["gaussian5", "sobel,emboss3", "gray:ref,contrast:3.5,emboss3"])
 def test_autotune_bands_keep_output_exact(m, chain):
-    """The band autotuner (engine.cpp autotune_bands: bursts of back-to-back
+    """The band autotuner (engine_tune.cpp autotune_bands: bursts of back-to-back
     launches into the scratch buffer) picks a band per stencil pass from its
     candidate set and leaves the run's result bit-exact vs the golden path."""
     C = m._C

@@ -61,6 +61,10 @@ CORE_SOURCES = [
     "runtime/comm_rccl.cpp",
     "runtime/comm_local.cpp",
     "runtime/engine.cpp",
+    "runtime/engine_schedules.cpp",
+    "runtime/engine_tune.cpp",
+    "runtime/engine_transfer.cpp",
+    "runtime/engine_group.cpp",
     "runtime/trace.cpp",
 ]
 # plain host C++ (no device compilation): CPU multiversioning (target_clones)
