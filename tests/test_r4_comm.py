@@ -424,3 +424,12 @@ def test_frame_stream_gpu_each_frame_exact(C, monkeypatch, chain, Cc):
         for _ in range(rounds):
             ref = C.golden_apply(ref, chain, "reflect101", True)
         assert (fs.frames[f].result_stripe() == ref).all(), f
+
+
+def test_bench_fixed_halo_schedule_recorded(tmp_path):
+    # --halo-schedule fixes the request (no probe); a host engine runs it as
+    # its one schedule and the record says both
+    r, lines, _ = _bench(tmp_path, 2, ["--halo-schedule", "pipeline", "--budget-s", "0.01"], {})
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = json.loads(lines[0])
+    assert rec["halo_schedule"] == {"chosen": "serial", "ms": {}, "requested": "pipeline"}
