@@ -422,6 +422,8 @@ int cmd_bench(const Args& a) {
       // round-robin, each engine on its own stream (parallel.FrameStream's
       // native counterpart: one frame's kernel boundary overlaps the next)
       const int nframes = scope == "resident" ? std::max(1, a.geti("frames", 1)) : 1;
+      std::vector<double> sched_ms(3, 0.0);  // frames mode: per-schedule step time, max over ranks
+      int chosen = -1;
       auto body = [&](int r) {
         try {
           EngineConfig c = cfg;
@@ -445,6 +447,39 @@ int cmd_bench(const Args& a) {
               if (!it_ok) fe.rewind();
               fe.run(1);
             };
+            // halo schedule by measurement (bench.py's FrameStream.pick_schedule):
+            // every rank times the same three schedules, the max over ranks
+            // decides; --halo-schedule serial|overlap|pipeline fixes one
+            const std::string hs = a.get("halo-schedule", "auto");
+            if (hs != "auto") {
+              STRIPE_CHECK(hs == "serial" || hs == "overlap" || hs == "pipeline",
+                           "--halo-schedule must be auto, serial, overlap or pipeline");
+              for (auto& fe : fr) fe->set_halo_schedule(hs == "serial" ? 0 : hs == "overlap" ? 1 : 2);
+            } else if (N > 1 && backend != "host") {
+              const int m = std::max(20, 4 * nframes);
+              for (int sc = 0; sc < 3; ++sc) {
+                for (auto& fe : fr) fe->set_halo_schedule(sc);
+                for (int i = 0; i < 2 * nframes; ++i) fstep(i);
+                for (auto& fe : fr) fe->synchronize();
+                g.comms[r]->barrier();
+                const double s0 = now_ms();
+                for (int i = 0; i < m; ++i) fstep(i);
+                for (auto& fe : fr) fe->synchronize();
+                g.comms[r]->barrier();
+                const double el = (now_ms() - s0) / m;
+                std::lock_guard<std::mutex> lk(mu);
+                sched_ms[(size_t)sc] = std::max(sched_ms[(size_t)sc], el);
+              }
+              g.comms[r]->barrier();  // every rank's timings are in
+              int best = 0;
+              {
+                std::lock_guard<std::mutex> lk(mu);
+                for (int sc = 1; sc < 3; ++sc)
+                  if (sched_ms[(size_t)sc] < sched_ms[(size_t)best]) best = sc;
+                chosen = best;
+              }
+              for (auto& fe : fr) fe->set_halo_schedule(best);
+            }
             for (int i = 0; i < warmup; ++i) fstep(i);
             for (auto& fe : fr) fe->synchronize();
             g.comms[r]->barrier();
@@ -523,12 +558,22 @@ int cmd_bench(const Args& a) {
       double ms = 0;
       for (double v : per_rank) ms = std::max(ms, v);
       const double mpx = (double)W * H / (ms * 1e-3) / 1e6;
-      char buf[512];
+      static const char* kSched[] = {"serial", "overlap", "pipeline"};
+      char sched[160];
+      if (chosen >= 0)
+        std::snprintf(sched, sizeof sched,
+                      ",\"halo_schedule\":{\"chosen\":\"%s\",\"ms\":{\"serial\":%.5f,\"overlap\":%.5f,"
+                      "\"pipeline\":%.5f}}",
+                      kSched[chosen], sched_ms[0], sched_ms[1], sched_ms[2]);
+      else
+        sched[0] = '\0';
+      char buf[768];
       std::snprintf(buf, sizeof buf,
                     "{\"metric\":\"Mpixels/s\",\"scope\":\"%s\",\"value\":%.1f,\"ms_per_iter\":%.4f,\"n_ranks\":%d,"
                     "\"backend\":\"%s\",\"chain\":\"%s\",\"W\":%d,\"H\":%d,\"C\":%d,\"iters\":%d,\"warmup\":%d,"
-                    "\"frames\":%d}",
-                    scope.c_str(), mpx, ms, N, backend.c_str(), cfg.chain.c_str(), W, H, C, iters, warmup, nframes);
+                    "\"frames\":%d%s}",
+                    scope.c_str(), mpx, ms, N, backend.c_str(), cfg.chain.c_str(), W, H, C, iters, warmup, nframes,
+                    sched);
       std::printf("%s\n", buf);
       std::fflush(stdout);
       results.push_back(buf);
@@ -554,6 +599,7 @@ void usage() {
                "        [--scope resident|device,dist,e2e] [--backend rccl|local|host] [--json out.json]\n"
                "        [--no-overlap] [--no-pipeline] [--graphs] [--band ROWS] [--halo-depth K] [--dist-chunks K]\n"
                "        [--frames F]  (resident: a stream of F independent frames, cache-cold tuning)\n"
+               "        [--halo-schedule auto|serial|overlap|pipeline]  (frames at N > 1: auto times all three)\n"
                "  cmp   a.ppm b.ppm [--tol T]\n"
                "  gen   --synthetic WxHxC [--seed S] --output out.ppm|out.jpg\n"
                "  convert --input in.ppm|in.jpg --output out.ppm|out.jpg [--quality 95]\n"

@@ -112,6 +112,11 @@ def test_bench_frames_host(tmp_path):
         "--warmup", "1", "--frames", "3", "--backend", "host", "--json", js)
     recs = [json.loads(l) for l in js.read_text().splitlines()]
     assert [(x["n_ranks"], x["frames"]) for x in recs] == [(1, 3), (2, 3)] and all(x["value"] > 0 for x in recs)
+    assert all("halo_schedule" not in x for x in recs)  # host engines: nothing to choose
+    js2 = tmp_path / "f2.json"
+    run("bench", "--synthetic", "128x64x3", "--chain", "gaussian5", "--ranks", "2", "--iters", "2", "--warmup", "1",
+        "--frames", "2", "--backend", "host", "--halo-schedule", "overlap", "--json", js2)
+    assert json.loads(js2.read_text().splitlines()[0])["value"] > 0
 
 
 @pytest.mark.gpu
@@ -121,6 +126,10 @@ def test_gpu_bench_frames_local(tmp_path):
         "--warmup", "2", "--frames", "4", "--backend", "local", "--json", js)
     recs = [json.loads(l) for l in js.read_text().splitlines()]
     assert [x["frames"] for x in recs] == [4, 4] and all(x["value"] > 0 for x in recs)
+    # two ranks: the three halo schedules were timed (max over ranks), the fastest kept
+    hs = recs[1]["halo_schedule"]
+    assert "halo_schedule" not in recs[0] and hs["chosen"] == min(hs["ms"], key=hs["ms"].get)
+    assert all(v > 0 for v in hs["ms"].values())
 
 
 @pytest.mark.gpu
