@@ -367,6 +367,14 @@ class FrameStream:
         # rank's own stripe runs another way (e.g. a thin stripe without the
         # pipeline); host engines have one schedule and time nothing
         scheds = list(self.SCHEDULES) if self.streams else ["serial"]
+        if getattr(getattr(self.head, "ctx", None), "world", 2) == 1:
+            # one rank exchanges nothing: only schedules that differ on it (none)
+            eff = []
+            for s in scheds:
+                self.set_schedule(s)
+                if self.schedule not in eff:
+                    eff.append(self.schedule)
+            scheds = eff
         opts = list(self.stream_options)
         cands = [(s, ns) for ns in opts for s in scheds]
         key = (lambda c: f"{c[0]}@{c[1]}") if len(opts) > 1 else (lambda c: c[0])
