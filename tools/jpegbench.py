@@ -23,7 +23,6 @@ def main():
     a = ap.parse_args()
     import torch
 
-    import mpi_cuda_imagemanipulation_amd as m
     from mpi_cuda_imagemanipulation_amd._native import C
 
     n = a.size
