@@ -1,8 +1,9 @@
 """Image I/O.  PPM (P6, RGB) / PGM (P5, gray), maxval 255, ASCII P2/P3 on read,
-and baseline JPEG (the reference's format: cv::imread, kernel.cu:110;
-imwrite, kernel.cu:236): native (csrc/core/image.cpp, csrc/core/jpeg.cpp),
-atomic writes (temp file + rename).  Other formats (PNG, BMP, TIFF,
-progressive JPEG) go through Pillow when it is installed.
+and JPEG (the reference's format: cv::imread, kernel.cu:110; imwrite,
+kernel.cu:236): native (csrc/core/image.cpp, csrc/core/jpeg.cpp: sequential
+and progressive decode, baseline encode), atomic writes (temp file + rename).
+Other formats (PNG, BMP, TIFF; lossless / arithmetic-coded JPEG) go through
+Pillow when it is installed.
 Arrays are HxW (gray) or HxWx3 (RGB order) uint8.
 """
 from __future__ import annotations
@@ -31,7 +32,7 @@ def read_image(path: str) -> np.ndarray:
     if _is_jpeg(path):
         try:
             return C.read_image(str(path))
-        except RuntimeError as e:  # progressive / arithmetic-coded: Pillow, if present
+        except RuntimeError as e:  # lossless / arithmetic-coded: Pillow, if present
             if "not supported" not in str(e):
                 raise
     try:

@@ -1,10 +1,15 @@
-// Mutation fuzz of the baseline JPEG decoder (csrc/core/jpeg.cpp), built with
-// host ASan/UBSan by tests/test_sanitizers.py: random byte mutations and
-// truncations of whole files, then targeted mutations of the table / frame
-// header segments (DHT, DQT, SOF0).  Every input must decode or throw.
+// Mutation fuzz of the JPEG decoder (csrc/core/jpeg.cpp), built with host
+// ASan/UBSan by tests/test_sanitizers.py: random byte mutations and
+// truncations of whole files, then targeted mutations of the table / frame /
+// scan header segments (DHT, DQT, SOF0/SOF2, SOS).  Seeds: two files of our
+// own encoder, plus any files named after the iteration count (the test
+// passes progressive files from another encoder).  Every input must decode
+// or throw.
 #include <cstdio>
 #include <cstdlib>
+#include <fstream>
 #include <random>
+#include <sstream>
 #include <vector>
 
 #include "stripe/image.h"
@@ -25,17 +30,24 @@ int main(int argc, char** argv) {
       ++err;
     }
   };
-  for (int sub = 0; sub < 2; ++sub) {
-    const std::string base = encode_jpeg(img, 80, sub != 0, 2);
+  std::vector<std::string> seeds = {encode_jpeg(img, 80, false, 2), encode_jpeg(img, 80, true, 2)};
+  for (int a = 2; a < argc; ++a) {
+    std::ifstream f(argv[a], std::ios::binary);
+    std::stringstream ss;
+    ss << f.rdbuf();
+    seeds.push_back(ss.str());
+  }
+  for (const std::string& base : seeds) {
+    attempt(base);
     std::vector<size_t> segs;
     for (size_t i = 2; i + 1 < base.size(); ++i) {
       const uint8_t m = (uint8_t)base[i + 1];
-      if ((uint8_t)base[i] == 0xFF && (m == 0xC4 || m == 0xDB || m == 0xC0)) segs.push_back(i);
+      if ((uint8_t)base[i] == 0xFF && (m == 0xC4 || m == 0xDB || m == 0xC0 || m == 0xC2 || m == 0xDA)) segs.push_back(i);
     }
     for (int t = 0; t < iters; ++t) {
       std::string b = base;
       const int nm = 1 + (int)(rng() % 5);
-      if (t % 2 == 0) {
+      if (t % 2 == 0 || segs.empty()) {
         for (int k = 0; k < nm; ++k) b[2 + rng() % (b.size() - 2)] = (char)(rng() & 255);
         if (rng() % 5 == 0) b.resize(2 + rng() % (b.size() - 2));
       } else {

@@ -1,4 +1,4 @@
-"""Native baseline JPEG codec (csrc/core/jpeg.cpp): the reference's own I/O
+"""Native JPEG codec (csrc/core/jpeg.cpp: sequential + progressive decode, baseline encode): the reference's own I/O
 format (cv::imread of a JPEG, kernel.cu:110; imwrite JPEG, kernel.cu:236).
 
 Oracle: Pillow (libjpeg-turbo) where it is importable.  Decoders may differ by
@@ -109,10 +109,58 @@ def test_extreme_statistics_huffman_tables(C):
         assert np.abs(theirs.astype(int) - C.decode_jpeg(enc).astype(int)).max() <= 3
 
 
-def test_progressive_refused_with_message(C):
-    data = _pil_encode(_smooth(32, 32, 3), quality=80, progressive=True)
-    with pytest.raises(RuntimeError, match="progressive"):
-        C.decode_jpeg(data)
+@pytest.mark.parametrize("shape", [(64, 64, 3), (67, 93, 3), (200, 301, 3), (57, 41, 1), (1, 1, 3), (9, 300, 1)])
+@pytest.mark.parametrize("subsampling", [0, 1, 2])
+@pytest.mark.parametrize("restart", [{}, {"restart_marker_rows": 1}, {"restart_marker_blocks": 3}])
+def test_progressive_decode_matches_libjpeg(C, shape, subsampling, restart):
+    # SOF2 (libjpeg's default progression: interleaved DC first / refine,
+    # spectral bands, successive approximation down to Al = 0), with and
+    # without restart intervals
+    h, w, c = shape
+    if c == 1 and subsampling:
+        pytest.skip("gray has one sampling")
+    img = _smooth(h, w, c)
+    data = _pil_encode(img, quality=90, subsampling=subsampling, progressive=True, **restart)
+    assert b"\xff\xc2" in data
+    ours = C.decode_jpeg(data)
+    ref = _pil_decode(data, c == 1)
+    assert ours.shape == ref.shape
+    d = np.abs(ours.astype(int) - ref.astype(int))
+    assert d.max() <= 3 and d.mean() < 0.1, (d.max(), d.mean())
+
+
+@pytest.mark.parametrize("shape,subsampling", [((67, 93, 3), 2), ((200, 301, 3), 0), ((200, 301, 3), 1),
+                                               ((57, 41, 1), 0)])
+@pytest.mark.parametrize("quality", [50, 95])
+def test_progressive_equals_sequential_exactly(C, shape, subsampling, quality):
+    # the same frame saved sequential and progressive carries the same
+    # quantised coefficients: the two decodes must agree bit for bit
+    img = _smooth(*shape, noise=20.0, seed=quality)
+    kw = {"subsampling": subsampling} if shape[2] == 3 else {}
+    seq = C.decode_jpeg(_pil_encode(img, quality=quality, **kw))
+    prog = C.decode_jpeg(_pil_encode(img, quality=quality, progressive=True, **kw))
+    assert np.array_equal(seq, prog)
+
+
+def test_truncated_progressive_decodes_what_arrived(C):
+    # like libjpeg: the scans that arrived give a coarser picture, the missing
+    # refinements stay zero (no error, same size, still the picture)
+    img = _smooth(96, 128, 3, noise=10.0)
+    data = _pil_encode(img, quality=90, progressive=True)
+    full = C.decode_jpeg(data)
+    part = C.decode_jpeg(data[: len(data) * 2 // 3])
+    assert part.shape == full.shape and not np.array_equal(part, full)
+    assert _psnr(part, img) > 20.0
+
+
+def test_progressive_out_of_order_refinement_rejected_or_decoded(C):
+    # a refinement scan whose Al is not Ah - 1 is malformed (T.81 G.1.1.1.1)
+    data = bytearray(_pil_encode(_smooth(32, 32, 3), quality=80, progressive=True))
+    k = data.index(b"\xff\xda", data.index(b"\xff\xda") + 2)  # second scan header
+    ns = data[k + 4]
+    data[k + 4 + 1 + 2 * ns + 2] = 0x31  # Ah 3, Al 1
+    with pytest.raises(RuntimeError, match="progressive scan parameters"):
+        C.decode_jpeg(bytes(data))
 
 
 def test_corrupt_input_raises(C):
@@ -208,14 +256,16 @@ def test_parallel_restart_intervals_decode_identically(C):
 
 # ---- pixel stages on the GPU (csrc/hip/jpeg_dev.hip) ----
 @pytest.mark.gpu
-@pytest.mark.parametrize("shape,subsampling", [((211, 157, 3), 0), ((211, 157, 3), 1), ((211, 157, 3), 2),
-                                               ((64, 99, 1), 0), ((1, 1, 3), 2)])
-def test_device_decode_matches_host(C, tmp_path, shape, subsampling):
+@pytest.mark.parametrize("shape,subsampling,progressive",
+                         [((211, 157, 3), 0, False), ((211, 157, 3), 1, False), ((211, 157, 3), 2, False),
+                          ((64, 99, 1), 0, False), ((1, 1, 3), 2, False), ((211, 157, 3), 2, True),
+                          ((64, 99, 1), 0, True)])
+def test_device_decode_matches_host(C, tmp_path, shape, subsampling, progressive):
     import mpi_cuda_imagemanipulation_amd as m
 
     h, w, c = shape
     img = _smooth(h, w, c)
-    data = _pil_encode(img, quality=90, **({"subsampling": subsampling} if c == 3 else {}))
+    data = _pil_encode(img, quality=90, progressive=progressive, **({"subsampling": subsampling} if c == 3 else {}))
     p = tmp_path / "x.jpg"
     p.write_bytes(data)
     got = m.utils.read_image_device(str(p))

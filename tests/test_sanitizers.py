@@ -98,6 +98,19 @@ def test_asan_jpeg_decoder_fuzz(tmp_path):
     if b.returncode != 0 and "sanitizer" in b.stderr.lower():
         pytest.skip("sanitizer runtimes unavailable: " + b.stderr[-300:])
     assert b.returncode == 0, b.stderr[-3000:]
-    r = _run(str(exe), "1500")
+    seeds = []
+    try:  # progressive (SOF2) seeds from libjpeg, with and without restart intervals
+        import numpy as np
+        from PIL import Image
+
+        rng = np.random.default_rng(5)
+        for k, kw in enumerate(({}, {"restart_marker_rows": 1})):
+            img = np.clip(128 + rng.normal(0, 30, (29, 37, 3)), 0, 255).astype(np.uint8)
+            f = tmp_path / f"prog{k}.jpg"
+            Image.fromarray(img).save(f, "JPEG", quality=85, progressive=True, **kw)
+            seeds.append(str(f))
+    except ImportError:
+        pass
+    r = _run(str(exe), "1000", *seeds)
     assert r.returncode == 0 and "jpeg fuzz:" in r.stdout, (r.stdout + r.stderr)[-3000:]
     assert "AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-3000:]

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """JPEG I/O throughput on one MI355X: host codec (csrc/core/jpeg.cpp), the
 split codec with pixel stages on the GPU (csrc/hip/jpeg_dev.hip), and Pillow
-(libjpeg-turbo) as the library baseline.  Synthetic smooth RGB frame.
-Prints one JSON line.  python tools/jpegbench.py [--size 8192] [--quality 90]"""
+(libjpeg-turbo) as the library baseline.  Synthetic smooth RGB frame; with
+Pillow also the same frame saved progressive by libjpeg (decode only: the
+native encoder writes baseline).  Prints one JSON line.  python tools/jpegbench.py [--size 8192] [--quality 90]"""
 import argparse
 import io
 import json
@@ -67,6 +68,31 @@ def main():
             Image.fromarray(img).save(b, "JPEG", quality=a.quality)
 
         rec["encode_ms"]["pillow"] = best(pil_enc)
+    except ImportError:
+        pass
+    try:
+        import tempfile
+
+        from PIL import Image
+
+        with tempfile.TemporaryDirectory() as td:  # (Pillow's progressive writer wants a real file)
+            f = os.path.join(td, "p.jpg")
+            Image.fromarray(img).save(f, "JPEG", quality=a.quality, progressive=True)
+            prog = open(f, "rb").read()
+
+        def dev_decode_prog():
+            jc = C.jpeg_entropy_decode(prog)
+            jc.to_device(out.data_ptr(), n * 3, stream)
+            torch.cuda.synchronize()
+
+        ref = np.asarray(Image.open(io.BytesIO(prog)).convert("RGB"))
+        rec["progressive"] = {
+            "jpeg_bytes": len(prog),
+            "decode_ms": {"host": best(lambda: C.decode_jpeg(prog)),
+                          "entropy_only": best(lambda: C.jpeg_entropy_decode(prog)),
+                          "entropy_host_pixels_gpu": best(dev_decode_prog),
+                          "pillow": best(lambda: np.asarray(Image.open(io.BytesIO(prog)).convert("RGB")))},
+            "host_vs_pillow_max_diff": int(np.abs(C.decode_jpeg(prog).astype(int) - ref.astype(int)).max())}
     except ImportError:
         pass
     dev_decode()
