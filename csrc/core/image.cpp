@@ -69,7 +69,7 @@ Image decode_pnm(const std::string& bytes) {
   } else {
     STRIPE_CHECK(avail >= 2 * n - 1, "PNM: truncated ASCII pixel data (" << n << " samples declared)");
   }
-  Image img((int)W, (int)H, C);
+  Image img((int)W, (int)H, C, NoInit{});  // every sample is read below (or the decode throws)
   if (kind == '5' || kind == '6') {
     rd.i += 1;
     std::copy(bytes.begin() + rd.i, bytes.begin() + rd.i + n, img.data.begin());
@@ -157,7 +157,7 @@ void synth_rows(uint64_t seed, int W, int C, int row0, int rows, uint8_t* dst) {
 }
 
 Image synth_image(uint64_t seed, int W, int H, int C) {
-  Image img(W, H, C);
+  Image img(W, H, C, NoInit{});
   synth_rows(seed, W, C, 0, H, img.data.data());
   return img;
 }

@@ -22,12 +22,37 @@
 
 namespace stripe {
 
+// Vector storage that does not zero on resize (large coefficient planes are
+// first touched by parallel workers instead of one thread's value-init).
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = NoInitAlloc<U>;
+  };
+  NoInitAlloc() = default;
+  template <class U>
+  NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
+  template <class U>
+  void construct(U* p) noexcept {
+    ::new ((void*)p) U;
+  }
+  template <class U, class... A>
+  void construct(U* p, A&&... a) {
+    ::new ((void*)p) U(std::forward<A>(a)...);
+  }
+};
+struct NoInit {};  // tag: storage the caller overwrites entirely
+
 struct Image {
-  int W = 0, H = 0, C = 0;      // C in {1, 3}; pixels interleaved R,G,B
-  std::vector<uint8_t> data;    // packed, H * W * C bytes
+  int W = 0, H = 0, C = 0;  // C in {1, 3}; pixels interleaved R,G,B
+  std::vector<uint8_t, NoInitAlloc<uint8_t>> data;  // packed, H * W * C bytes
 
   Image() = default;
-  Image(int w, int h, int c) : W(w), H(h), C(c), data((size_t)w * h * c, 0) {}
+  Image(int w, int h, int c) : W(w), H(h), C(c), data((size_t)w * h * c, 0) {}  // zeroed
+  // not zeroed: for producers that write every byte (first touched by their
+  // own, often parallel, writers instead of one thread's memset)
+  Image(int w, int h, int c, NoInit) : W(w), H(h), C(c), data((size_t)w * h * c) {}
   size_t bytes() const { return data.size(); }
   int64_t row_bytes() const { return (int64_t)W * C; }
   uint8_t* row(int y) { return data.data() + (size_t)y * W * C; }
@@ -55,26 +80,6 @@ std::string encode_jpeg(const Image& img, int quality = 95, bool subsample = tru
 // Decode: jpeg_entropy_decode() parses the file and Huffman-decodes every
 // block into dequantised DCT coefficients (natural order; block rows of the
 // MCU-padded component plane); jpeg_pixels() runs IDCT + upsampling + colour.
-// Vector storage that does not zero on resize (large coefficient planes are
-// first touched by parallel workers instead of one thread's value-init).
-template <class T>
-struct NoInitAlloc : std::allocator<T> {
-  template <class U>
-  struct rebind {
-    using other = NoInitAlloc<U>;
-  };
-  NoInitAlloc() = default;
-  template <class U>
-  NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
-  template <class U>
-  void construct(U* p) noexcept {
-    ::new ((void*)p) U;
-  }
-  template <class U, class... A>
-  void construct(U* p, A&&... a) {
-    ::new ((void*)p) U(std::forward<A>(a)...);
-  }
-};
 using CoefVec = std::vector<int16_t, NoInitAlloc<int16_t>>;
 
 struct JpegCoefs {

@@ -31,9 +31,9 @@ using U8Array = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>;
 Image image_from_numpy(const U8Array& a) {
   Image img;
   if (a.ndim() == 2) {
-    img = Image((int)a.shape(1), (int)a.shape(0), 1);
+    img = Image((int)a.shape(1), (int)a.shape(0), 1, NoInit{});
   } else if (a.ndim() == 3) {
-    img = Image((int)a.shape(1), (int)a.shape(0), (int)a.shape(2));
+    img = Image((int)a.shape(1), (int)a.shape(0), (int)a.shape(2), NoInit{});
   } else {
     fail("image array must be HxW or HxWxC");
   }
@@ -128,7 +128,7 @@ PYBIND11_MODULE(_C, m) {
       py::arg("path"), py::arg("img"), py::arg("quality") = 95);
   m.def("synth_image", [](uint64_t seed, int W, int H, int C) { return image_to_numpy(synth_image(seed, W, H, C)); });
   m.def("synth_rows", [](uint64_t seed, int W, int C, int row0, int rows) {
-    Image img(W, rows, C);
+    Image img(W, rows, C, NoInit{});
     synth_rows(seed, W, C, row0, rows, img.data.data());
     return image_to_numpy(img);
   });

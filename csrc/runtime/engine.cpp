@@ -716,7 +716,7 @@ std::string Engine::store_root_jpeg(int quality) {
   if (rank_ != 0) return {};
   const int C = out_c_ > 0 ? out_c_ : plan_.cout;
   if (!device()) {
-    Image img(cfg_.W, cfg_.H, C);
+    Image img(cfg_.W, cfg_.H, C, NoInit{});
     store_root(img.data.data(), false);
     return encode_jpeg(img, quality);
   }

@@ -154,7 +154,7 @@ Image run_rank_impl(const EngineConfig& cfg_in, Comm* comm, int device, const Im
   if (rank == 0 && jpeg_out) {
     jpeg_out->bytes = e.store_root_jpeg(jpeg_out->quality);
   } else if (rank == 0) {
-    out = Image(c.W, c.H, e.out_channels());
+    out = Image(c.W, c.H, e.out_channels(), NoInit{});  // store_root writes every byte
     e.store_root(out.data.data(), false);
   }
   e.synchronize();
