@@ -65,10 +65,11 @@ void write_pnm(const std::string& path, const Image& img);
 Image decode_pnm(const std::string& bytes);
 std::string encode_pnm(const Image& img);
 
-// Baseline JPEG (csrc/core/jpeg.cpp): the reference's own input / output
-// format (cv::imread / imwrite, kernel.cu:110,236).  decode: sequential
-// Huffman, 1 or 3 components, any sampling, restart intervals (decoded in
-// parallel when every marker is in place); encode: JFIF, 4:2:0 (subsample)
+// JPEG (csrc/core/jpeg.cpp): the reference's own input / output format
+// (cv::imread / imwrite, kernel.cu:110,236).  decode: sequential and
+// progressive Huffman, 1 or 3 components, any sampling, restart intervals
+// (decoded in parallel when every marker is in place; the scans of a
+// progressive frame concurrently); encode (baseline): JFIF, 4:2:0 (subsample)
 // or 4:4:4 YCbCr, quality 1..100 on the Annex K tables, Huffman tables fitted
 // to the image, restart interval in MCUs (-1: one MCU row, coded in parallel;
 // 0: none).
