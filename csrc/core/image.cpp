@@ -9,9 +9,14 @@
 #include <cstdio>
 #include <fstream>
 #include <sstream>
+#include <sys/mman.h>
 #include <unistd.h>
 
 namespace stripe {
+
+void advise_huge(void* p, size_t bytes) {
+  (void)madvise(p, bytes, MADV_HUGEPAGE);  // best effort: a kernel with THP off says no
+}
 
 namespace {
 

@@ -9,6 +9,8 @@
 #pragma once
 
 #include <cstdint>
+#include <cstdlib>
+#include <new>
 #include <memory>
 #include <string>
 #include <utility>
@@ -24,6 +26,8 @@ namespace stripe {
 
 // Vector storage that does not zero on resize (large coefficient planes are
 // first touched by parallel workers instead of one thread's value-init).
+void advise_huge(void* p, size_t bytes);  // madvise(MADV_HUGEPAGE), best effort
+
 template <class T>
 struct NoInitAlloc : std::allocator<T> {
   template <class U>
@@ -40,6 +44,21 @@ struct NoInitAlloc : std::allocator<T> {
   template <class U, class... A>
   void construct(U* p, A&&... a) {
     ::new ((void*)p) U(std::forward<A>(a)...);
+  }
+  // large buffers (frames, coefficient planes) on 2 MiB-aligned transparent
+  // huge pages: first touch then faults once per 2 MiB instead of per 4 KiB
+  static constexpr size_t kHuge = size_t(2) << 20;
+  T* allocate(size_t n) {
+    const size_t b = n * sizeof(T);
+    if (b < 4 * kHuge) return std::allocator<T>::allocate(n);
+    void* p = std::aligned_alloc(kHuge, (b + kHuge - 1) / kHuge * kHuge);
+    if (!p) throw std::bad_alloc();
+    advise_huge(p, (b + kHuge - 1) / kHuge * kHuge);
+    return static_cast<T*>(p);
+  }
+  void deallocate(T* p, size_t n) noexcept {
+    if (n * sizeof(T) < 4 * kHuge) std::allocator<T>::deallocate(p, n);
+    else std::free(p);
   }
 };
 struct NoInit {};  // tag: storage the caller overwrites entirely
