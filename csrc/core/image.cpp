@@ -7,6 +7,7 @@
 #include <cctype>
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <fstream>
 #include <sstream>
 #include <sys/mman.h>
@@ -50,35 +51,61 @@ struct Reader {
 
 }  // namespace
 
-Image decode_pnm(const std::string& bytes) {
+// Magic, size and maxval of a PNM file; `data` is where the samples start
+// (binary: after the one whitespace byte that ends the header).
+namespace {
+
+struct PnmHeader {
+  char kind = 0;
+  int C = 0;
+  long W = 0, H = 0;
+  size_t data = 0;
+  size_t samples() const { return (size_t)W * (size_t)H * (size_t)C; }
+};
+
+PnmHeader pnm_header(const std::string& bytes) {
   STRIPE_CHECK(bytes.size() >= 2 && bytes[0] == 'P', "PNM: missing magic");
-  const char kind = bytes[1];
-  STRIPE_CHECK(kind == '2' || kind == '3' || kind == '5' || kind == '6',
-               "PNM: unsupported magic P" << kind << " (P2/P3/P5/P6 only)");
-  const int C = (kind == '3' || kind == '6') ? 3 : 1;
+  PnmHeader h;
+  h.kind = bytes[1];
+  STRIPE_CHECK(h.kind == '2' || h.kind == '3' || h.kind == '5' || h.kind == '6',
+               "PNM: unsupported magic P" << h.kind << " (P2/P3/P5/P6 only)");
+  h.C = (h.kind == '3' || h.kind == '6') ? 3 : 1;
   Reader rd(bytes);
   rd.i = 2;
-  const long W = rd.read_int("width");
-  const long H = rd.read_int("height");
+  h.W = rd.read_int("width");
+  h.H = rd.read_int("height");
   const long maxval = rd.read_int("maxval");
-  STRIPE_CHECK(W >= 1 && H >= 1, "PNM: bad size " << W << "x" << H);
+  STRIPE_CHECK(h.W >= 1 && h.H >= 1, "PNM: bad size " << h.W << "x" << h.H);
   STRIPE_CHECK(maxval == 255, "PNM: only maxval 255 supported, got " << maxval);
-  // validate the payload size against the header before allocating (a forged
-  // header must not request a huge allocation; found by the ASan CLI tests)
-  const size_t n = (size_t)W * (size_t)H * (size_t)C;
-  const size_t avail = bytes.size() > rd.i ? bytes.size() - rd.i : 0;
-  if (kind == '5' || kind == '6') {
+  if (h.kind == '5' || h.kind == '6') {
     // exactly one whitespace byte after maxval, then raw samples
     STRIPE_CHECK(rd.i < bytes.size() && isspace((unsigned char)bytes[rd.i]), "PNM: header not terminated");
-    STRIPE_CHECK(avail - 1 >= n, "PNM: truncated pixel data (" << avail - 1 << " of " << n << " bytes)");
+    h.data = rd.i + 1;
   } else {
-    STRIPE_CHECK(avail >= 2 * n - 1, "PNM: truncated ASCII pixel data (" << n << " samples declared)");
+    h.data = rd.i;
   }
-  Image img((int)W, (int)H, C, NoInit{});  // every sample is read below (or the decode throws)
-  if (kind == '5' || kind == '6') {
-    rd.i += 1;
-    std::copy(bytes.begin() + rd.i, bytes.begin() + rd.i + n, img.data.begin());
+  return h;
+}
+
+}  // namespace
+
+Image decode_pnm(const std::string& bytes) {
+  const PnmHeader h = pnm_header(bytes);
+  // validate the payload size against the header before allocating (a forged
+  // header must not request a huge allocation; found by the ASan CLI tests)
+  const size_t n = h.samples();
+  const size_t avail = bytes.size() > h.data ? bytes.size() - h.data : 0;
+  if (h.kind == '5' || h.kind == '6') {
+    STRIPE_CHECK(avail >= n, "PNM: truncated pixel data (" << avail << " of " << n << " bytes)");
   } else {
+    STRIPE_CHECK(avail + 1 >= 2 * n, "PNM: truncated ASCII pixel data (" << n << " samples declared)");
+  }
+  Image img((int)h.W, (int)h.H, h.C, NoInit{});  // every sample is read below (or the decode throws)
+  if (h.kind == '5' || h.kind == '6') {
+    std::memcpy(img.data.data(), bytes.data() + h.data, n);
+  } else {
+    Reader rd(bytes);
+    rd.i = h.data;
     for (size_t k = 0; k < n; ++k) {
       long v = rd.read_int("sample");
       STRIPE_CHECK(v <= 255, "PNM: sample > maxval");
@@ -97,11 +124,54 @@ std::string encode_pnm(const Image& img) {
   return out;
 }
 
-Image read_pnm(const std::string& path) {
-  std::ifstream f(path, std::ios::binary);
+namespace {
+
+// whole file in one read (size from the stream end)
+std::string slurp(const std::string& path) {
+  std::ifstream f(path, std::ios::binary | std::ios::ate);
   STRIPE_CHECK(f.good(), "cannot open '" << path << "'");
-  std::string bytes((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
-  return decode_pnm(bytes);
+  const std::streamoff n = f.tellg();
+  STRIPE_CHECK(n >= 0, "cannot size '" << path << "'");
+  std::string s((size_t)n, '\0');
+  f.seekg(0);
+  f.read(&s[0], n);
+  STRIPE_CHECK(f.gcount() == n, "short read of '" << path << "'");
+  return s;
+}
+
+// binary PNM straight into the frame: header from the first 4 KiB, samples
+// read once into the (huge-page) image buffer; ASCII files, or a header that
+// does not fit the prefix, decode from the whole file
+Image read_pnm_file(const std::string& path, const std::string& prefix, std::ifstream& f, std::streamoff size) {
+  PnmHeader h;
+  try {
+    h = pnm_header(prefix);
+  } catch (const std::exception&) {
+    if ((std::streamoff)prefix.size() >= size) throw;
+    return decode_pnm(slurp(path));
+  }
+  if (h.kind != '5' && h.kind != '6') return decode_pnm(slurp(path));
+  const size_t n = h.samples();
+  const size_t avail = (size_t)size > h.data ? (size_t)size - h.data : 0;
+  STRIPE_CHECK(avail >= n, "PNM: truncated pixel data (" << avail << " of " << n << " bytes)");
+  Image img((int)h.W, (int)h.H, h.C, NoInit{});
+  f.clear();
+  f.seekg((std::streamoff)h.data);
+  f.read(reinterpret_cast<char*>(img.data.data()), (std::streamsize)n);
+  STRIPE_CHECK(f.gcount() == (std::streamsize)n, "short read of '" << path << "'");
+  return img;
+}
+
+}  // namespace
+
+Image read_pnm(const std::string& path) {
+  std::ifstream f(path, std::ios::binary | std::ios::ate);
+  STRIPE_CHECK(f.good(), "cannot open '" << path << "'");
+  const std::streamoff size = f.tellg();
+  f.seekg(0);
+  std::string prefix((size_t)std::min<std::streamoff>(size, 4096), '\0');
+  f.read(&prefix[0], (std::streamsize)prefix.size());
+  return read_pnm_file(path, prefix, f, size);
 }
 
 void write_pnm(const std::string& path, const Image& img) {
@@ -109,22 +179,17 @@ void write_pnm(const std::string& path, const Image& img) {
   {
     std::ofstream f(tmp, std::ios::binary | std::ios::trunc);
     STRIPE_CHECK(f.good(), "cannot write '" << tmp << "'");
-    const std::string enc = encode_pnm(img);
-    f.write(enc.data(), (std::streamsize)enc.size());
+    STRIPE_CHECK(img.C == 1 || img.C == 3, "PNM: only 1 or 3 channels can be written");
+    std::ostringstream hd;
+    hd << (img.C == 3 ? "P6" : "P5") << "\n" << img.W << " " << img.H << "\n255\n";
+    const std::string head = hd.str();
+    f.write(head.data(), (std::streamsize)head.size());
+    f.write(reinterpret_cast<const char*>(img.data.data()), (std::streamsize)img.data.size());  // no copy
     f.flush();
     STRIPE_CHECK(f.good(), "write failed for '" << tmp << "'");
   }
   STRIPE_CHECK(std::rename(tmp.c_str(), path.c_str()) == 0, "rename to '" << path << "' failed");
 }
-
-namespace {
-std::string slurp(const std::string& path) {
-  std::ifstream f(path, std::ios::binary);
-  STRIPE_CHECK(f.good(), "cannot open '" << path << "'");
-  return std::string((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
-}
-
-}  // namespace
 
 void write_file_atomic(const std::string& path, const std::string& bytes) {
   const std::string tmp = path + ".tmp." + std::to_string(getpid());
@@ -145,9 +210,14 @@ bool is_jpeg_path(const std::string& path) {
 }
 
 Image read_image(const std::string& path) {
-  const std::string bytes = slurp(path);
-  if (bytes.size() >= 2 && (uint8_t)bytes[0] == 0xFF && (uint8_t)bytes[1] == 0xD8) return decode_jpeg(bytes);
-  return decode_pnm(bytes);
+  std::ifstream f(path, std::ios::binary | std::ios::ate);
+  STRIPE_CHECK(f.good(), "cannot open '" << path << "'");
+  const std::streamoff size = f.tellg();
+  f.seekg(0);
+  std::string prefix((size_t)std::min<std::streamoff>(size, 4096), '\0');
+  f.read(&prefix[0], (std::streamsize)prefix.size());
+  if (prefix.size() >= 2 && (uint8_t)prefix[0] == 0xFF && (uint8_t)prefix[1] == 0xD8) return decode_jpeg(slurp(path));
+  return read_pnm_file(path, prefix, f, size);
 }
 
 void write_image(const std::string& path, const Image& img, int quality) {

@@ -49,3 +49,24 @@ def test_synthetic_is_deterministic_and_row_addressable(C):
     assert (rows == a[5:14]).all()
     # byte values are well spread
     assert 100 < a.mean() < 155 and len(np.unique(a)) > 200
+
+
+def test_file_reads_direct_and_fallback_paths(C, tmp_path, rng):
+    # binary files are read straight into the frame from a 4 KiB header
+    # prefix; a header longer than the prefix (comments) and ASCII files take
+    # the whole-file path; both agree with the in-memory decoder
+    img = rng.integers(0, 256, size=(37, 53, 3), dtype=np.uint8)
+    cases = {"plain.ppm": b"P6\n53 37\n255\n" + img.tobytes(),
+             "long_comment.ppm": b"P6\n#" + b"c" * 5000 + b"\n53 37\n255\n" + img.tobytes(),
+             "ascii.ppm": b"P3\n53 37\n255\n" + " ".join(map(str, img.reshape(-1).tolist())).encode()}
+    for name, data in cases.items():
+        p = tmp_path / name
+        p.write_bytes(data)
+        for reader in (C.read_pnm, C.read_image):
+            assert np.array_equal(reader(str(p)), img), (name, reader)
+    short = tmp_path / "short.ppm"
+    short.write_bytes(cases["plain.ppm"][:-5])
+    with pytest.raises(RuntimeError, match="truncated"):
+        C.read_pnm(str(short))
+    with pytest.raises(RuntimeError):
+        C.read_pnm(str(tmp_path / "missing.ppm"))
