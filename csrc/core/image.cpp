@@ -222,7 +222,7 @@ Image read_image(const std::string& path) {
 
 void write_image(const std::string& path, const Image& img, int quality) {
   if (is_jpeg_path(path)) write_file_atomic(path, encode_jpeg(img, quality));
-  else write_file_atomic(path, encode_pnm(img));
+  else write_pnm(path, img);  // (atomic too, without an encoded copy of the frame)
 }
 
 void synth_rows(uint64_t seed, int W, int C, int row0, int rows, uint8_t* dst) {
