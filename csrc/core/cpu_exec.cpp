@@ -296,12 +296,15 @@ void cpu_pass(const Pass& p, ConstView in, MutView out, int W, RowGeom g, int y0
 
 Image cpu_apply_plan(const Image& in, const Plan& plan, int threads) {
   STRIPE_CHECK(in.C == plan.cin, "image has " << in.C << " channels, chain expects " << plan.cin);
-  Image cur = in;
+  if (plan.passes.empty()) return in;
+  Image cur;  // the first pass reads the input in place (no copy of the frame)
+  const Image* src = &in;
   for (const Pass& p : plan.passes) {
     Image nxt(in.W, in.H, p.cout, NoInit{});  // cpu_pass writes every row of [0, H)
-    cpu_pass(p, ConstView{cur.data.data(), cur.row_bytes()}, MutView{nxt.data.data(), nxt.row_bytes()}, in.W,
+    cpu_pass(p, ConstView{src->data.data(), src->row_bytes()}, MutView{nxt.data.data(), nxt.row_bytes()}, in.W,
              RowGeom{0, in.H}, 0, in.H, threads);
     cur = std::move(nxt);
+    src = &cur;
   }
   return cur;
 }
