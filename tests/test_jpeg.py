@@ -109,7 +109,8 @@ def test_extreme_statistics_huffman_tables(C):
         assert np.abs(theirs.astype(int) - C.decode_jpeg(enc).astype(int)).max() <= 3
 
 
-@pytest.mark.parametrize("shape", [(64, 64, 3), (67, 93, 3), (200, 301, 3), (57, 41, 1), (1, 1, 3), (9, 300, 1)])
+@pytest.mark.parametrize("shape", [(64, 64, 3), (67, 93, 3), (200, 301, 3), (57, 41, 1), (1, 1, 3), (9, 300, 1),
+                                   (530, 610, 3)])
 @pytest.mark.parametrize("subsampling", [0, 1, 2])
 @pytest.mark.parametrize("restart", [{}, {"restart_marker_rows": 1}, {"restart_marker_blocks": 3}])
 def test_progressive_decode_matches_libjpeg(C, shape, subsampling, restart):
@@ -130,9 +131,11 @@ def test_progressive_decode_matches_libjpeg(C, shape, subsampling, restart):
 
 
 @pytest.mark.parametrize("shape,subsampling", [((67, 93, 3), 2), ((200, 301, 3), 0), ((200, 301, 3), 1),
-                                               ((57, 41, 1), 0)])
+                                               ((57, 41, 1), 0), ((520, 600, 3), 2), ((600, 520, 1), 0)])
 @pytest.mark.parametrize("quality", [50, 95])
 def test_progressive_equals_sequential_exactly(C, shape, subsampling, quality):
+    # (the two largest frames, >= 4096 blocks, take the threaded row pipeline
+    # between scans; the small ones decode their scans in order)
     # the same frame saved sequential and progressive carries the same
     # quantised coefficients: the two decodes must agree bit for bit
     img = _smooth(*shape, noise=20.0, seed=quality)
