@@ -114,3 +114,14 @@ def test_asan_jpeg_decoder_fuzz(tmp_path):
     r = _run(str(exe), "1000", *seeds)
     assert r.returncode == 0 and "jpeg fuzz:" in r.stdout, (r.stdout + r.stderr)[-3000:]
     assert "AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-3000:]
+    if seeds:
+        # a frame of >= 4096 blocks: its scans run concurrently on the row
+        # pipeline (threads + progress counters) -- fewer, slower iterations
+        y, x = np.mgrid[0:520, 0:600]
+        big = np.clip(np.stack([128 + 90 * np.sin(x / (9.0 + k)) * np.cos(y / 13.0) for k in range(3)], -1)
+                      + rng.normal(0, 12, (520, 600, 3)), 0, 255).astype(np.uint8)
+        f = tmp_path / "prog_big.jpg"
+        Image.fromarray(big).save(f, "JPEG", quality=85, progressive=True)
+        r = _run(str(exe), "40", str(f))
+        assert r.returncode == 0 and "jpeg fuzz:" in r.stdout, (r.stdout + r.stderr)[-3000:]
+    assert "AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-3000:]
