@@ -125,3 +125,37 @@ def test_asan_jpeg_decoder_fuzz(tmp_path):
         r = _run(str(exe), "40", str(f))
         assert r.returncode == 0 and "jpeg fuzz:" in r.stdout, (r.stdout + r.stderr)[-3000:]
     assert "AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-3000:]
+
+
+def test_tsan_jpeg_scan_pipeline(tmp_path):
+    # the threaded paths of the JPEG decoder under ThreadSanitizer (host g++):
+    # the row pipeline between progressive scans (progress counters, one thread
+    # per scan), restart intervals decoded in parallel, the parallel pixel
+    # stages; a few mutations too (a failing scan unwinds the ones waiting on it)
+    import shutil
+
+    if not shutil.which("g++"):
+        pytest.skip("g++ not available")
+    np = pytest.importorskip("numpy")
+    Image = pytest.importorskip("PIL.Image")
+    exe = tmp_path / "jpeg_tsan"
+    src = [os.path.join(ROOT, "tests", "native", "jpeg_fuzz.cpp"), os.path.join(ROOT, "csrc", "core", "jpeg.cpp"),
+           os.path.join(ROOT, "csrc", "core", "image.cpp")]
+    b = subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=thread", "-I" + os.path.join(ROOT, "csrc", "include"),
+                        *src, "-o", str(exe), "-lpthread"], capture_output=True, text=True, timeout=300)
+    if b.returncode != 0 and "sanitizer" in b.stderr.lower():
+        pytest.skip("ThreadSanitizer runtime unavailable: " + b.stderr[-300:])
+    assert b.returncode == 0, b.stderr[-3000:]
+    rng = np.random.default_rng(2)
+    y, x = np.mgrid[0:520, 0:600]
+    img = np.clip(np.stack([128 + 90 * np.sin(x / (9.0 + k)) * np.cos(y / 13.0) for k in range(3)], -1)
+                  + rng.normal(0, 12, (520, 600, 3)), 0, 255).astype(np.uint8)
+    seeds = []
+    for k, kw in enumerate(({}, {"restart_marker_rows": 1})):
+        f = tmp_path / f"p{k}.jpg"
+        Image.fromarray(img).save(f, "JPEG", quality=85, progressive=True, **kw)
+        seeds.append(str(f))
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1:exitcode=66", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([str(exe), "6", *seeds], capture_output=True, text=True, timeout=600, env=env)
+    assert "ThreadSanitizer" not in r.stderr, r.stderr[-4000:]
+    assert r.returncode == 0 and "jpeg fuzz:" in r.stdout, (r.returncode, (r.stdout + r.stderr)[-3000:])
