@@ -209,6 +209,8 @@ bool is_jpeg_path(const std::string& path) {
   return ext == ".jpg" || ext == ".jpeg" || ext == ".jfif";
 }
 
+std::string read_file(const std::string& path) { return slurp(path); }
+
 Image read_image(const std::string& path) {
   std::ifstream f(path, std::ios::binary | std::ios::ate);
   STRIPE_CHECK(f.good(), "cannot open '" << path << "'");

@@ -137,6 +137,8 @@ const int* jpeg_zigzag();
 // (temp file + rename).
 Image read_image(const std::string& path);
 void write_image(const std::string& path, const Image& img, int quality = 95);
+// the whole file, in one read
+std::string read_file(const std::string& path);
 // bytes to a temp file, then rename over `path`
 void write_file_atomic(const std::string& path, const std::string& bytes);
 // .jpg / .jpeg / .jfif (any case)
