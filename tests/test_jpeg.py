@@ -354,3 +354,29 @@ def test_cli_convert_and_cmp(C, tmp_path):
     assert np.array_equal(C.read_image(str(back)), C.decode_jpeg(jpg.read_bytes()))
     r = subprocess.run([cli, "cmp", str(back), str(jpg)], capture_output=True, text=True, env=env, timeout=60)
     assert r.returncode == 0 and '"max_abs":0' in r.stdout
+
+
+@pytest.mark.parametrize("shape,subsampling", [((1200, 1400, 3), 2), ((1300, 1100, 3), 0), ((1500, 1600, 1), 0),
+                                               ((1024, 1536, 3), 1)])
+def test_long_scan_speculative_decode_is_exact(C, shape, subsampling):
+    # > 1 MiB of entropy-coded data and no restart markers (libjpeg's default):
+    # the scan is cut into pieces decoded speculatively in parallel and
+    # stitched by one exact pass.  The same frame saved WITH restart markers
+    # (the same coefficients, decoded interval by interval) must come out
+    # bit-identical, and both agree with libjpeg
+    rng = np.random.default_rng(shape[0])
+    img = np.clip(128 + rng.normal(0, 50, shape), 0, 255).astype(np.uint8)
+    if shape[2] == 1:
+        img = img[..., 0]
+    kw = {"subsampling": subsampling} if shape[2] == 3 else {}
+    plain = _pil_encode(img, quality=90, **kw)
+    marked = _pil_encode(img, quality=90, restart_marker_rows=1, **kw)
+    assert len(plain) > (1 << 20) and b"\xff\xdd" not in plain and b"\xff\xdd" in marked
+    ours = C.decode_jpeg(plain)
+    assert np.array_equal(ours, C.decode_jpeg(marked))
+    d = np.abs(ours.astype(int) - _pil_decode(plain, shape[2] == 1).astype(int))
+    assert d.max() <= 3 and d.mean() < 0.1
+    # truncated: the rows before the cut decode as in the whole file
+    part = C.decode_jpeg(plain[: len(plain) * 3 // 5])
+    rows = shape[0] // 3
+    assert part.shape == ours.shape and np.array_equal(part[:rows], ours[:rows])

@@ -122,7 +122,12 @@ def test_asan_jpeg_decoder_fuzz(tmp_path):
                       + rng.normal(0, 12, (520, 600, 3)), 0, 255).astype(np.uint8)
         f = tmp_path / "prog_big.jpg"
         Image.fromarray(big).save(f, "JPEG", quality=85, progressive=True)
-        r = _run(str(exe), "40", str(f))
+        # > 1 MiB of sequential data without restart markers: the speculative
+        # parallel decode (pieces, resynchronisation, stitching)
+        noise = np.clip(128 + rng.normal(0, 50, (1200, 1400, 3)), 0, 255).astype(np.uint8)
+        g = tmp_path / "seq_big.jpg"
+        Image.fromarray(noise).save(g, "JPEG", quality=90)
+        r = _run(str(exe), "40", str(f), str(g))
         assert r.returncode == 0 and "jpeg fuzz:" in r.stdout, (r.stdout + r.stderr)[-3000:]
     assert "AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-3000:]
 
@@ -130,8 +135,8 @@ def test_asan_jpeg_decoder_fuzz(tmp_path):
 def test_tsan_jpeg_scan_pipeline(tmp_path):
     # the threaded paths of the JPEG decoder under ThreadSanitizer (host g++):
     # the row pipeline between progressive scans (progress counters, one thread
-    # per scan), restart intervals decoded in parallel, the parallel pixel
-    # stages; a few mutations too (a failing scan unwinds the ones waiting on it)
+    # per scan), restart intervals decoded in parallel, the speculative pieces
+    # of a long sequential scan, the parallel pixel stages; a few mutations too (a failing scan unwinds the ones waiting on it)
     import shutil
 
     if not shutil.which("g++"):
@@ -155,6 +160,11 @@ def test_tsan_jpeg_scan_pipeline(tmp_path):
         f = tmp_path / f"p{k}.jpg"
         Image.fromarray(img).save(f, "JPEG", quality=85, progressive=True, **kw)
         seeds.append(str(f))
+    # and the speculative parallel decode of a long sequential scan
+    noise = np.clip(128 + rng.normal(0, 50, (1200, 1400, 3)), 0, 255).astype(np.uint8)
+    f = tmp_path / "seq.jpg"
+    Image.fromarray(noise).save(f, "JPEG", quality=90)
+    seeds.append(str(f))
     env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1:exitcode=66", HIP_VISIBLE_DEVICES="")
     r = subprocess.run([str(exe), "6", *seeds], capture_output=True, text=True, timeout=600, env=env)
     assert "ThreadSanitizer" not in r.stderr, r.stderr[-4000:]
