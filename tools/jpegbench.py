@@ -79,12 +79,29 @@ def main():
             f = os.path.join(td, "p.jpg")
             Image.fromarray(img).save(f, "JPEG", quality=a.quality, progressive=True)
             prog = open(f, "rb").read()
+            # libjpeg's own sequential save: no restart markers, so the native
+            # decoder's speculative parallel entropy stage is what runs
+            Image.fromarray(img).save(f, "JPEG", quality=a.quality)
+            lib = open(f, "rb").read()
 
         def dev_decode_prog():
             jc = C.jpeg_entropy_decode(prog)
             jc.to_device(out.data_ptr(), n * 3, stream)
             torch.cuda.synchronize()
 
+        def dev_decode_lib():
+            jc = C.jpeg_entropy_decode(lib)
+            jc.to_device(out.data_ptr(), n * 3, stream)
+            torch.cuda.synchronize()
+
+        rec["libjpeg_sequential"] = {
+            "jpeg_bytes": len(lib),
+            "decode_ms": {"host": best(lambda: C.decode_jpeg(lib)),
+                          "entropy_only": best(lambda: C.jpeg_entropy_decode(lib)),
+                          "entropy_host_pixels_gpu": best(dev_decode_lib),
+                          "pillow": best(lambda: np.asarray(Image.open(io.BytesIO(lib)).convert("RGB")))},
+            "host_vs_pillow_max_diff": int(np.abs(C.decode_jpeg(lib).astype(int)
+                                                  - np.asarray(Image.open(io.BytesIO(lib)).convert("RGB")).astype(int)).max())}
         ref = np.asarray(Image.open(io.BytesIO(prog)).convert("RGB"))
         rec["progressive"] = {
             "jpeg_bytes": len(prog),
