@@ -2,7 +2,7 @@
 # Round-end validation on one MI355X: the GPU suite, smoke(), the driver's
 # bench command, the stream-copy ceiling (membench) and the 8K JPEG bench.
 set -o pipefail
-O=gpurun_out/r4/final6
+O=gpurun_out/r4/final7
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/gpu_suite.txt 2>&1 || exit 1
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.txt 2>&1 || exit 1
