@@ -37,6 +37,8 @@ def test_config1_gray_512(tmp_path):
     r = run("run", "--input", src, "--output", out, "--chain", "gray", "--backend", "host", "--ranks", "1")
     rec = json.loads(r.stdout.strip().splitlines()[-1])
     assert rec["ranks"] == 1 and rec["backend"] == "host"
+    # the file stages around the run are timed too
+    assert rec["read_ms"] >= 0 and rec["write_ms"] >= 0 and rec["wall_ms"] > 0
     g = utils.read_image(out)
     assert g.shape == (512, 512) and (g == np_ref.gray_bt601(img)).all()
     assert out.read_bytes().startswith(b"P5\n512 512\n255\n")
