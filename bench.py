@@ -22,8 +22,10 @@ the cache, not HBM; the headline then steps round-robin over F independent
 frames (F engines, each its own stripe pair; consecutive frames may alternate
 over two streams) with F x working set > 2 x 256 MiB, so every step reads data
 evicted long before -- a stream of distinct frames, the way a video-rate
-workload sees the GPUs.  Stripes too big for the cache (N = 2, 4) get two
-frames, so one frame's exchange can run beside the other's filter.  The
+workload sees the GPUs.  Stripes too big for the cache (N = 1, 2, 4) get two
+frames, so one frame's kernel boundary (and exchange) can run beside the
+other's filter.  The rule and the 1-vs-2-stream probe are the same at every N,
+N = 1 included, so a 1 -> N curve compares one execution mode.  The
 warm single-frame number (resident_warm) and the communication-avoiding deep
 halo (resident_deep: k*2 rows exchanged once per k steps, bit-identical) are
 reported beside it as named scopes, never as `value`.
@@ -247,6 +249,18 @@ def main():
     part, active = C.plan_rows(H, world, R)
     max_rows = max(r for _, r in part)
 
+    # ---- transport check (untimed): the headline's halo messages (R rows of
+    # a stripe each way) around the ring through this run's communicator, in
+    # the frame-stream pattern (4 frames over 2 streams), every word verified;
+    # at N = 1 the RCCL communicator sends to and receives from itself ----
+    transport = None
+    if ctx.comm is not None and ctx.device:
+        transport = dict(parallel.ring_check(ctx, 4 * (-(-R * W * Cc // 4)), frames=4, streams=2, iters=200),
+                         peers="self (loopback)" if world == 1 else "ring r -> r+1")
+        transport["errors"] = int(max_over_ranks(float(transport["errors"])))
+        if transport["errors"]:
+            log.error("transport check: %d corrupted words", transport["errors"])
+
     # ---- headline: a FrameStream (halo exchanged every step; when a stripe
     # fits the Infinity Cache, round-robin over enough frames that every step
     # reads HBM-cold data; consecutive frames on alternating streams) ----
@@ -264,16 +278,18 @@ def main():
     fs.tune()
     # which halo schedule is fastest depends on the link and the transport's
     # per-exchange cost: at N>1 measure them here, untimed, on every rank
-    if world == 1:
-        sched = {"chosen": "none", "ms": {}, "requested": a.halo_schedule}  # no exchange
-    elif a.no_overlap:
+    # (N = 1 exchanges nothing, but runs the same frames x streams probe, so
+    # every N of a scaling curve is measured in the same execution mode)
+    if a.no_overlap and world > 1:
         fs.set_schedule("serial")
         sched = {"chosen": fs.schedule, "ms": {}, "requested": "serial"}
-    elif a.halo_schedule != "auto":
+    elif a.halo_schedule != "auto" and world > 1:
         fs.set_schedule(a.halo_schedule)
         sched = {"chosen": fs.schedule, "ms": {}, "requested": a.halo_schedule}
     else:
         sched = dict(fs.pick_schedule(max_over_ranks, barrier), requested="auto")
+        if world == 1:
+            sched["chosen"] = "none (one rank: no exchange)"
     nstreams = fs.nstreams  # the probe may have settled on one stream
     log.info("halo schedule: %s on %d stream(s) %s", sched["chosen"], nstreams, sched["ms"])
     step = fs.step
@@ -316,8 +332,12 @@ def main():
         sync_frames()
         sync()
         # with s streams consecutive steps overlap: a step's time is the span
-        # of s consecutive steps divided by s (s = 1: the plain delta)
-        w = nstreams
+        # between two events on the SAME stream divided by the steps between
+        # them.  Step i runs on stream (i mod F) mod s, so i and i + s share a
+        # stream when s divides the frame count F; otherwise i and i + F do
+        # (s = 1: the plain delta)
+        w = nstreams if nframes % nstreams == 0 else nframes
+        assert all(frame_stream(i) is frame_stream(i + w) for i in range(n_ev - w + 1))
         step_ms = stats([ev[i].elapsed_time(ev[i + w]) / w for i in range(n_ev - w + 1)])
     # device-event stage times of one step of frame 0 on rank 0
     dp.engine.stage_timing = True
@@ -359,30 +379,22 @@ def main():
             ok &= same(out[0:reach], ref[2 * reach:3 * reach])
         verify = all_ok(ok)
 
-    # ---- same-box roofline: a device copy of the same bytes per step ----
+    # ---- same-box roofline: the framework's hand-written linear copy of the
+    # same bytes per step (csrc/hip/pointwise.hip k_copy_linear: one 16-byte
+    # chunk per lane, the faster of two store policies), rotating over enough
+    # buffer pairs that every copy reads cache-cold data, like the headline ----
     bytes_in = rows * W * pinfo["cin"]
     bytes_out = rows * W * pinfo["cout"]
     step_bytes = bytes_in + bytes_out
-    copy_ms = None
+    copy = None
     if dev and rows > 0:
         n = step_bytes // 2
-        src = torch.empty(n, dtype=torch.uint8, device="cuda").random_(0, 256)
-        dst = torch.empty_like(src)
-        for _ in range(3):
-            dst.copy_(src)
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(21)]
-        ev[0].record()
-        for i in range(20):
-            dst.copy_(src)
-            ev[i + 1].record()
-        ev[-1].synchronize()
-        copy_ms = sorted(ev[i].elapsed_time(ev[i + 1]) for i in range(20))[10]
-        del src, dst
+        copy = C.copy_roofline(ctx.gpu, n, max(1, -(-3 * MALL_BYTES // (2 * n))), 20)
         torch.cuda.empty_cache()
+    copy_ms = copy["event_ms"] if copy else None
 
     scopes = {"resident": {"mpx_s": round(mpx, 1), "ms": round(ms_per_step, 5), "verified": verify,
-                           "frames": nframes, "streams": nstreams, "halo_depth": 1, "cache": "cold" if cold else (
-                               "exceeds the Infinity Cache" if not fits_mall else "warm")}}
+                           "frames": nframes, "streams": nstreams, "halo_depth": 1, "cache": fs.cache}}
     med = step_ms["median"] if step_ms else None
     rec = {
         "metric": METRIC,
@@ -411,20 +423,27 @@ def main():
         },
         "verified_vs_golden": verify,
         # rank 0's per-step device time (HIP events between steps) and the
-        # same-box copy of the same per-GPU bytes (read + write)
+        # same-box hand-written copy of the same per-GPU bytes (read + write):
+        # per copy (events between copies, vs step_ms_device) and back to back
+        # (burst, vs the host-clock ms_per_step)
         "step_ms_device": step_ms,
         "bytes_per_step_per_gpu": step_bytes,
         "copy_roofline_ms": None if copy_ms is None else round(copy_ms, 5),
         "frac_of_copy_roofline": None if not (copy_ms and med) else round(copy_ms / med, 4),
+        "copy_burst_ms": None if not copy else round(copy["burst_ms"], 5),
+        "frac_of_copy_burst": None if not copy else round(copy["burst_ms"] / ms_per_step, 4),
+        "copy_roofline": copy,
         "hbm_tb_s": None if not med else round(step_bytes / (med * 1e-3) / 1e12, 3),
         "working_set_fits_mall": fits_mall,
         "frames": nframes,
         "streams": nstreams,
         "scopes": scopes,
         "tuned": {"band_rows": dp.engine.bands, "occupancy_caps": dp.engine.caps, "policies": dp.engine.policies,
-                  "cold": cold},
+                  "cold": cold, "streaming_policy": fs.streaming},
+        "cache": fs.cache,
         "halo_depth": 1,
         "halo_schedule": sched,
+        "transport_check": transport,
         "stripe_rows": [r for _, r in part],
         "stage_ms_rank0": stages,
         "world": {"summary": parallel.identity_summary(ids), "ranks": ids},

@@ -12,9 +12,11 @@
 // paths agree to within one level (the device may fuse a multiply-add).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <mutex>
+#include <vector>
 
 #include "stripe/image.h"
 #include "stripe/kernels.h"
@@ -205,34 +207,78 @@ bool pin_uploads() {
 }
 }  // namespace
 
+namespace {
+// What jpeg_pixels_device holds while its work is queued: page-locked host
+// ranges and device buffers.  On the normal path the function releases them
+// itself; if anything throws on the way (an allocation, a copy, a launch), the
+// destructor waits for the stream (copies from registered pages may still be
+// in flight) and then unregisters and frees everything, so no registration
+// outlives the host memory it covers and no device buffer leaks.
+struct JpegStaging {
+  hipStream_t s;
+  std::vector<void*> pinned;    // hipHostRegister'ed host ranges
+  std::vector<void*> device;    // hipMallocAsync'ed buffers not yet freed
+  bool released = false;
+  explicit JpegStaging(hipStream_t st) : s(st) {}
+  void* alloc(size_t bytes) {
+    void* p = nullptr;
+    HIP_CHECK(hipMallocAsync(&p, bytes, s));
+    device.push_back(p);
+    return p;
+  }
+  void free_async(void* p) {
+    HIP_CHECK(hipFreeAsync(p, s));
+    device.erase(std::find(device.begin(), device.end(), p));
+  }
+  // normal path: queue the frees, then (registered pages only) wait for the
+  // copies out of them before unregistering
+  void release() {
+    for (void* p : device) HIP_CHECK(hipFreeAsync(p, s));
+    device.clear();
+    if (!pinned.empty()) {
+      HIP_CHECK(hipStreamSynchronize(s));
+      for (void* hp : pinned) (void)hipHostUnregister(hp);
+      pinned.clear();
+    }
+    released = true;
+  }
+  ~JpegStaging() {
+    if (released) return;
+    (void)hipStreamSynchronize(s);
+    for (void* p : device) (void)hipFree(p);
+    for (void* hp : pinned) (void)hipHostUnregister(hp);
+    (void)hipGetLastError();  // the error being thrown is the one to report
+  }
+};
+}  // namespace
+
 void jpeg_pixels_device(const JpegCoefs& jc, uint8_t* dst, int64_t pitch, hipStream_t s) {
   const int nc = (int)jc.comps.size();
-  // large coefficient planes are page-locked for the upload (a pageable copy
-  // is staged through the runtime's bounce buffers at a fraction of the link
-  // rate); they are unregistered once the copies have run
-  std::vector<void*> pinned;
   STRIPE_CHECK(nc == 1 || nc == 3, "JPEG: 1 or 3 components");
   STRIPE_CHECK(pitch >= (int64_t)jc.W * nc, "JPEG: destination pitch " << pitch << " < row bytes " << jc.W * nc);
   upload_jpeg_constants();
+  // large coefficient planes are page-locked for the upload (a pageable copy
+  // is staged through the runtime's bounce buffers at a fraction of the link
+  // rate); they are unregistered once the copies have run
+  JpegStaging st(s);
   std::vector<uint8_t*> planes((size_t)nc, nullptr);
   dev::JpegPlaneRef ref[3] = {};
   for (int ci = 0; ci < nc; ++ci) {
     const JpegCoefs::Comp& c = jc.comps[(size_t)ci];
     const int64_t nb = (int64_t)c.bw * c.bh, ps = (int64_t)c.bw * 8;
     STRIPE_CHECK(c.coef.size() == (size_t)nb * 64, "JPEG: coefficient plane size");
-    int16_t* dcoef = nullptr;
-    HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&dcoef), (size_t)nb * 64 * sizeof(int16_t), s));
-    HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&planes[(size_t)ci]), (size_t)ps * c.bh * 8, s));
     const size_t cbytes = (size_t)nb * 64 * sizeof(int16_t);
+    auto* dcoef = static_cast<int16_t*>(st.alloc(cbytes));
+    planes[(size_t)ci] = static_cast<uint8_t*>(st.alloc((size_t)ps * c.bh * 8));
     if (pin_uploads() && cbytes >= ((size_t)8 << 20)) {
       void* hp = const_cast<int16_t*>(c.coef.data());
-      if (hipHostRegister(hp, cbytes, hipHostRegisterDefault) == hipSuccess) pinned.push_back(hp);
+      if (hipHostRegister(hp, cbytes, hipHostRegisterDefault) == hipSuccess) st.pinned.push_back(hp);
       else (void)hipGetLastError();  // not registrable: the pageable copy below still works
     }
     HIP_CHECK(hipMemcpyAsync(dcoef, c.coef.data(), cbytes, hipMemcpyHostToDevice, s));
     dev::k_jpeg_idct<<<blocks_for(nb, 4), 256, 0, s>>>(dcoef, nb, c.bw, planes[(size_t)ci], ps);
     HIP_CHECK(hipGetLastError());
-    HIP_CHECK(hipFreeAsync(dcoef, s));
+    st.free_async(dcoef);
     ref[ci] = {planes[(size_t)ci], ps, (jc.W * c.h + jc.hmax - 1) / jc.hmax, (jc.H * c.v + jc.vmax - 1) / jc.vmax,
                jc.hmax / c.h, jc.vmax / c.v};
   }
@@ -240,11 +286,7 @@ void jpeg_pixels_device(const JpegCoefs& jc, uint8_t* dst, int64_t pitch, hipStr
   dev::k_jpeg_color<<<blocks_for(npx, 256), 256, 0, s>>>(ref[0], ref[nc == 3 ? 1 : 0], ref[nc == 3 ? 2 : 0], nc,
                                                           jc.rgb, jc.W, jc.H, dst, pitch);
   HIP_CHECK(hipGetLastError());
-  for (uint8_t* p : planes) HIP_CHECK(hipFreeAsync(p, s));
-  if (!pinned.empty()) {
-    HIP_CHECK(hipStreamSynchronize(s));  // the copies from the registered pages are done
-    for (void* hp : pinned) (void)hipHostUnregister(hp);
-  }
+  st.release();
 }
 
 JpegQuant jpeg_quantise_device(const uint8_t* src, int64_t pitch, int W, int H, int C, int quality, bool subsample,

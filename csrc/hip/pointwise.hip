@@ -7,7 +7,9 @@
 // per-channel truncation, kernel.cu:40-42, is reproduced with verified
 // multiply-shift constants).  Margins are processed like pixels, so the output
 // keeps the x-border contract of the next stencil.
+#include <algorithm>
 #include <cstdlib>
+#include <vector>
 
 #include "dev_common.h"
 #include "stripe/image.h"
@@ -211,7 +213,122 @@ __global__ __launch_bounds__(kNT) void k_copy_rows(uint8_t* dst, int64_t dpitch,
   }
 }
 
+// Linear device copy, the same-box streaming floor the benchmark record quotes
+// beside its headline: one 16-byte chunk per lane, one chunk per thread, a
+// grid of n/4096 workgroups that the dispatcher refills (on MI355X this beat
+// every grid-stride / persistent shape: 0.2521 ms for 768 MiB = 6.39 TB/s,
+// profiles/r4/final/late/membench_768m.txt); nt loads, store policy SAUX.
+template <int SAUX>
+__global__ __launch_bounds__(kNT) void k_copy_linear(const uint8_t* in, uint8_t* out, uint32_t bytes) {
+  const __amdgpu_buffer_rsrc_t ri = make_rsrc(in, bytes);
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(out, bytes);
+  typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+  const uint32_t off = ((uint32_t)blockIdx.x * kNT + threadIdx.x) * 16u;  // past `bytes`: masked by the range check
+  const u32x4v v = __builtin_amdgcn_raw_buffer_load_b128(ri, off, 0, 2);
+  __builtin_amdgcn_raw_buffer_store_b128(v, ro, off, 0, SAUX);
+}
+
+// Transport check pattern (comm_ring_check): word j of a message tagged `tag`
+// is pattern_word(tag, j); fill writes it, check counts the words that differ.
+__global__ __launch_bounds__(kNT) void k_pattern_fill(uint32_t* p, int64_t words, uint32_t tag) {
+  for (int64_t j = (int64_t)blockIdx.x * kNT + threadIdx.x; j < words; j += (int64_t)gridDim.x * kNT)
+    p[j] = pattern_word(tag, (uint64_t)j);
+}
+
+__global__ __launch_bounds__(kNT) void k_pattern_check(const uint32_t* p, int64_t words, uint32_t tag,
+                                                       unsigned long long* errors) {
+  unsigned bad = 0;
+  for (int64_t j = (int64_t)blockIdx.x * kNT + threadIdx.x; j < words; j += (int64_t)gridDim.x * kNT)
+    bad += p[j] != pattern_word(tag, (uint64_t)j);
+  if (bad) atomicAdd(errors, (unsigned long long)bad);
+}
+
 }  // namespace dev
+
+void launch_pattern_fill(void* p, int64_t bytes, uint32_t tag, hipStream_t s) {
+  const int64_t words = bytes / 4;
+  const unsigned g = (unsigned)std::min<int64_t>(std::max<int64_t>(1, div_up(words, dev::kNT)), 4096);
+  dev::k_pattern_fill<<<g, dev::kNT, 0, s>>>(static_cast<uint32_t*>(p), words, tag);
+  HIP_CHECK(hipGetLastError());
+}
+
+void launch_pattern_check(const void* p, int64_t bytes, uint32_t tag, unsigned long long* errors, hipStream_t s) {
+  const int64_t words = bytes / 4;
+  const unsigned g = (unsigned)std::min<int64_t>(std::max<int64_t>(1, div_up(words, dev::kNT)), 4096);
+  dev::k_pattern_check<<<g, dev::kNT, 0, s>>>(static_cast<const uint32_t*>(p), words, tag, errors);
+  HIP_CHECK(hipGetLastError());
+}
+
+CopyRoofline copy_roofline(int device, int64_t bytes, int frames, int reps) {
+  STRIPE_CHECK(bytes > 0 && bytes < (int64_t)dev::kOOB, "copy roofline: 0 < bytes < 2 GiB");
+  frames = std::max(1, frames);
+  reps = std::max(3, reps);
+  HIP_CHECK(hipSetDevice(device));
+  const int64_t n = align_up(bytes, 16);
+  std::vector<uint8_t*> buf((size_t)2 * frames, nullptr);
+  hipStream_t s = nullptr;
+  std::vector<hipEvent_t> ev((size_t)reps + 1, nullptr);
+  CopyRoofline r;
+  auto cleanup = [&]() {
+    if (s) (void)hipStreamSynchronize(s);
+    for (auto* p : buf)
+      if (p) (void)hipFree(p);
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e);
+    if (s) (void)hipStreamDestroy(s);
+  };
+  try {
+    for (auto*& p : buf) {
+      HIP_CHECK(hipMalloc(&p, (size_t)n));
+      HIP_CHECK(hipMemsetAsync(p, 0x5A, (size_t)n, nullptr));
+    }
+    HIP_CHECK(hipDeviceSynchronize());
+    HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
+    const unsigned blocks = (unsigned)div_up(n, 16 * dev::kNT);
+    r.bytes = n;
+    r.frames = frames;
+    for (int policy : {0, 16}) {  // default stores; sc1 (write-through) stores
+      auto launch = [&](int i) {
+        const int f = i % frames;
+        if (policy == 0) dev::k_copy_linear<0><<<blocks, dev::kNT, 0, s>>>(buf[2 * f], buf[2 * f + 1], (uint32_t)n);
+        else dev::k_copy_linear<16><<<blocks, dev::kNT, 0, s>>>(buf[2 * f], buf[2 * f + 1], (uint32_t)n);
+      };
+      for (int i = 0; i < 2 * frames + 2; ++i) launch(i);
+      HIP_CHECK(hipGetLastError());
+      // per-copy device time: an event between consecutive copies
+      HIP_CHECK(hipEventRecord(ev[0], s));
+      for (int i = 0; i < reps; ++i) {
+        launch(i);
+        HIP_CHECK(hipEventRecord(ev[(size_t)i + 1], s));
+      }
+      HIP_CHECK(hipEventSynchronize(ev[(size_t)reps]));
+      std::vector<float> t((size_t)reps);
+      for (int i = 0; i < reps; ++i) HIP_CHECK(hipEventElapsedTime(&t[(size_t)i], ev[(size_t)i], ev[(size_t)i + 1]));
+      std::sort(t.begin(), t.end());
+      const double med = t[t.size() / 2];
+      // back-to-back copies, events at the two ends only (what a host clock
+      // around a burst of steps sees)
+      HIP_CHECK(hipEventRecord(ev[0], s));
+      for (int i = 0; i < reps; ++i) launch(i);
+      HIP_CHECK(hipEventRecord(ev[1], s));
+      HIP_CHECK(hipEventSynchronize(ev[1]));
+      float burst = 0;
+      HIP_CHECK(hipEventElapsedTime(&burst, ev[0], ev[1]));
+      const double bm = burst / reps;
+      if (r.event_ms <= 0 || med < r.event_ms) {
+        r.event_ms = med;
+        r.policy = policy;
+      }
+      if (r.burst_ms <= 0 || bm < r.burst_ms) r.burst_ms = bm;
+    }
+  } catch (...) {
+    cleanup();
+    throw;
+  }
+  cleanup();
+  return r;
+}
 
 void launch_copy_rows(uint8_t* dst, int64_t dpitch, const uint8_t* src, int64_t spitch, int64_t E, int rows,
                       hipStream_t s) {

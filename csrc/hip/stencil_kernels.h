@@ -61,20 +61,80 @@ struct WaveTask {
   bool valid;
 };
 
-__device__ __forceinline__ WaveTask wave_task(const KArgs& a) {
+// Row range of band `by` of a persistent launch: range 0 in `band`-row bands
+// down to tail_y, then tail_band-row bands (KArgs::tail_y); range 1 as usual.
+__device__ __forceinline__ void band_range_tail(const KArgs& a, int by, int& ys, int& ye) {
+  if (by < a.nbig) {
+    ys = a.ry0 + by * a.band;
+    ye = min(ys + a.band, a.tail_y);
+  } else if (by < a.nb0) {
+    ys = a.tail_y + (by - a.nbig) * a.tail_band;
+    ye = min(ys + a.tail_band, a.ry1);
+  } else {
+    ys = a.ry2 + (by - a.nb0) * a.band;
+    ye = min(ys + a.band, a.ry3);
+  }
+}
+
+// Task w of a pass: tile column w mod ntx of band w / ntx (band-major).
+template <bool TAIL = false>
+__device__ __forceinline__ WaveTask task_at(const KArgs& a, int w) {
   WaveTask t;
   t.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   t.lane = threadIdx.x & 63;
-  const int w = xcd_remap((int)blockIdx.x, (int)gridDim.x, a.nxcd) * kWaves + t.wave;
   t.xt = w % a.ntx;
   const int bt = w / a.ntx;
   t.valid = bt < a.nbands;
   t.ys = t.ye = 0;
   if (t.valid) {
-    band_range(a, bt, t.ys, t.ye);
+    if constexpr (TAIL) band_range_tail(a, bt, t.ys, t.ye);
+    else band_range(a, bt, t.ys, t.ye);
     t.valid = t.ys < t.ye;
   }
   return t;
+}
+
+// The task of this wave in a one-task-per-wave launch (XCD-aware workgroup order).
+__device__ __forceinline__ WaveTask wave_task(const KArgs& a) {
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  return task_at(a, xcd_remap((int)blockIdx.x, (int)gridDim.x, a.nxcd) * kWaves + wave);
+}
+
+// Work queue of persistent launches (KArgs::queue, kQueueWords dwords).
+//   * round 0 is static: wave w of the grid takes task w (no claim);
+//   * the remaining tasks form kQueueShards classes (task - nwaves mod 8), each
+//     with its own head counter on its own 128-byte line, drained by the
+//     workgroups with blockIdx % 8 == class (on MI355X those share an XCD).
+//     One counter serves ~88 claims / us (MI355X_MICROARCH.md, row dequeue):
+//     a single head for all 2048 waves made a 40 us pass take 150 us;
+//   * a wave claims its next task (one lane, a device-scope atomic with
+//     return) before streaming the current one, so the claim's latency hides
+//     under the task and the index is read only at the end;
+//   * the workgroups of a class arrive on the class's counter after their last
+//     (failed) claim; the last to arrive resets the class's head and counter
+//     for the next launch on this queue (stream order publishes the reset).
+// Correct for any workgroup placement and residency: every class has >= 1
+// workgroup (grid >= kQueueShards, launch side) and each one drains its class.
+constexpr int kQueueShards = 8;
+constexpr int kQueueLine = 32;                          // dwords per 128-byte line
+constexpr int kQueueWords = 2 * kQueueShards * kQueueLine;  // heads, then arrival counters
+
+__device__ __forceinline__ uint32_t queue_claim_async(uint32_t* head) {
+  uint32_t v = 0;
+  if ((threadIdx.x & 63) == 0) v = atomicAdd(head, 1u);
+  return v;  // lane 0's VGPR; read with readfirstlane once needed
+}
+
+__device__ __forceinline__ void queue_retire(uint32_t* q, int shard) {
+  __syncthreads();  // every wave of the workgroup has made its last claim
+  if (threadIdx.x == 0) {
+    const uint32_t members = (gridDim.x - (uint32_t)shard + kQueueShards - 1) / kQueueShards;
+    uint32_t* arrived = q + (kQueueShards + shard) * kQueueLine;
+    if (atomicAdd(arrived, 1u) == members - 1u) {
+      atomicExch(q + shard * kQueueLine, 0u);
+      atomicExch(arrived, 0u);
+    }
+  }
 }
 
 enum { PRO_NONE = 0, PRO_LUT = 1, PRO_GRAY = 2, PRO_GRAYLUT = 3 };
@@ -476,24 +536,15 @@ __device__ __forceinline__ void dpp_window(const uint32_t (&v)[8], uint32_t (&w)
   }
 }
 
-// (skip border + expand epilogue, a rare combination: 2 VGPRs over the 128 of
-// 4 waves/SIMD with the gray prologue -> 3 waves rather than a scratch spill)
-template <int C, class F, int PRO, bool SKIP, int SAUX, bool EXP = false>
-__global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : (SKIP && EXP ? 3 : 4))) void k_sep(KArgs a) {
+// One wave task (a band of rows of one tile column) of a separable filter.
+template <int C, class F, int PRO, bool SKIP, int SAUX, bool EXP>
+__device__ __forceinline__ void sep_task(const KArgs& a, const WaveTask& t, const uint8_t* luts, uint4* xb) {
   static_assert(!EXP || C == 1, "expand epilogue needs a 1-channel stencil");
   constexpr int R = F::R, K = F::K;
   constexpr int WLO = (R * C <= 8) ? 8 : 16;  // u16 window start (relative to chunk)
   constexpr int WDW = (2 * WLO + 16) / 2;     // window dwords
   constexpr int CIN = is_gray(PRO) ? 3 : 1;  // input bytes per output byte
   using T = SepTraits<F>;
-  __shared__ __attribute__((aligned(16))) uint4 xbuf[EXP ? kWaves : 1][EXP ? 3 * kW : 1];
-  __shared__ uint8_t luts[768];
-  if (PRO != PRO_NONE || a.has_epi) {
-    load_luts<PRO>(a, luts);
-    __syncthreads();
-  }
-  const WaveTask t = wave_task(a);
-  if (!t.valid) return;
   const int lane = t.lane;
   const int ys = t.ys, ye = t.ye;
   const int cb = t.xt * (kOutChunks * 16) - 16 + lane * 16;
@@ -502,7 +553,6 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : (SKIP && EXP ? 3 : 4))) void 
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);
   const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
   const uint32_t last_row = in_row_off(a, ye - 1 + R);
-  uint4* xb = xbuf[EXP ? t.wave : 0];
   // @skip: the prologue bytes of the last 4 input rows (slot (r - ys) mod 4),
   // so an output row's centre bytes come from registers, not a second load
   constexpr int kRing = SKIP ? 4 : 1;
@@ -678,6 +728,53 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : (SKIP && EXP ? 3 : 4))) void 
   band_margins<C, EXP ? 3 : C>(a, t);
 }
 
+// Separable filter kernel.  MODE (KMode) picks how waves get their tasks:
+//   kOneTask   one band of one tile column per wave (the hardware dispatcher
+//              refills the CUs as workgroups retire);
+//   kTailBands the same, but range 0 ends in short bands (KArgs::tail_y):
+//              the workgroups dispatched last carry the short tasks, so the
+//              launch's tail is one short task long;
+//   kQueue     a grid of the resident workgroups claiming tasks from the work
+//              queue (KArgs::queue) until none is left.
+// STAMP: the per-wave timeline of KArgs::stamps (diagnostic instances,
+// tools/sepx.hip).  Both are compile-time, so the one-task instances carry
+// neither the loop nor the stamp code.
+// (skip border + expand epilogue, a rare combination: 2 VGPRs over the 128 of
+// 4 waves/SIMD with the gray prologue -> 3 waves rather than a scratch spill)
+enum KMode { kOneTask = 0, kTailBands = 1, kQueue = 2 };
+template <int C, class F, int PRO, bool SKIP, int SAUX, bool EXP = false, int MODE = kOneTask, bool STAMP = false>
+__global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : (SKIP && EXP ? 3 : 4))) void k_sep(KArgs a) {
+  constexpr bool PERSIST = MODE == kQueue;
+  const uint32_t t_start = STAMP ? stamp_now() : 0u;
+  __shared__ __attribute__((aligned(16))) uint4 xbuf[EXP ? kWaves : 1][EXP ? 3 * kW : 1];
+  __shared__ uint8_t luts[768];
+  if (PRO != PRO_NONE || a.has_epi) {
+    load_luts<PRO>(a, luts);
+    __syncthreads();
+  }
+  if constexpr (PERSIST) {
+    const int nw = (int)gridDim.x * kWaves;
+    const int shard = (int)(blockIdx.x % kQueueShards);
+    uint32_t* head = a.queue + shard * kQueueLine;
+    int task = (int)blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // static round 0
+    while (task < a.persist_tasks) {
+      const uint32_t next = queue_claim_async(head);  // in flight while this task streams
+      const WaveTask t = task_at<true>(a, task);
+      if (t.valid) sep_task<C, F, PRO, SKIP, SAUX, EXP>(a, t, luts, xbuf[EXP ? t.wave : 0]);
+      task = nw + kQueueShards * (int)__builtin_amdgcn_readfirstlane(next) + shard;
+    }
+    queue_retire(a.queue, shard);
+  } else if constexpr (MODE == kTailBands) {
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const WaveTask t = task_at<true>(a, xcd_remap((int)blockIdx.x, (int)gridDim.x, a.nxcd) * kWaves + wave);
+    if (t.valid) sep_task<C, F, PRO, SKIP, SAUX, EXP>(a, t, luts, xbuf[EXP ? t.wave : 0]);
+  } else {
+    const WaveTask t = wave_task(a);
+    if (t.valid) sep_task<C, F, PRO, SKIP, SAUX, EXP>(a, t, luts, xbuf[EXP ? t.wave : 0]);
+  }
+  if constexpr (STAMP) stamp_wave(a.stamps, (int)blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), t_start);
+}
+
 // ------------------------------------------------------------------------------
 // Direct (non-separable) filters: emboss3/5, sharpen, laplace
 // ------------------------------------------------------------------------------
@@ -834,6 +931,53 @@ inline void plan_bands(KArgs& a, dim3& grid, int tiles, int n0, int n1, int band
   a.nbands = a.nb0 + (int)div_up(n1, band);
   a.ntx = tiles;
   grid = dim3((unsigned)div_up((int64_t)tiles * a.nbands, kWaves));
+}
+
+// Persistent launch geometry (after plan_bands): a grid of the resident
+// workgroups of `fn` at dynamic LDS `dyn` (the occupancy cap), and range 0's
+// last rows re-cut into tail_band-row bands, one tail task per resident wave,
+// so the tasks claimed last are short (tail_band <= 0 or >= band: no tail).
+inline int resident_wgs(const void* fn, size_t dyn) {
+  int per_cu = 0, cus = 0, dev = 0;
+  HIP_CHECK(hipGetDevice(&dev));
+  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kNT, dyn));
+  HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  return std::max(1, per_cu) * std::max(1, cus);
+}
+
+// Re-cut range 0's last rows into tail_band-row bands, one tail task per
+// resident wave (`waves`), and recount the bands (KArgs::tail_y; kTailBands /
+// kQueue kernels).  tail_band <= 0 or >= band: no tail.
+inline void set_tail_bands(KArgs& a, int tail_band, int waves) {
+  const int n0 = a.ry1 - a.ry0;
+  const int n1 = a.ry3 - a.ry2;
+  int tail_rows = 0;
+  if (tail_band > 0 && tail_band < a.band) {
+    tail_rows = (int)std::min<int64_t>(div_up((int64_t)waves, a.ntx) * tail_band, n0 / 2);
+    tail_rows -= tail_rows % tail_band;
+  }
+  a.tail_band = tail_rows > 0 ? tail_band : a.band;
+  a.tail_y = a.ry1 - tail_rows;
+  a.nbig = (int)div_up(a.tail_y - a.ry0, a.band);
+  a.nb0 = a.nbig + (int)div_up(tail_rows, a.tail_band);
+  a.nbands = a.nb0 + (int)div_up(n1, a.band);
+}
+
+// One-task launch with tail bands (kTailBands): the grid covers every task.
+inline void plan_tail(KArgs& a, dim3& grid, const void* fn, size_t dyn, int tail_band) {
+  set_tail_bands(a, tail_band, resident_wgs(fn, dyn) * kWaves);
+  grid = dim3((unsigned)div_up((int64_t)a.ntx * a.nbands, kWaves));
+}
+
+inline void plan_persistent(KArgs& a, dim3& grid, const void* fn, size_t dyn, int tail_band) {
+  const int wgs = resident_wgs(fn, dyn);
+  set_tail_bands(a, tail_band, wgs * kWaves);
+  a.persist_tasks = a.ntx * a.nbands;
+  a.nxcd = 0;
+  int64_t g = std::max<int64_t>(1, std::min<int64_t>(wgs, div_up(a.persist_tasks, kWaves)));
+  // tasks past round 0 are claimed per queue class: every class needs a workgroup
+  if (a.persist_tasks > g * kWaves) g = std::max<int64_t>(g, kQueueShards);
+  grid = dim3((unsigned)g);
 }
 
 // Occupancy cap of the HBM-streaming (nt-store) stencil launches: fewer

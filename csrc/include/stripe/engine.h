@@ -338,6 +338,19 @@ void broadcast_small(Comm* comm, void* host, size_t bytes, int root, int device)
 // direction), the same value on every rank; 0 for a one-rank communicator.
 double probe_link_rate(Comm* comm, int device, size_t bytes, int reps = 3);
 
+// Transport check in the FrameStream pattern: `iters` grouped send/recv
+// exchanges around the ring (rank r sends to r + 1, receives from r - 1; a
+// one-rank communicator sends to and receives from itself -- RCCL loopback),
+// frame i mod `frames` per exchange on stream (i mod frames) mod `streams`,
+// each message a fresh pattern tagged by (iteration, sender) and every word of
+// it verified on the device after its receive.
+struct RingCheck {
+  int64_t errors = 0;         // words that differed from the sender's pattern
+  int64_t bytes_checked = 0;  // bytes received and verified
+  double ms = 0;              // whole run (device events / host clock)
+};
+RingCheck comm_ring_check(Comm* comm, int device, size_t bytes, int frames, int streams, int iters);
+
 // Convenience driver: run the whole distributed pipeline on `world` in-process
 // ranks (local device backend or host backend), root -> scatter -> run -> gather.
 Image run_local_group(const EngineConfig& cfg, int world, const Image& input, int iterations,

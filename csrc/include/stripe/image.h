@@ -165,6 +165,16 @@ STRIPE_SYNTH_HD uint32_t synth_byte(uint64_t seed, int64_t y, int64_t b) {
   return (uint32_t)(z >> 24) & 0xFFu;
 }
 
+// Word j of a transport-check message tagged `tag` (comm_ring_check): host
+// and device compute the same value, so either side can fill or verify.
+STRIPE_SYNTH_HD uint32_t pattern_word(uint32_t tag, uint64_t j) {
+  uint64_t z = (uint64_t)tag * 0x9E3779B97F4A7C15ull + j * 0xD1B54A32D192ED03ull + 0x632BE59BD9B4E019ull;
+  z ^= z >> 31;
+  z *= 0xBF58476D1CE4E5B9ull;
+  z ^= z >> 29;
+  return (uint32_t)(z >> 16);
+}
+
 // rows [row0, row0 + rows) of a W x H x C synthetic frame, packed
 void synth_rows(uint64_t seed, int W, int C, int row0, int rows, uint8_t* dst);
 Image synth_image(uint64_t seed, int W, int H, int C);

@@ -84,6 +84,24 @@ void launch_fill_margins(uint8_t* origin, int64_t pitch, int W, int C, int y0, i
 void launch_copy_rows(uint8_t* dst, int64_t dpitch, const uint8_t* src, int64_t spitch, int64_t E, int rows,
                       hipStream_t s);
 
+// Same-box streaming floor: a hand-written linear device copy of `bytes`
+// (csrc/hip/pointwise.hip k_copy_linear) rotating over `frames` buffer pairs
+// (frames x 2 x bytes > 2 x 256 MiB: every copy reads cache-cold data), the
+// faster of two store policies.  event_ms: median device time of one copy
+// (events between copies); burst_ms: mean per copy of `reps` back-to-back.
+struct CopyRoofline {
+  double event_ms = 0, burst_ms = 0;
+  int64_t bytes = 0;
+  int frames = 0;
+  int policy = 0;  // store aux of the faster per-copy time (0 default, 16 write-through)
+};
+CopyRoofline copy_roofline(int device, int64_t bytes, int frames, int reps);
+
+// Transport check (comm_ring_check): fill `bytes` (a multiple of 4) with the
+// pattern of `tag` / add the number of differing words to *errors (device).
+void launch_pattern_fill(void* p, int64_t bytes, uint32_t tag, hipStream_t s);
+void launch_pattern_check(const void* p, int64_t bytes, uint32_t tag, unsigned long long* errors, hipStream_t s);
+
 // Synthetic pixels for local rows [0, rows) (global row0..), margins included.
 void launch_synth(uint8_t* origin, int64_t pitch, int W, int C, int row0, int rows, uint64_t seed,
                   int margin_px, Border b, hipStream_t s);

@@ -133,6 +133,7 @@ PYBIND11_MODULE(_C, m) {
     return image_to_numpy(img);
   });
   m.def("synth_byte", [](uint64_t seed, int64_t y, int64_t b) { return synth_byte(seed, y, b); });
+  m.def("pattern_word", [](uint32_t tag, uint64_t j) { return pattern_word(tag, j); });
 
   // ---- filter spec ----
   m.def("parse_chain", [](const std::string& s) { return chain_to_string(parse_chain(s)); },
@@ -307,6 +308,38 @@ PYBIND11_MODULE(_C, m) {
     py::gil_scoped_release nogil;
     return probe_link_rate(c->comm.get(), device, bytes, reps);
   }, py::arg("comm"), py::arg("device"), py::arg("bytes"), py::arg("reps") = 3);
+  // Transport check: ring send/recv (one rank: RCCL loopback) in the
+  // FrameStream pattern, every received word verified.
+  m.def("comm_ring_check", [](PyComm* c, int device, size_t bytes, int frames, int streams, int iters) {
+    STRIPE_CHECK(c != nullptr, "comm_ring_check needs a communicator");
+    RingCheck r;
+    {
+      py::gil_scoped_release nogil;
+      r = comm_ring_check(c->comm.get(), device, bytes, frames, streams, iters);
+    }
+    py::dict d;
+    d["errors"] = r.errors;
+    d["bytes_checked"] = r.bytes_checked;
+    d["ms"] = r.ms;
+    return d;
+  }, py::arg("comm"), py::arg("device"), py::arg("bytes"), py::arg("frames") = 4, py::arg("streams") = 2,
+     py::arg("iters") = 500);
+  // Same-box streaming floor of the benchmark record: hand-written linear copy
+  // of `bytes` rotating over `frames` buffer pairs (csrc/hip/pointwise.hip).
+  m.def("copy_roofline", [](int device, int64_t bytes, int frames, int reps) {
+    CopyRoofline r;
+    {
+      py::gil_scoped_release nogil;
+      r = copy_roofline(device, bytes, frames, reps);
+    }
+    py::dict d;
+    d["event_ms"] = r.event_ms;
+    d["burst_ms"] = r.burst_ms;
+    d["bytes"] = r.bytes;
+    d["frames"] = r.frames;
+    d["store_policy"] = r.policy == 0 ? "default" : "write-through (sc1)";
+    return d;
+  }, py::arg("device"), py::arg("bytes"), py::arg("frames") = 1, py::arg("reps") = 20);
   // Page-lock an existing host range (e.g. a shared-memory frame every rank
   // downloads its stripe into) so hipMemcpyAsync DMAs it without staging.
   m.def("host_register", [](uintptr_t p, size_t bytes) {

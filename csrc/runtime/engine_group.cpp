@@ -118,6 +118,93 @@ double probe_link_rate(Comm* comm, int device, size_t bytes, int reps) {
   return rate;
 }
 
+RingCheck comm_ring_check(Comm* comm, int device, size_t bytes, int frames, int streams, int iters) {
+  STRIPE_CHECK(comm != nullptr, "ring check needs a communicator");
+  STRIPE_CHECK(bytes >= 4 && bytes % 4 == 0, "ring check: bytes must be a positive multiple of 4");
+  STRIPE_CHECK(frames >= 1 && iters >= 1, "ring check: frames, iters >= 1");
+  streams = std::max(1, std::min(streams, frames));
+  const int world = comm->size(), rank = comm->rank();
+  const int to = (rank + 1) % world, from = (rank + world - 1) % world;  // world 1: both are this rank
+  // unique per (iteration, sender): a stale or misrouted message fails the check
+  auto tag = [](int i, int sender) { return (uint32_t)i * 131071u + (uint32_t)sender * 7919u + 1u; };
+  const bool dev = comm->device_buffers();
+  RingCheck res;
+  res.bytes_checked = (int64_t)bytes * iters;
+  std::vector<Buffer> src, dst;
+  for (int f = 0; f < frames; ++f) {
+    if (dev && device >= 0 && f == 0) HIP_CHECK(hipSetDevice(device));
+    src.emplace_back(bytes, dev);
+    dst.emplace_back(bytes, dev);
+  }
+  if (!dev) {
+    const double t0 = host_ms();
+    for (int i = 0; i < iters; ++i) {
+      const int f = i % frames;
+      auto* sp = reinterpret_cast<uint32_t*>(src[(size_t)f].data());
+      for (size_t j = 0; j < bytes / 4; ++j) sp[j] = pattern_word(tag(i, rank), j);
+      comm->group_start();
+      comm->send(sp, bytes, to, nullptr);
+      comm->recv(dst[(size_t)f].data(), bytes, from, nullptr);
+      comm->group_end();
+      comm->wait(nullptr);
+      const auto* dp = reinterpret_cast<const uint32_t*>(dst[(size_t)f].data());
+      for (size_t j = 0; j < bytes / 4; ++j) res.errors += dp[j] != pattern_word(tag(i, from), j);
+    }
+    res.ms = host_ms() - t0;
+    return res;
+  }
+  // device: frame f's buffers live on stream f mod `streams` (the FrameStream
+  // pattern: consecutive frames alternate streams, one communicator serves all)
+  std::vector<hipStream_t> st((size_t)streams, nullptr);
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  unsigned long long* err = nullptr;
+  auto release = [&]() {
+    for (auto s : st)
+      if (s) (void)hipStreamSynchronize(s);
+    if (err) (void)hipFree(err);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    for (auto s : st)
+      if (s) (void)hipStreamDestroy(s);
+  };
+  try {
+    for (auto& s : st) HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    HIP_CHECK(hipEventCreate(&e0));
+    HIP_CHECK(hipEventCreate(&e1));
+    HIP_CHECK(hipMalloc(&err, sizeof *err));
+    HIP_CHECK(hipMemsetAsync(err, 0, sizeof *err, st[0]));
+    HIP_CHECK(hipEventRecord(e0, st[0]));
+    for (size_t k = 1; k < st.size(); ++k) HIP_CHECK(hipStreamWaitEvent(st[k], e0, 0));
+    for (int i = 0; i < iters; ++i) {
+      const int f = i % frames;
+      hipStream_t s = st[(size_t)(f % streams)];
+      launch_pattern_fill(src[(size_t)f].data(), (int64_t)bytes, tag(i, rank), s);
+      comm->group_start();
+      comm->send(src[(size_t)f].data(), bytes, to, s);
+      comm->recv(dst[(size_t)f].data(), bytes, from, s);
+      comm->group_end();
+      launch_pattern_check(dst[(size_t)f].data(), (int64_t)bytes, tag(i, from), err, s);
+    }
+    for (size_t k = 1; k < st.size(); ++k) {
+      HIP_CHECK(hipEventRecord(e1, st[k]));
+      HIP_CHECK(hipStreamWaitEvent(st[0], e1, 0));
+    }
+    HIP_CHECK(hipEventRecord(e1, st[0]));
+    comm->wait(st[0]);  // bounded (STRIPE_COMM_TIMEOUT_S): a stuck transfer aborts the group
+    float ms = 0;
+    HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    res.ms = ms;
+    unsigned long long e = 0;
+    HIP_CHECK(hipMemcpy(&e, err, sizeof e, hipMemcpyDeviceToHost));
+    res.errors = (int64_t)e;
+  } catch (...) {
+    release();
+    throw;
+  }
+  release();
+  return res;
+}
+
 namespace {
 Image run_rank_impl(const EngineConfig& cfg_in, Comm* comm, int device, const Image* input, const JpegCoefs* jpeg,
                     int iterations, PhaseTimes* times, JpegOut* jpeg_out) {

@@ -69,9 +69,13 @@ class GlooComm:
     def __init__(self, group=None):
         self.group = group
         self.ops = []
-        self.done = threading.Event()
-        self.done.set()
-        self.err = None
+        # state of the latest group_end: [done Event, error]; each group gets
+        # its own pair, bound into its waiter thread, so a waiter left over from
+        # a group the native side abandoned (timeout) can never mark a later
+        # group done
+        done = threading.Event()
+        done.set()
+        self._state = [done, None]
 
     def group_start(self):
         self.ops = []
@@ -85,32 +89,41 @@ class GlooComm:
     def group_end(self):
         works = dist.batch_isend_irecv(self.ops) if self.ops else []
         self.ops = []
-        self.done = threading.Event()
-        self.err = None
+        state = [threading.Event(), None]  # this group's own done flag and error slot
+        self._state = state
         if not works:
-            self.done.set()
+            state[0].set()
             return
         # gloo p2p works only progress inside wait(): a helper thread waits on
         # them and `poll` reads its state (a stalled peer leaves the helper
         # blocked until the process group's own timeout; the native side has
         # given up and raised by then)
 
-        def waiter():
+        def waiter(works=works, state=state):
             try:
                 for w in works:
                     w.wait()
             except Exception as e:  # noqa: BLE001 - reported to the native side as a failed group
-                self.err = e
+                state[1] = e
             finally:
-                self.done.set()
+                state[0].set()
 
         threading.Thread(target=waiter, daemon=True).start()
 
+    @property
+    def done(self) -> threading.Event:
+        return self._state[0]
+
+    @property
+    def err(self):
+        return self._state[1]
+
     def poll(self) -> int:
-        """0: every posted op completed, 1: pending, 2: an op failed."""
-        if not self.done.is_set():
+        """0: every posted op of the latest group completed, 1: pending, 2: an op failed."""
+        done, err = self._state
+        if not done.is_set():
             return 1
-        return 2 if self.err is not None else 0
+        return 2 if err is not None else 0
 
     def barrier(self):
         dist.barrier(group=self.group)
@@ -274,12 +287,20 @@ class FrameStream:
     independent, so with two streams one frame's kernel boundary and tail
     overlap the next frame's step (measured on MI355X, one N=8 share of a
     16384^2 RGB gaussian5: 41.0 -> 35.6 us a step, profiles/r4/cold/).  With
-    `frames=0` the count is chosen so that F x (stripe in + out) exceeds twice
-    the 256 MiB Infinity Cache whenever one stripe fits it: every step then
-    reads data evicted long before (cache-cold), never a warm re-read.
+    `frames=0` the rule is the same at every world size (N = 1 included, so a
+    1 -> N scaling curve compares one execution mode): at least two frames,
+    and when one stripe fits the 256 MiB Infinity Cache, enough that
+    F x (stripe in + out) exceeds twice it -- every step then reads data
+    evicted long before (cache-cold), never a warm re-read.  `cache` says
+    what the rotation achieves: "cold" (F x working set > 2 x the cache),
+    "exceeds the Infinity Cache" (one stripe alone does), "partially warm"
+    (the frame cap left the rotation inside 2 x the cache) or "warm" (one
+    frame that fits).
 
     The reference has one frame, one pass (kernel.cu:190-226); a frame stream
     is this framework's throughput mode on top of the same engine."""
+
+    MAX_FRAMES = 8
 
     def __init__(self, ctx: DistContext, pipeline, W: int, H: int, Cc: int = 3, frames: int = 0, streams: int = 0,
                  autotune: bool = True, stage_timing: bool = False):
@@ -288,18 +309,11 @@ class FrameStream:
         self.iterable = info["cin"] == info["cout"]
         self.ws_max = max(r for _, r in part) * W * (info["cin"] + info["cout"])  # per-GPU bytes of one step
         self.fits_mall = self.ws_max <= MALL_BYTES
-        if frames <= 0:
-            if self.fits_mall and self.iterable and ctx.device:
-                frames = min(8, -(-2 * MALL_BYTES // max(1, self.ws_max)) + 1)
-            elif ctx.device and ctx.world > 1 and self.iterable:
-                frames = 2  # one frame's halo exchange can run beside the other's filter
-            else:
-                frames = 1
-        self.cold = frames > 1 and self.fits_mall
+        frames, self.streaming, self.cold, self.cache = self.plan(self.ws_max, self.iterable, ctx.device, frames)
         nmax = max(1, min(streams if streams > 0 else 2, frames)) if ctx.device else 1
         # stream counts pick_schedule may choose between (a fixed --streams: that one)
         self.stream_options = [nmax] if (streams > 0 or nmax == 1) else [1, nmax]
-        self.frames = [DistributedPipeline(ctx, pipeline, W, H, Cc, autotune=autotune and i == 0, cold=self.cold)
+        self.frames = [DistributedPipeline(ctx, pipeline, W, H, Cc, autotune=autotune and i == 0, cold=self.streaming)
                        for i in range(frames)]
         self.streams = []
         self.nstreams = 1
@@ -309,6 +323,36 @@ class FrameStream:
                 f.engine.stage_timing = stage_timing
         self.set_streams(nmax)
         self._i = 0
+
+    @classmethod
+    def plan(cls, ws_max: int, iterable: bool, device: bool, frames: int = 0):
+        """(frames, streaming, cold, cache) for a stripe whose step touches
+        ws_max bytes per GPU: the frame count (frames <= 0: the auto rule of
+        the class docstring), the engine's streaming policy (a rotated stripe
+        that fits the cache: nt stores, cold autotune), whether the rotation
+        really defeats the cache, and the record's label for it."""
+        fits = ws_max <= MALL_BYTES
+        if frames <= 0:
+            if fits and iterable and device:
+                frames = min(cls.MAX_FRAMES, -(-2 * MALL_BYTES // max(1, ws_max)) + 1)
+            elif device and iterable:
+                # one frame's kernel boundary (and at N > 1 its halo exchange)
+                # can run beside the other's filter -- at every N, N = 1 included
+                frames = 2
+            else:
+                frames = 1
+        streaming = frames > 1 and fits
+        # bytes the rotation touches between two visits of one frame
+        cold = streaming and frames * ws_max > 2 * MALL_BYTES
+        if not fits:
+            cache = "exceeds the Infinity Cache"
+        elif cold:
+            cache = "cold"
+        elif frames > 1:
+            cache = "partially warm"
+        else:
+            cache = "warm"
+        return frames, streaming, cold, cache
 
     def set_streams(self, n: int):
         """Queue frame f on stream f mod n (n <= the streams created)."""
@@ -453,5 +497,18 @@ def probe_link_rate(ctx: DistContext, nbytes: int = 64 << 20, reps: int = 3) -> 
     return C.probe_link_rate(ctx.comm, ctx.gpu if ctx.device else -1, nbytes, reps)
 
 
+def ring_check(ctx: DistContext, nbytes: int = 1 << 20, frames: int = 4, streams: int = 2, iters: int = 500) -> dict:
+    """Transport check of this context's communicator in the FrameStream
+    pattern: `iters` grouped send/recv exchanges around the ring (one rank:
+    the RCCL communicator sends to and receives from itself), consecutive
+    frames alternating over `streams` streams on the one communicator, every
+    received word checked against its sender's (iteration, rank) pattern.
+    Returns {"errors", "bytes_checked", "ms"} (every rank must call it)."""
+    if ctx.comm is None:
+        raise ValueError("ring_check needs a communicator (a device context, or world > 1)")
+    return C.comm_ring_check(ctx.comm, ctx.gpu if ctx.device else -1, int(nbytes), frames, streams, iters)
+
+
 __all__ = ["DistContext", "GlooComm", "init", "DistributedPipeline", "plan_rows", "plan_rows_weighted", "dist_split",
-           "probe_link_rate", "run_local_group", "rank_identity", "world_identity", "identity_summary", "FrameStream"]
+           "probe_link_rate", "ring_check", "run_local_group", "rank_identity", "world_identity", "identity_summary",
+           "FrameStream"]

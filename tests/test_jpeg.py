@@ -9,6 +9,7 @@ a mean difference well under 0.1 level.
 import io
 import os
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -172,6 +173,37 @@ def test_corrupt_input_raises(C):
     good = C.encode_jpeg(_smooth(16, 16, 3), 90)
     with pytest.raises(RuntimeError):
         C.decode_jpeg(good[: len(good) // 3])  # truncated: header fine, tables / scan cut
+
+
+def _sof_file(W, H, pad):
+    # SOI, a 3-component progressive SOF declaring W x H, then `pad` bytes
+    sof = bytes([0xFF, 0xC2, 0x00, 17, 8, H >> 8, H & 255, W >> 8, W & 255, 3,
+                 1, 0x11, 0, 2, 0x11, 0, 3, 0x11, 0])
+    return b"\xff\xd8" + sof + b"\x00" * pad
+
+
+def test_huge_frame_header_in_small_file_rejected(C):
+    # a ~262 KB file declaring 65535 x 65535 4:4:4 passed the
+    # pixels-per-byte guard and would allocate ~40 GB; the absolute pixel cap
+    # (2^28 by default) rejects it before any allocation
+    with pytest.raises(RuntimeError, match="pixel limit"):
+        C.decode_jpeg(_sof_file(65535, 65535, 262144 + 1024))
+
+
+def test_pixel_cap_env_override(tmp_path):
+    # STRIPE_JPEG_MAX_PIXELS lowers (or raises) the cap; read once per process
+    code = ("import sys; sys.path.insert(0, %r); from mpi_cuda_imagemanipulation_amd._native import C\n"
+            "import numpy as np\n"
+            "img = np.full((64, 64, 3), 90, np.uint8)\n"
+            "data = C.encode_jpeg(img, 90)\n"
+            "try:\n    C.decode_jpeg(data); print('DECODED')\n"
+            "except RuntimeError as e:\n    print('REJECTED', 'pixel limit' in str(e))\n") % ROOT
+    env = dict(os.environ, STRIPE_JPEG_MAX_PIXELS="1000")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert "REJECTED True" in r.stdout, r.stdout + r.stderr
+    env["STRIPE_JPEG_MAX_PIXELS"] = "4096"
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert "DECODED" in r.stdout, r.stdout + r.stderr
 
 
 def test_read_image_sniffs_content_and_python_io(C, tmp_path):

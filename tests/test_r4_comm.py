@@ -396,7 +396,26 @@ def test_frame_stream_auto_frames_rule(C, monkeypatch):
         monkeypatch.delenv(k, raising=False)
     ctx = parallel.init("gloo")
     fs = parallel.FrameStream(ctx, m.models.Pipeline("gaussian5"), 64, 40, 3)
-    assert len(fs) == 1 and fs.fits_mall and not fs.cold  # host engines never rotate
+    assert len(fs) == 1 and fs.fits_mall and not fs.cold and fs.cache == "warm"  # host engines never rotate
+
+
+@pytest.mark.parametrize("ws,iterable,device,frames,want", [
+    # the headline's per-GPU step bytes (16384^2 RGB gaussian5) at N = 1 / 2 / 8
+    (16384 * 16384 * 6, True, True, 0, (2, False, False, "exceeds the Infinity Cache")),
+    (8192 * 16384 * 6, True, True, 0, (2, False, False, "exceeds the Infinity Cache")),
+    (2048 * 16384 * 6, True, True, 0, (4, True, True, "cold")),
+    # a small share: the 8-frame cap leaves the rotation inside 2 x the cache
+    (16 << 20, True, True, 0, (8, True, False, "partially warm")),
+    (16 << 20, True, True, 1, (1, False, False, "warm")),
+    (16 << 20, True, False, 0, (1, False, False, "warm")),      # host engines never rotate
+    (16 << 20, False, True, 0, (1, False, False, "warm")),      # channel-changing chain
+])
+def test_frame_stream_plan_same_rule_every_n(ws, iterable, device, frames, want):
+    # one frames rule at every N (N = 1 too: two frames), and the
+    # cache label says what the rotation achieves
+    from mpi_cuda_imagemanipulation_amd import parallel
+
+    assert parallel.FrameStream.plan(ws, iterable, device, frames) == want
 
 
 @pytest.mark.gpu
@@ -412,7 +431,8 @@ def test_frame_stream_gpu_each_frame_exact(C, monkeypatch, chain, Cc):
     ctx = parallel.init("rccl")
     W, H = 1030, 200
     fs = parallel.FrameStream(ctx, m.models.Pipeline(chain, halo_depth=1), W, H, Cc, frames=3)
-    assert len(fs) == 3 and fs.nstreams == 2 and fs.cold
+    # (3 small frames fit the cache together: streaming policy, honestly not "cold")
+    assert len(fs) == 3 and fs.nstreams == 2 and fs.streaming and not fs.cold and fs.cache == "partially warm"
     fs.load_synthetic(9)
     fs.tune()
     rounds = 3 if fs.iterable else 1

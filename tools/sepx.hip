@@ -1,0 +1,339 @@
+// Cache-cold separable-stencil experiments on one N=8 share of the headline
+// (16384 x rows RGB gaussian5, default rows = 2048): where does a cold step's
+// time go, and which launch shape / store policy gets closest to a plain copy
+// of the same bytes?  (profiles/r5/cold/README.md)
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Icsrc/include -Icsrc/hip \
+//         -o bin/sepx tools/sepx.hip
+//   bin/sepx [rows] [frames] [stamp_csv_prefix] [sweep: tail | policy]
+//
+// Every measurement rotates over `frames` independent in/out buffer pairs
+// (default: enough that frames x (in + out) > 3 x 256 MiB), so each launch
+// reads data the Infinity Cache evicted long before.  Reported per variant:
+// the mean time per launch of a burst of back-to-back launches (one stream,
+// and frames alternating over two streams): what the headline's host clock
+// sees.  Kernel-only times come from rocprofv3 over the same binary.
+//
+// Variants (k_sep<3, Gaussian5, ...> of csrc/hip/stencil_kernels.h): store
+// policy aux 0 (default), 2 (nt), 16 (sc1 write-through), 18 (sc1 nt); band
+// height x occupancy cap x workgroup order (XCD remap); the task mode
+// (kOneTask, kTailBands, kQueue); a linear copy of the same bytes as the
+// floor.  Then per-wave stamps (KArgs::stamps) of one cold dispatch of chosen
+// variants: start / end spread and wave lifetime, written as CSV.
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "stencil_kernels.h"
+
+using namespace stripe;
+using namespace stripe::dev;
+
+#define CK(x)                                                                             \
+  do {                                                                                    \
+    hipError_t e_ = (x);                                                                  \
+    if (e_ != hipSuccess) {                                                               \
+      std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_));      \
+      std::exit(1);                                                                       \
+    }                                                                                     \
+  } while (0)
+
+template <int AUX>
+__global__ __launch_bounds__(256) void k_copy_lin(const uint8_t* in, uint8_t* out, uint32_t bytes) {
+  const __amdgpu_buffer_rsrc_t ri = make_rsrc(in, bytes);
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(out, bytes);
+  const uint32_t off = ((uint32_t)blockIdx.x * 256u + threadIdx.x) * 16u;
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(ri, off, 0, 2);
+  __builtin_amdgcn_raw_buffer_store_b128(v, ro, off, 0, AUX);
+}
+
+struct Frame {
+  uint8_t* in = nullptr;
+  uint8_t* out = nullptr;
+  uint32_t* queue = nullptr;  // kQueue launches' work queue (zeroed once)
+};
+
+static int g_W = 16384, g_C = 3, g_rows = 2048;
+static int64_t g_pitch = 0, g_bytes = 0, g_org = 0;
+static std::vector<Frame> g_frames;
+
+using SepFn = void (*)(KArgs);
+template <int SAUX, int MODE>
+static SepFn sep_fn_mode(bool stamp) {
+  using G = sdef::Gaussian5;
+  return stamp ? k_sep<3, G, PRO_NONE, false, SAUX, false, MODE, true> : k_sep<3, G, PRO_NONE, false, SAUX, false, MODE>;
+}
+template <int SAUX>
+static SepFn sep_fn_aux(int mode, bool stamp) {
+  if (mode == kQueue) return sep_fn_mode<SAUX, kQueue>(stamp);
+  if (mode == kTailBands) return sep_fn_mode<SAUX, kTailBands>(stamp);
+  return sep_fn_mode<SAUX, kOneTask>(stamp);
+}
+static SepFn sep_fn(int saux, int mode, bool stamp) {
+  switch (saux) {
+    case 0: return sep_fn_aux<0>(mode, stamp);
+    case 2: return sep_fn_aux<2>(mode, stamp);
+    case 16: return sep_fn_aux<16>(mode, stamp);
+    default: return sep_fn_aux<18>(mode, stamp);
+  }
+}
+
+struct SepCfg {
+  int saux = 2, band = 12, cap = 2, nxcd = 0, mode = kOneTask, tail = 0;
+  std::string name() const {
+    static const char* modes[] = {"one-task", "tail-bands", "queue"};
+    char b[128];
+    std::snprintf(b, sizeof b, "sep aux=%2d band=%2d cap=%d xcd=%d %s tail=%d", saux, band, cap, nxcd, modes[mode],
+                  tail);
+    return b;
+  }
+};
+
+static void launch_sep(const SepCfg& c, const Frame& f, hipStream_t s, uint32_t* stamps = nullptr,
+                       int* grid_out = nullptr) {
+  KArgs a{};
+  a.in = f.in + g_org;
+  a.out = f.out + g_org;
+  a.in_pitch = a.out_pitch = g_pitch;
+  a.W = g_W;
+  a.E = g_W * g_C;
+  a.rows = g_rows;
+  a.row0 = 0;
+  a.Hg = g_rows;
+  a.border = 0;
+  a.in_base = f.in;
+  a.out_base = f.out;
+  a.in_bytes = a.out_bytes = (uint32_t)g_bytes;
+  a.in_org = a.out_org = (uint32_t)g_org;
+  a.in_zero = kMarginBytes;
+  a.ry0 = 0;
+  a.ry1 = g_rows;
+  a.stamps = stamps;
+  const int tiles = (int)div_up(a.E, kOutChunks * 16);
+  dim3 grid;
+  const SepFn fn = sep_fn(c.saux, c.mode, stamps != nullptr);
+  plan_bands(a, grid, tiles, g_rows, 0, c.band, 2, 0);
+  a.nxcd = c.nxcd;
+  const size_t dyn = nt_lds_reserve((const void*)fn, c.cap);
+  if (c.mode == kQueue) {
+    a.queue = f.queue;
+    plan_persistent(a, grid, (const void*)fn, dyn, c.tail);
+  } else if (c.mode == kTailBands) {
+    plan_tail(a, grid, (const void*)fn, dyn, c.tail);
+  }
+  if (grid_out) *grid_out = (int)grid.x;
+  fn<<<grid, kNT, dyn, s>>>(a);
+}
+
+static void launch_copy(int aux, const Frame& f, hipStream_t s) {
+  const uint32_t n = (uint32_t)((int64_t)g_rows * g_pitch);
+  const unsigned blocks = (unsigned)div_up(n, 4096);
+  if (aux == 0) k_copy_lin<0><<<blocks, 256, 0, s>>>(f.in, f.out, n);
+  else if (aux == 2) k_copy_lin<2><<<blocks, 256, 0, s>>>(f.in, f.out, n);
+  else k_copy_lin<16><<<blocks, 256, 0, s>>>(f.in, f.out, n);
+}
+
+// mean ms per launch of a burst of n back-to-back launches over the frames
+// (frame i % F on stream (i % F) % ns); median of 3 bursts
+static double burst(const std::function<void(const Frame&, hipStream_t)>& launch, int ns, int n,
+                    hipStream_t* st) {
+  const int F = (int)g_frames.size();
+  for (int i = 0; i < 2 * F; ++i) launch(g_frames[i % F], st[(i % F) % ns]);
+  CK(hipDeviceSynchronize());
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  std::vector<double> r;
+  for (int rep = 0; rep < 3; ++rep) {
+    CK(hipEventRecord(e0, st[0]));
+    for (int k = 1; k < ns; ++k) CK(hipStreamWaitEvent(st[k], e0, 0));
+    for (int i = 0; i < n; ++i) launch(g_frames[i % F], st[(i % F) % ns]);
+    for (int k = 1; k < ns; ++k) {
+      hipEvent_t j;
+      CK(hipEventCreateWithFlags(&j, hipEventDisableTiming));
+      CK(hipEventRecord(j, st[k]));
+      CK(hipStreamWaitEvent(st[0], j, 0));
+      CK(hipEventDestroy(j));
+    }
+    CK(hipEventRecord(e1, st[0]));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    r.push_back(ms / n);
+  }
+  CK(hipEventDestroy(e0));
+  CK(hipEventDestroy(e1));
+  std::sort(r.begin(), r.end());
+  return r[1];
+}
+
+static void fill_random(uint8_t* d, int64_t n, uint32_t seed) {
+  std::vector<uint8_t> h((size_t)n);
+  uint64_t x = 0x9E3779B97F4A7C15ull * (seed + 1);
+  for (int64_t i = 0; i < n; ++i) {
+    x ^= x << 13;
+    x ^= x >> 7;
+    x ^= x << 17;
+    h[(size_t)i] = (uint8_t)(x >> 24);
+  }
+  CK(hipMemcpy(d, h.data(), (size_t)n, hipMemcpyHostToDevice));
+}
+
+// output of variant c on frame 0 equals the plain one-task launch's, byte for byte
+static int64_t check_same(const SepCfg& c) {
+  std::vector<uint8_t> ref((size_t)g_bytes), got((size_t)g_bytes);
+  hipStream_t s = nullptr;
+  CK(hipStreamCreate(&s));
+  launch_sep(SepCfg{}, g_frames[0], s);
+  CK(hipStreamSynchronize(s));
+  CK(hipMemcpy(ref.data(), g_frames[0].out, (size_t)g_bytes, hipMemcpyDeviceToHost));
+  CK(hipMemset(g_frames[0].out, 0, (size_t)g_bytes));
+  launch_sep(c, g_frames[0], s);
+  launch_sep(c, g_frames[0], s);  // twice: the queue must have been reset by the first
+  CK(hipStreamSynchronize(s));
+  CK(hipMemcpy(got.data(), g_frames[0].out, (size_t)g_bytes, hipMemcpyDeviceToHost));
+  CK(hipStreamDestroy(s));
+  int64_t bad = 0;
+  for (int y = 0; y < g_rows; ++y)
+    for (int64_t b = 0; b < (int64_t)g_W * g_C; ++b) {
+      const size_t i = (size_t)(g_org + y * g_pitch + b);
+      bad += ref[i] != got[i];
+    }
+  return bad;
+}
+
+int main(int argc, char** argv) {
+  g_rows = argc > 1 ? std::atoi(argv[1]) : 2048;
+  int F = argc > 2 ? std::atoi(argv[2]) : 0;
+  const std::string csv = argc > 3 ? argv[3] : "";
+  const std::string sweep = argc > 4 ? argv[4] : "tail";
+  g_pitch = padded_pitch(g_W, g_C);
+  g_org = 2 * g_pitch + kMarginBytes;
+  g_bytes = (int64_t)(g_rows + 4) * g_pitch + 256;
+  if (F <= 0) F = std::max<int>(1, (int)div_up(3ll * (256 << 20), 2 * g_bytes));
+  int cus = 0;
+  CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  std::printf("# sepx: %dx%dx%d gaussian5, pitch %lld, %d frames (%.0f MiB in+out each), %d CUs\n", g_W, g_rows, g_C,
+              (long long)g_pitch, F, 2.0 * g_bytes / (1 << 20), cus);
+  g_frames.resize((size_t)F);
+  for (int f = 0; f < F; ++f) {
+    CK(hipMalloc(&g_frames[f].in, (size_t)g_bytes));
+    CK(hipMalloc(&g_frames[f].out, (size_t)g_bytes));
+    fill_random(g_frames[f].in, g_bytes, (uint32_t)f);
+    CK(hipMemset(g_frames[f].out, 0, (size_t)g_bytes));
+    CK(hipMalloc(&g_frames[f].queue, kQueueWords * 4));
+    CK(hipMemset(g_frames[f].queue, 0, kQueueWords * 4));
+  }
+  hipStream_t st[2];
+  for (auto& s : st) CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  const double mb = 2.0 * (double)g_rows * g_W * g_C;  // useful bytes per launch (in + out)
+  const int n = std::max(48, 4 * F);
+  auto report = [&](const std::string& name, const std::function<void(const Frame&, hipStream_t)>& fn) {
+    const double t1 = burst(fn, 1, n, st), t2 = burst(fn, 2, n, st);
+    std::printf("%-56s 1 stream %8.2f us (%5.2f TB/s)   2 streams %8.2f us (%5.2f TB/s)\n", name.c_str(), t1 * 1e3,
+                mb / (t1 * 1e-3) / 1e12, t2 * 1e3, mb / (t2 * 1e-3) / 1e12);
+    std::fflush(stdout);
+  };
+
+  std::vector<SepCfg> cfgs;
+  auto add = [&](int saux, int band, int cap, int nxcd, int mode, int tail) {
+    SepCfg c;
+    c.saux = saux;
+    c.band = band;
+    c.cap = cap;
+    c.nxcd = nxcd;
+    c.mode = mode;
+    c.tail = tail;
+    cfgs.push_back(c);
+  };
+  if (sweep == "policy") {  // store policy x band x cap, one task per wave
+    for (int saux : {0, 2, 16, 18})
+      for (int band : {8, 12, 16})
+        for (int cap : {0, 2, 3}) add(saux, band, cap, 0, kOneTask, 0);
+  } else {  // task modes (nt stores)
+    for (int band : {8, 12, 16})
+      for (int cap : {2, 3})
+        for (int nxcd : {0, 8}) add(2, band, cap, nxcd, kOneTask, 0);
+    for (int band : {12, 16, 20, 24, 32})
+      for (int cap : {2, 3})
+        for (int tail : {4, 8}) add(2, band, cap, 0, kTailBands, tail);
+    add(2, 16, 2, 0, kQueue, 4);
+  }
+  // correctness of every non-default task mode / band split: byte-equal to the
+  // one-task launch (run twice: a queue must come back reset)
+  for (const SepCfg& c : cfgs)
+    if (c.mode != kOneTask) {
+      const int64_t bad = check_same(c);
+      std::printf("# %s vs one-task: %lld differing bytes\n", c.name().c_str(), (long long)bad);
+      if (bad) return 2;
+    }
+  for (int aux : {0, 2, 16}) report("copy aux=" + std::to_string(aux), [&](const Frame& f, hipStream_t s) {
+    launch_copy(aux, f, s);
+  });
+  for (const SepCfg& c : cfgs) report(c.name(), [&](const Frame& f, hipStream_t s) { launch_sep(c, f, s); });
+
+  // per-wave timeline of one cold dispatch (the last of a rotation)
+  std::vector<SepCfg> stamped(3);
+  stamped[1].mode = kTailBands;
+  stamped[1].band = 16;
+  stamped[1].tail = 4;
+  stamped[2].mode = kTailBands;
+  stamped[2].band = 24;
+  stamped[2].tail = 4;
+  for (size_t k = 0; k < stamped.size(); ++k) {
+    const SepCfg& c = stamped[k];
+    int grid = 0;
+    for (int i = 0; i < F; ++i) launch_sep(c, g_frames[i], st[0], nullptr, &grid);
+    uint32_t* ds = nullptr;
+    const size_t nw = (size_t)grid * kWaves;
+    CK(hipMalloc(&ds, nw * 16));
+    CK(hipMemset(ds, 0, nw * 16));
+    launch_sep(c, g_frames[0], st[0], ds);
+    CK(hipStreamSynchronize(st[0]));
+    std::vector<uint32_t> h(nw * 4);
+    CK(hipMemcpy(h.data(), ds, nw * 16, hipMemcpyDeviceToHost));
+    CK(hipFree(ds));
+    uint32_t t0 = 0xFFFFFFFFu, t1 = 0;
+    std::vector<double> life, starts, ends;
+    for (size_t w = 0; w < nw; ++w) {
+      if (h[4 * w] == 0 && h[4 * w + 1] == 0) continue;
+      t0 = std::min(t0, h[4 * w]);
+      t1 = std::max(t1, h[4 * w + 1]);
+    }
+    for (size_t w = 0; w < nw; ++w) {
+      if (h[4 * w] == 0 && h[4 * w + 1] == 0) continue;
+      starts.push_back((h[4 * w] - t0) * 0.01);
+      ends.push_back((h[4 * w + 1] - t0) * 0.01);
+      life.push_back((h[4 * w + 1] - h[4 * w]) * 0.01);
+    }
+    auto pct = [](std::vector<double> v, double p) {
+      std::sort(v.begin(), v.end());
+      return v.empty() ? 0.0 : v[std::min(v.size() - 1, (size_t)(p * (v.size() - 1)))];
+    };
+    std::printf("stamps %-48s waves %zu span %.2f us | start p50 %.2f p99 %.2f max %.2f | end min %.2f p01 %.2f p50 %.2f "
+                "| life p50 %.2f max %.2f\n",
+                c.name().c_str(), starts.size(), (t1 - t0) * 0.01, pct(starts, 0.5), pct(starts, 0.99),
+                pct(starts, 1.0), pct(ends, 0.0), pct(ends, 0.01), pct(ends, 0.5), pct(life, 0.5), pct(life, 1.0));
+    if (!csv.empty()) {
+      const std::string path = csv + "_" + std::to_string(k) + ".csv";
+      FILE* fp = std::fopen(path.c_str(), "w");
+      if (fp) {
+        std::fprintf(fp, "# %s\nwave,start_us,end_us,hw_id,xcc_id\n", c.name().c_str());
+        for (size_t w = 0; w < nw; ++w)
+          if (h[4 * w] || h[4 * w + 1])
+            std::fprintf(fp, "%zu,%.2f,%.2f,%u,%u\n", w, (h[4 * w] - t0) * 0.01, (h[4 * w + 1] - t0) * 0.01,
+                         h[4 * w + 2], h[4 * w + 3]);
+        std::fclose(fp);
+      }
+    }
+  }
+  for (auto& f : g_frames) {
+    CK(hipFree(f.in));
+    CK(hipFree(f.out));
+    CK(hipFree(f.queue));
+  }
+  return 0;
+}
