@@ -56,29 +56,33 @@ struct Frame {
   uint32_t* queue = nullptr;  // kQueue launches' work queue (zeroed once)
 };
 
-static int g_W = 16384, g_C = 3, g_rows = 2048;
+static int g_W = 16384, g_C = 3, g_rows = 2048, g_out_px = 0;
 static int64_t g_pitch = 0, g_bytes = 0, g_org = 0;
 static std::vector<Frame> g_frames;
 
 using SepFn = void (*)(KArgs);
-template <int SAUX, int MODE>
+static bool g_sobel = false;  // the filter: gaussian5 on RGB (default) or sobel on gray
+template <int C, class Flt, int SAUX, int MODE>
 static SepFn sep_fn_mode(bool stamp) {
-  using G = sdef::Gaussian5;
-  return stamp ? k_sep<3, G, PRO_NONE, false, SAUX, false, MODE, true> : k_sep<3, G, PRO_NONE, false, SAUX, false, MODE>;
+  return stamp ? k_sep<C, Flt, PRO_NONE, false, SAUX, false, MODE, true> : k_sep<C, Flt, PRO_NONE, false, SAUX, false, MODE>;
 }
-template <int SAUX>
+template <int C, class Flt, int SAUX>
 static SepFn sep_fn_aux(int mode, bool stamp) {
-  if (mode == kQueue) return sep_fn_mode<SAUX, kQueue>(stamp);
-  if (mode == kTailBands) return sep_fn_mode<SAUX, kTailBands>(stamp);
-  return sep_fn_mode<SAUX, kOneTask>(stamp);
+  if (mode == kQueue) return sep_fn_mode<C, Flt, SAUX, kQueue>(stamp);
+  if (mode == kTailBands) return sep_fn_mode<C, Flt, SAUX, kTailBands>(stamp);
+  return sep_fn_mode<C, Flt, SAUX, kOneTask>(stamp);
+}
+template <int C, class Flt>
+static SepFn sep_fn_flt(int saux, int mode, bool stamp) {
+  switch (saux) {
+    case 0: return sep_fn_aux<C, Flt, 0>(mode, stamp);
+    case 2: return sep_fn_aux<C, Flt, 2>(mode, stamp);
+    case 16: return sep_fn_aux<C, Flt, 16>(mode, stamp);
+    default: return sep_fn_aux<C, Flt, 18>(mode, stamp);
+  }
 }
 static SepFn sep_fn(int saux, int mode, bool stamp) {
-  switch (saux) {
-    case 0: return sep_fn_aux<0>(mode, stamp);
-    case 2: return sep_fn_aux<2>(mode, stamp);
-    case 16: return sep_fn_aux<16>(mode, stamp);
-    default: return sep_fn_aux<18>(mode, stamp);
-  }
+  return g_sobel ? sep_fn_flt<1, sdef::Sobel>(saux, mode, stamp) : sep_fn_flt<3, sdef::Gaussian5>(saux, mode, stamp);
 }
 
 struct SepCfg {
@@ -111,11 +115,13 @@ static void launch_sep(const SepCfg& c, const Frame& f, hipStream_t s, uint32_t*
   a.in_zero = kMarginBytes;
   a.ry0 = 0;
   a.ry1 = g_rows;
+  a.out_px = g_out_px;  // x-margins of the output kept like the engine's iterated passes
+  a.out_border = 0;
   a.stamps = stamps;
   const int tiles = (int)div_up(a.E, kOutChunks * 16);
   dim3 grid;
   const SepFn fn = sep_fn(c.saux, c.mode, stamps != nullptr);
-  plan_bands(a, grid, tiles, g_rows, 0, c.band, 2, 0);
+  plan_bands(a, grid, tiles, g_rows, 0, c.band, g_sobel ? 1 : 2, 0);
   a.nxcd = c.nxcd;
   const size_t dyn = nt_lds_reserve((const void*)fn, c.cap);
   if (c.mode == kQueue) {
@@ -210,14 +216,20 @@ int main(int argc, char** argv) {
   int F = argc > 2 ? std::atoi(argv[2]) : 0;
   const std::string csv = argc > 3 ? argv[3] : "";
   const std::string sweep = argc > 4 ? argv[4] : "tail";
+  if (sweep == "sobel") {  // config 3's share: 8192 x rows gray sobel, margins kept (iterated pass)
+    g_sobel = true;
+    g_W = 8192;
+    g_C = 1;
+    g_out_px = 1;
+  }
   g_pitch = padded_pitch(g_W, g_C);
   g_org = 2 * g_pitch + kMarginBytes;
   g_bytes = (int64_t)(g_rows + 4) * g_pitch + 256;
   if (F <= 0) F = std::max<int>(1, (int)div_up(3ll * (256 << 20), 2 * g_bytes));
   int cus = 0;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
-  std::printf("# sepx: %dx%dx%d gaussian5, pitch %lld, %d frames (%.0f MiB in+out each), %d CUs\n", g_W, g_rows, g_C,
-              (long long)g_pitch, F, 2.0 * g_bytes / (1 << 20), cus);
+  std::printf("# sepx: %dx%dx%d %s, pitch %lld, %d frames (%.0f MiB in+out each), %d CUs\n", g_W, g_rows, g_C,
+              g_sobel ? "sobel" : "gaussian5", (long long)g_pitch, F, 2.0 * g_bytes / (1 << 20), cus);
   g_frames.resize((size_t)F);
   for (int f = 0; f < F; ++f) {
     CK(hipMalloc(&g_frames[f].in, (size_t)g_bytes));
@@ -249,7 +261,13 @@ int main(int argc, char** argv) {
     c.tail = tail;
     cfgs.push_back(c);
   };
-  if (sweep == "policy") {  // store policy x band x cap, one task per wave
+  if (sweep == "sobel") {  // band x cap x order, and tail bands
+    for (int band : {4, 8, 12})
+      for (int cap : {0, 2, 4})
+        for (int nxcd : {0, 8}) add(0, band, cap, nxcd, kOneTask, 0);
+    for (int band : {8, 12})
+      for (int cap : {0, 4}) add(0, band, cap, 8, kTailBands, 4);
+  } else if (sweep == "policy") {  // store policy x band x cap, one task per wave
     for (int saux : {0, 2, 16, 18})
       for (int band : {8, 12, 16})
         for (int cap : {0, 2, 3}) add(saux, band, cap, 0, kOneTask, 0);
@@ -277,12 +295,24 @@ int main(int argc, char** argv) {
 
   // per-wave timeline of one cold dispatch (the last of a rotation)
   std::vector<SepCfg> stamped(3);
+  if (g_sobel)
+    for (auto& c : stamped) {
+      c.saux = 0;
+      c.cap = 0;
+      c.nxcd = 8;
+    }
+  if (g_sobel) {
+    stamped[0].band = 4;
+    stamped[1].band = 8;
+    stamped[2].band = 12;
+  } else {
   stamped[1].mode = kTailBands;
   stamped[1].band = 16;
   stamped[1].tail = 4;
   stamped[2].mode = kTailBands;
   stamped[2].band = 24;
   stamped[2].tail = 4;
+  }
   for (size_t k = 0; k < stamped.size(); ++k) {
     const SepCfg& c = stamped[k];
     int grid = 0;
