@@ -21,6 +21,13 @@
 #include "stripe/image.h"
 #include "stripe/kernels.h"
 
+// No multiply-add contraction in this file: every kernel form (per-pixel or
+// 16 samples per lane) and the host stages then round each product and sum
+// the same way, so the vectorised kernels are bit-identical to the per-pixel
+// ones (contraction chose different fma trees in the two forms of the encode
+// planes: one quantisation tie in a 61 x 1000 frame flipped)
+#pragma clang fp contract(off)
+
 namespace stripe {
 
 namespace dev {
@@ -86,8 +93,141 @@ __device__ __forceinline__ int jpeg_sample(const JpegPlaneRef& q, int x, int y) 
   return at(min(q.cw - 1, x / q.fx), min(q.ch - 1, y / q.fy));
 }
 
+// Upsampled samples x0 .. x0 + 15 of one component in output row y, for a
+// group inside the frame (x0 + 16 <= W, x0 % 16 == 0): the same filter as
+// jpeg_sample, on 8-byte plane loads.  Returns false for sampling ratios other
+// than 1 and 2 (the caller then samples pixel by pixel).
+__device__ __forceinline__ bool jpeg_row16(const JpegPlaneRef& q, int x0, int y, int (&s)[16]) {
+  if (q.fx > 2 || q.fy > 2) return false;
+  const int iy = y / q.fy;
+  const bool v4 = q.fy == 2;
+  const int ny = (y % 2 == 0) ? max(0, iy - 1) : min(q.ch - 1, iy + 1);
+  const uint8_t* r0 = q.p + (int64_t)iy * q.ps;
+  const uint8_t* r1 = q.p + (int64_t)ny * q.ps;
+  // column sums cs(i) = 3 at(i, iy) + at(i, ny) (v4) or at(i, iy), for the
+  // plane columns the 16 outputs read
+  auto bytes8 = [](const uint8_t* p, int (&o)[8]) __attribute__((always_inline)) {
+    const uint2 v = *reinterpret_cast<const uint2*>(p);  // x0 % 16 == 0, pitch % 8 == 0: 8-byte aligned
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      o[e] = (v.x >> (8 * e)) & 0xFF;
+      o[4 + e] = (v.y >> (8 * e)) & 0xFF;
+    }
+  };
+  if (q.fx == 1) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      int a[8], b[8];
+      bytes8(r0 + x0 + 8 * h, a);
+      if (v4) bytes8(r1 + x0 + 8 * h, b);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s[8 * h + e] = v4 ? (3 * a[e] + b[e] + 1 + (y & 1)) >> 2 : a[e];
+    }
+    return true;
+  }
+  // fx == 2: output x reads plane columns x / 2 and its neighbour
+  const int i0 = x0 >> 1;  // 8-byte aligned
+  int a[8], b[8];
+  bytes8(r0 + i0, a);
+  if (v4) bytes8(r1 + i0, b);
+  int cs[10];  // columns i0 - 1 .. i0 + 8 (clamped to the plane)
+#pragma unroll
+  for (int e = 0; e < 8; ++e) cs[1 + e] = v4 ? 3 * a[e] + b[e] : a[e];
+  const int il = max(0, i0 - 1), ir = min(q.cw - 1, i0 + 8);
+  cs[0] = v4 ? 3 * r0[il] + r1[il] : r0[il];
+  cs[9] = v4 ? 3 * r0[ir] + r1[ir] : r0[ir];
+  const int sh = v4 ? 4 : 2, b0 = v4 ? 8 : 1, b1 = v4 ? 7 : 2;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int c = cs[1 + (j >> 1)];
+    s[j] = (j & 1) == 0 ? (3 * c + cs[j >> 1] + b0) >> sh : (3 * c + cs[2 + (j >> 1)] + b1) >> sh;
+  }
+  return true;
+}
+
+// YCbCr (or RGB / gray) samples -> output bytes, the host conversion's arithmetic.
+__device__ __forceinline__ void jpeg_convert(int Y, int U, int V, bool rgb, uint8_t (&o)[3]) {
+  if (rgb) {
+    o[0] = (uint8_t)Y;
+    o[1] = (uint8_t)U;
+    o[2] = (uint8_t)V;
+    return;
+  }
+  const float yy = (float)Y, cb = (float)U - 128.f, cr = (float)V - 128.f;
+  o[0] = jpeg_u8(yy + 1.402f * cr);
+  o[1] = jpeg_u8(yy - 0.344136f * cb - 0.714136f * cr);
+  o[2] = jpeg_u8(yy + 1.772f * cb);
+}
+
+// Decode colour stage: 16 output pixels of one row per lane (2-D grid: blockIdx.y
+// = row, no 64-bit index division).  Groups inside the frame read the planes
+// with 8-byte loads and store their 16 RGB pixels as three 16-byte stores (or
+// one for gray) when the destination rows are 16-byte aligned (ALIGNED); the
+// row's last, partial group samples and stores pixel by pixel.  Same samples
+// and arithmetic as the per-pixel form: the GPU and host pixels stay identical.
+template <bool ALIGNED>
+__global__ __launch_bounds__(256) void k_jpeg_color16(JpegPlaneRef c0, JpegPlaneRef c1, JpegPlaneRef c2, int nc,
+                                                      bool rgb, int W, uint8_t* __restrict__ dst, int64_t pitch) {
+  const int x0 = ((int)blockIdx.x * 256 + (int)threadIdx.x) * 16;
+  const int y = (int)blockIdx.y;
+  if (x0 >= W) return;
+  uint8_t* o = dst + (int64_t)y * pitch + (int64_t)x0 * nc;
+  int sy[16], su[16], sv[16];
+  bool fast = x0 + 16 <= W && jpeg_row16(c0, x0, y, sy);
+  if (fast && nc == 3) fast = jpeg_row16(c1, x0, y, su) && jpeg_row16(c2, x0, y, sv);
+  if (!fast) {
+    for (int j = 0; j < 16 && x0 + j < W; ++j) {
+      const int x = x0 + j;
+      const int Y = jpeg_sample(c0, x, y);
+      if (nc == 1) {
+        o[j] = (uint8_t)Y;
+        continue;
+      }
+      uint8_t px[3];
+      jpeg_convert(Y, jpeg_sample(c1, x, y), jpeg_sample(c2, x, y), rgb, px);
+      o[3 * j] = px[0];
+      o[3 * j + 1] = px[1];
+      o[3 * j + 2] = px[2];
+    }
+    return;
+  }
+  if (nc == 1) {
+    uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j >> 2] |= (uint32_t)sy[j] << (8 * (j & 3));
+    if (ALIGNED) {
+      *reinterpret_cast<uint4*>(o) = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) o[j] = (uint8_t)sy[j];
+    }
+    return;
+  }
+  uint32_t w[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    uint8_t px[3];
+    jpeg_convert(sy[j], su[j], sv[j], rgb, px);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const int e = 3 * j + c;  // compile-time byte index after unrolling
+      w[e >> 2] |= (uint32_t)px[c] << (8 * (e & 3));
+    }
+  }
+  if (ALIGNED) {
+    uint4* o4 = reinterpret_cast<uint4*>(o);
+    o4[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    o4[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    o4[2] = make_uint4(w[8], w[9], w[10], w[11]);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 48; ++e) o[e] = (uint8_t)(w[e >> 2] >> (8 * (e & 3)));
+  }
+}
+
 // one thread per output pixel: upsample every component, convert, store
-// interleaved RGB (or gray) rows of `pitch` bytes
+// interleaved RGB (or gray) rows of `pitch` bytes (STRIPE_JPEG_COLOR=1: the
+// round-4 form, kept for A/B runs)
 __global__ __launch_bounds__(256) void k_jpeg_color(JpegPlaneRef c0, JpegPlaneRef c1, JpegPlaneRef c2, int nc,
                                                     bool rgb, int W, int H, uint8_t* __restrict__ dst, int64_t pitch) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -138,6 +278,101 @@ __global__ __launch_bounds__(256) void k_jpeg_planes(const uint8_t* __restrict__
       acc += comp == 1 ? -0.168736f * r - 0.331264f * g + 0.5f * b : 0.5f * r - 0.418688f * g - 0.081312f * b;
     }
   out[i] = acc / (float)(f * f);
+}
+
+// 16 plane samples x0 .. x0 + 15 of row y from an in-frame source block of
+// 16 FS pixels x FS rows (NC channels): words of 16-byte row loads, bytes
+// picked at compile-time indices (no scratch), the per-element expressions.
+template <int NC, int FS, bool ALIGNED>
+__device__ __forceinline__ void planes_group(const uint8_t* __restrict__ src, int64_t pitch, int x0, int y, int comp,
+                                             float (&v)[16]) {
+  constexpr int NW = 16 * FS * NC / 4;  // source words per row
+  uint32_t w[FS][NW];
+#pragma unroll
+  for (int r = 0; r < FS; ++r) {
+    const uint8_t* s = src + (int64_t)(y * FS + r) * pitch + (int64_t)x0 * FS * NC;
+    if constexpr (ALIGNED) {
+#pragma unroll
+      for (int q = 0; q < NW / 4; ++q) {
+        const uint4 u = reinterpret_cast<const uint4*>(s)[q];
+        w[r][4 * q] = u.x;
+        w[r][4 * q + 1] = u.y;
+        w[r][4 * q + 2] = u.z;
+        w[r][4 * q + 3] = u.w;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < NW; ++q)
+        w[r][q] = (uint32_t)s[4 * q] | ((uint32_t)s[4 * q + 1] << 8) | ((uint32_t)s[4 * q + 2] << 16) |
+                  ((uint32_t)s[4 * q + 3] << 24);
+    }
+  }
+  auto byte = [&](int r, int e) -> float { return (float)((w[r][e >> 2] >> (8 * (e & 3))) & 0xFFu); };
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    if (comp == 0) {
+      if constexpr (NC == 1) v[j] = byte(0, j) - 128.f;
+      else v[j] = (0.299f * byte(0, 3 * j) + 0.587f * byte(0, 3 * j + 1) + 0.114f * byte(0, 3 * j + 2)) - 128.f;
+    } else {
+      float acc = 0.f;
+#pragma unroll
+      for (int dy = 0; dy < FS; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < FS; ++dx) {
+          const int e = NC * (j * FS + dx);
+          const float r = byte(dy, e), g = byte(dy, e + 1), b = byte(dy, e + 2);
+          acc += comp == 1 ? -0.168736f * r - 0.331264f * g + 0.5f * b : 0.5f * r - 0.418688f * g - 0.081312f * b;
+        }
+      v[j] = acc / (float)(FS * FS);
+    }
+  }
+}
+
+// Encode planes, 16 consecutive plane samples of one row per lane (2-D grid,
+// no 64-bit division): a group whose source pixels are all inside the frame
+// (no edge replication) reads them as 16-byte row loads (ALIGNED: source rows
+// 16-byte aligned) and stores 16 floats as four 16-byte stores; edge groups
+// replicate edge pixels element by element.  Each sample is the per-element
+// form's expression in the same order (k_jpeg_planes).
+template <bool ALIGNED>
+__global__ __launch_bounds__(256) void k_jpeg_planes16(const uint8_t* __restrict__ src, int64_t pitch, int W, int H,
+                                                       int nc, int comp, int f, int ps,
+                                                       float* __restrict__ out) {
+  const int x0 = ((int)blockIdx.x * 256 + (int)threadIdx.x) * 16;
+  const int y = (int)blockIdx.y;
+  if (x0 >= ps) return;
+  float* o = out + (int64_t)y * ps + x0;
+  auto px = [&](int xx, int yy, int c) -> float {
+    xx = min(W - 1, xx);
+    yy = min(H - 1, yy);
+    return (float)src[(int64_t)yy * pitch + (int64_t)xx * nc + c];
+  };
+  auto sample = [&](int x) -> float {
+    if (comp == 0)
+      return (nc == 1 ? px(x, y, 0) : 0.299f * px(x, y, 0) + 0.587f * px(x, y, 1) + 0.114f * px(x, y, 2)) - 128.f;
+    float acc = 0.f;
+    for (int dy = 0; dy < f; ++dy)
+      for (int dx = 0; dx < f; ++dx) {
+        const int sx = x * f + dx, sy = y * f + dy;
+        const float r = px(sx, sy, 0), g = px(sx, sy, 1), b = px(sx, sy, 2);
+        acc += comp == 1 ? -0.168736f * r - 0.331264f * g + 0.5f * b : 0.5f * r - 0.418688f * g - 0.081312f * b;
+      }
+    return acc / (float)(f * f);
+  };
+  const int fs = comp == 0 ? 1 : f;  // source pixels per sample, each way
+  const bool inside = (x0 + 16) * fs <= W && (y + 1) * fs <= H && x0 + 16 <= ps;
+  if (!inside || fs > 2 || (comp != 0 && nc != 3)) {
+    for (int j = 0; j < 16 && x0 + j < ps; ++j) o[j] = sample(x0 + j);
+    return;
+  }
+  float v[16];
+  if (comp == 0 && nc == 1) planes_group<1, 1, ALIGNED>(src, pitch, x0, y, comp, v);
+  else if (comp == 0) planes_group<3, 1, ALIGNED>(src, pitch, x0, y, comp, v);
+  else if (fs == 1) planes_group<3, 1, ALIGNED>(src, pitch, x0, y, comp, v);
+  else planes_group<3, 2, ALIGNED>(src, pitch, x0, y, comp, v);
+  float4* o4 = reinterpret_cast<float4*>(o);  // ps % 8 == 0, x0 % 16 == 0: 64-byte aligned
+#pragma unroll
+  for (int q = 0; q < 4; ++q) o4[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
 }
 
 // forward DCT + quantisation, one wave per block: F[v][u] = sum_y B[y][v]
@@ -202,6 +437,14 @@ bool pin_uploads() {
   static const bool on = [] {
     const char* e = std::getenv("STRIPE_JPEG_PIN");
     return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
+// STRIPE_JPEG_COLOR=1: the per-pixel colour / planes kernels (A/B switch)
+bool legacy_color() {
+  static const bool on = [] {
+    const char* e = std::getenv("STRIPE_JPEG_COLOR");
+    return e && std::atoi(e) == 1;
   }();
   return on;
 }
@@ -282,9 +525,18 @@ void jpeg_pixels_device(const JpegCoefs& jc, uint8_t* dst, int64_t pitch, hipStr
     ref[ci] = {planes[(size_t)ci], ps, (jc.W * c.h + jc.hmax - 1) / jc.hmax, (jc.H * c.v + jc.vmax - 1) / jc.vmax,
                jc.hmax / c.h, jc.vmax / c.v};
   }
-  const int64_t npx = (int64_t)jc.W * jc.H;
-  dev::k_jpeg_color<<<blocks_for(npx, 256), 256, 0, s>>>(ref[0], ref[nc == 3 ? 1 : 0], ref[nc == 3 ? 2 : 0], nc,
-                                                          jc.rgb, jc.W, jc.H, dst, pitch);
+  const dev::JpegPlaneRef& r1 = ref[nc == 3 ? 1 : 0];
+  const dev::JpegPlaneRef& r2 = ref[nc == 3 ? 2 : 0];
+  if (legacy_color()) {
+    const int64_t npx = (int64_t)jc.W * jc.H;
+    dev::k_jpeg_color<<<blocks_for(npx, 256), 256, 0, s>>>(ref[0], r1, r2, nc, jc.rgb, jc.W, jc.H, dst, pitch);
+  } else {
+    const dim3 grid(blocks_for(blocks_for(jc.W, 16), 256), (unsigned)jc.H);
+    if ((uintptr_t)dst % 16 == 0 && pitch % 16 == 0)
+      dev::k_jpeg_color16<true><<<grid, 256, 0, s>>>(ref[0], r1, r2, nc, jc.rgb, jc.W, dst, pitch);
+    else
+      dev::k_jpeg_color16<false><<<grid, 256, 0, s>>>(ref[0], r1, r2, nc, jc.rgb, jc.W, dst, pitch);
+  }
   HIP_CHECK(hipGetLastError());
   st.release();
 }
@@ -316,8 +568,17 @@ JpegQuant jpeg_quantise_device(const uint8_t* src, int64_t pitch, int W, int H, 
     int16_t* dcoef = nullptr;
     HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&plane), (size_t)ps * rows * sizeof(float), s));
     HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&dcoef), (size_t)nb * 64 * sizeof(int16_t), s));
-    dev::k_jpeg_planes<<<blocks_for((int64_t)ps * rows, 256), 256, 0, s>>>(src, pitch, W, H, C, ci,
-                                                                             ci == 0 ? 1 : jq.hs, ps, rows, plane);
+    const int f = ci == 0 ? 1 : jq.hs;
+    if (legacy_color()) {
+      dev::k_jpeg_planes<<<blocks_for((int64_t)ps * rows, 256), 256, 0, s>>>(src, pitch, W, H, C, ci, f, ps, rows,
+                                                                               plane);
+    } else {
+      const dim3 grid(blocks_for(blocks_for(ps, 16), 256), (unsigned)rows);
+      if ((uintptr_t)src % 16 == 0 && pitch % 16 == 0)
+        dev::k_jpeg_planes16<true><<<grid, 256, 0, s>>>(src, pitch, W, H, C, ci, f, ps, plane);
+      else
+        dev::k_jpeg_planes16<false><<<grid, 256, 0, s>>>(src, pitch, W, H, C, ci, f, ps, plane);
+    }
     HIP_CHECK(hipGetLastError());
     dev::k_jpeg_fdct<<<blocks_for(nb, 4), 256, 0, s>>>(plane, ps, nb, c.bw, dq + (ci == 0 ? 0 : 64), dcoef);
     HIP_CHECK(hipGetLastError());

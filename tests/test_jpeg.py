@@ -412,3 +412,56 @@ def test_long_scan_speculative_decode_is_exact(C, shape, subsampling):
     part = C.decode_jpeg(plain[: len(plain) * 3 // 5])
     rows = shape[0] // 3
     assert part.shape == ours.shape and np.array_equal(part[:rows], ours[:rows])
+
+
+# ---- round 5: vectorised colour / planes kernels are bit-identical to the per-pixel forms ----
+_COLOR_WORKER = r'''
+import io, os, sys, json
+import numpy as np
+sys.path.insert(0, os.environ["STRIPE_ROOT"])
+import torch
+import mpi_cuda_imagemanipulation_amd as m
+from mpi_cuda_imagemanipulation_amd._native import C
+from PIL import Image
+out = os.environ["OUT"]
+res = {}
+def smooth(h, w, c, seed):
+    rng = np.random.default_rng(seed)
+    y, x = np.mgrid[0:h, 0:w]
+    base = np.stack([128 + 100 * np.sin(x / 17.0 + k) * np.cos(y / 23.0 - k) for k in range(c)], -1)
+    img = np.clip(base + rng.normal(0, 6.0, base.shape), 0, 255).astype(np.uint8)
+    return img[..., 0] if c == 1 else img
+k = 0
+for (h, w, c) in [(211, 157, 3), (96, 512, 3), (61, 1000, 3), (64, 99, 1), (48, 256, 1), (1, 1, 3), (17, 33, 3)]:
+    for sub in ([0, 1, 2] if c == 3 else [None]):
+        img = smooth(h, w, c, k)
+        b = io.BytesIO()
+        Image.fromarray(img).save(b, "JPEG", quality=90, **({"subsampling": sub} if sub is not None else {}))
+        p = os.path.join(out, f"in{k}.jpg")
+        open(p, "wb").write(b.getvalue())
+        dec = m.utils.read_image_device(p).cpu().numpy()
+        np.save(os.path.join(out, f"dec{k}_{os.environ['TAG']}.npy"), dec)
+        q = os.path.join(out, f"enc{k}_{os.environ['TAG']}.jpg")
+        m.utils.write_image_device(q, torch.from_numpy(img).cuda(), quality=90)
+        k += 1
+print("DONE", k)
+'''
+
+
+@pytest.mark.gpu
+def test_vectorised_color_and_planes_match_per_pixel_kernels(tmp_path):
+    # k_jpeg_color16 / k_jpeg_planes16 (16 samples per lane, wide loads and
+    # stores) against the per-pixel kernels they replace (STRIPE_JPEG_COLOR=1):
+    # decoded pixels and encoded files byte for byte, over 4:4:4 / 4:2:2 /
+    # 4:2:0 / gray, widths that are and are not multiples of 16, a 1x1 frame
+    script = tmp_path / "w.py"
+    script.write_text(_COLOR_WORKER)
+    for tag, legacy in (("new", "0"), ("old", "1")):
+        env = dict(os.environ, STRIPE_ROOT=ROOT, OUT=str(tmp_path), TAG=tag, STRIPE_JPEG_COLOR=legacy)
+        r = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0 and "DONE" in r.stdout, (r.stdout + r.stderr)[-3000:]
+    n = int([ln for ln in r.stdout.splitlines() if ln.startswith("DONE")][0].split()[1])
+    for k in range(n):
+        a, b = np.load(tmp_path / f"dec{k}_new.npy"), np.load(tmp_path / f"dec{k}_old.npy")
+        assert a.shape == b.shape and np.array_equal(a, b), k
+        assert (tmp_path / f"enc{k}_new.jpg").read_bytes() == (tmp_path / f"enc{k}_old.jpg").read_bytes(), k
