@@ -95,9 +95,10 @@ __device__ __forceinline__ WaveTask task_at(const KArgs& a, int w) {
 }
 
 // The task of this wave in a one-task-per-wave launch (XCD-aware workgroup order).
+template <int NW = kWaves>
 __device__ __forceinline__ WaveTask wave_task(const KArgs& a) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  return task_at(a, xcd_remap((int)blockIdx.x, (int)gridDim.x, a.nxcd) * kWaves + wave);
+  return task_at(a, xcd_remap((int)blockIdx.x, (int)gridDim.x, a.nxcd) * NW + wave);
 }
 
 // Work queue of persistent launches (KArgs::queue, kQueueWords dwords).
@@ -253,7 +254,7 @@ __device__ __forceinline__ void load_chunk(const KArgs& a, __amdgpu_buffer_rsrc_
 
 template <int PRO>
 __device__ __forceinline__ void load_luts(const KArgs& a, uint8_t* lds) {
-  for (int i = threadIdx.x; i < 768; i += kNT) lds[i] = a.luts[i];
+  for (int i = threadIdx.x; i < 768; i += (int)blockDim.x) lds[i] = a.luts[i];
 }
 
 // Legacy skip border (kernel.cu:83 interior-only bounds): bytes of pixels in the
@@ -738,15 +739,18 @@ __device__ __forceinline__ void sep_task(const KArgs& a, const WaveTask& t, cons
 //              queue (KArgs::queue) until none is left.
 // STAMP: the per-wave timeline of KArgs::stamps (diagnostic instances,
 // tools/sepx.hip).  Both are compile-time, so the one-task instances carry
-// neither the loop nor the stamp code.
+// neither the loop nor the stamp code.  NW: waves per workgroup (one-task
+// mode; the engine launches kWaves, tools/sepx.hip's `wg` sweep varies it).
 // (skip border + expand epilogue, a rare combination: 2 VGPRs over the 128 of
 // 4 waves/SIMD with the gray prologue -> 3 waves rather than a scratch spill)
 enum KMode { kOneTask = 0, kTailBands = 1, kQueue = 2 };
-template <int C, class F, int PRO, bool SKIP, int SAUX, bool EXP = false, int MODE = kOneTask, bool STAMP = false>
-__global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : (SKIP && EXP ? 3 : 4))) void k_sep(KArgs a) {
+template <int C, class F, int PRO, bool SKIP, int SAUX, bool EXP = false, int MODE = kOneTask, bool STAMP = false,
+          int NW = kWaves>
+__global__ __launch_bounds__(NW * kW, (F::K >= 7 ? 2 : (SKIP && EXP ? 3 : 4))) void k_sep(KArgs a) {
   constexpr bool PERSIST = MODE == kQueue;
+  static_assert(NW == kWaves || MODE == kOneTask, "task modes assume kWaves-wave workgroups");
   const uint32_t t_start = STAMP ? stamp_now() : 0u;
-  __shared__ __attribute__((aligned(16))) uint4 xbuf[EXP ? kWaves : 1][EXP ? 3 * kW : 1];
+  __shared__ __attribute__((aligned(16))) uint4 xbuf[EXP ? NW : 1][EXP ? 3 * kW : 1];
   __shared__ uint8_t luts[768];
   if (PRO != PRO_NONE || a.has_epi) {
     load_luts<PRO>(a, luts);
@@ -769,10 +773,10 @@ __global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : (SKIP && EXP ? 3 : 4))) void 
     const WaveTask t = task_at<true>(a, xcd_remap((int)blockIdx.x, (int)gridDim.x, a.nxcd) * kWaves + wave);
     if (t.valid) sep_task<C, F, PRO, SKIP, SAUX, EXP>(a, t, luts, xbuf[EXP ? t.wave : 0]);
   } else {
-    const WaveTask t = wave_task(a);
+    const WaveTask t = wave_task<NW>(a);
     if (t.valid) sep_task<C, F, PRO, SKIP, SAUX, EXP>(a, t, luts, xbuf[EXP ? t.wave : 0]);
   }
-  if constexpr (STAMP) stamp_wave(a.stamps, (int)blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), t_start);
+  if constexpr (STAMP) stamp_wave(a.stamps, (int)blockIdx.x * NW + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), t_start);
 }
 
 // ------------------------------------------------------------------------------

@@ -5,7 +5,7 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Icsrc/include -Icsrc/hip \
 //         -o bin/sepx tools/sepx.hip
-//   bin/sepx [rows] [frames] [stamp_csv_prefix] [sweep: tail | policy]
+//   bin/sepx [rows] [frames] [stamp_csv_prefix] [sweep: tail | policy | sobel | wg]
 //
 // Every measurement rotates over `frames` independent in/out buffer pairs
 // (default: enough that frames x (in + out) > 3 x 256 MiB), so each launch
@@ -17,8 +17,9 @@
 // Variants (k_sep<3, Gaussian5, ...> of csrc/hip/stencil_kernels.h): store
 // policy aux 0 (default), 2 (nt), 16 (sc1 write-through), 18 (sc1 nt); band
 // height x occupancy cap x workgroup order (XCD remap); the task mode
-// (kOneTask, kTailBands, kQueue); a linear copy of the same bytes as the
-// floor.  Then per-wave stamps (KArgs::stamps) of one cold dispatch of chosen
+// (kOneTask, kTailBands, kQueue); waves per workgroup (`wg`: 1, 2 or 4 with
+// the occupancy cap held in waves per CU); a linear copy of the same bytes as
+// the floor.  Then per-wave stamps (KArgs::stamps) of one cold dispatch of chosen
 // variants: start / end spread and wave lifetime, written as CSV.
 #include <algorithm>
 #include <cstdio>
@@ -81,17 +82,26 @@ static SepFn sep_fn_flt(int saux, int mode, bool stamp) {
     default: return sep_fn_aux<C, Flt, 18>(mode, stamp);
   }
 }
-static SepFn sep_fn(int saux, int mode, bool stamp) {
+// gaussian5, nt stores, one task per wave, NW waves per workgroup
+template <int NW>
+static SepFn sep_fn_nw(bool stamp) {
+  return stamp ? k_sep<3, sdef::Gaussian5, PRO_NONE, false, 2, false, kOneTask, true, NW>
+               : k_sep<3, sdef::Gaussian5, PRO_NONE, false, 2, false, kOneTask, false, NW>;
+}
+static SepFn sep_fn(int saux, int mode, bool stamp, int nw) {
+  if (nw == 1) return sep_fn_nw<1>(stamp);
+  if (nw == 2) return sep_fn_nw<2>(stamp);
   return g_sobel ? sep_fn_flt<1, sdef::Sobel>(saux, mode, stamp) : sep_fn_flt<3, sdef::Gaussian5>(saux, mode, stamp);
 }
 
 struct SepCfg {
   int saux = 2, band = 12, cap = 2, nxcd = 0, mode = kOneTask, tail = 0;
+  int nw = kWaves;  // waves per workgroup; cap counts workgroups per CU
   std::string name() const {
     static const char* modes[] = {"one-task", "tail-bands", "queue"};
     char b[128];
-    std::snprintf(b, sizeof b, "sep aux=%2d band=%2d cap=%d xcd=%d %s tail=%d", saux, band, cap, nxcd, modes[mode],
-                  tail);
+    std::snprintf(b, sizeof b, "sep aux=%2d band=%2d cap=%d xcd=%d %s tail=%d%s", saux, band, cap, nxcd, modes[mode],
+                  tail, nw == kWaves ? "" : (" wg=" + std::to_string(nw)).c_str());
     return b;
   }
 };
@@ -120,8 +130,9 @@ static void launch_sep(const SepCfg& c, const Frame& f, hipStream_t s, uint32_t*
   a.stamps = stamps;
   const int tiles = (int)div_up(a.E, kOutChunks * 16);
   dim3 grid;
-  const SepFn fn = sep_fn(c.saux, c.mode, stamps != nullptr);
+  const SepFn fn = sep_fn(c.saux, c.mode, stamps != nullptr, c.nw);
   plan_bands(a, grid, tiles, g_rows, 0, c.band, g_sobel ? 1 : 2, 0);
+  grid.x = (unsigned)div_up((int64_t)tiles * a.nbands, c.nw);
   a.nxcd = c.nxcd;
   const size_t dyn = nt_lds_reserve((const void*)fn, c.cap);
   if (c.mode == kQueue) {
@@ -131,7 +142,7 @@ static void launch_sep(const SepCfg& c, const Frame& f, hipStream_t s, uint32_t*
     plan_tail(a, grid, (const void*)fn, dyn, c.tail);
   }
   if (grid_out) *grid_out = (int)grid.x;
-  fn<<<grid, kNT, dyn, s>>>(a);
+  fn<<<grid, c.nw * kW, dyn, s>>>(a);
 }
 
 static void launch_copy(int aux, const Frame& f, hipStream_t s) {
@@ -261,7 +272,14 @@ int main(int argc, char** argv) {
     c.tail = tail;
     cfgs.push_back(c);
   };
-  if (sweep == "sobel") {  // band x cap x order, and tail bands
+  if (sweep == "wg") {  // waves per workgroup x band, cap held at 8 / 12 waves per CU, one task per wave
+    for (int nw : {4, 2, 1})
+      for (int band : {12, 16})
+        for (int wpc : {8, 12}) {
+          add(2, band, wpc / nw, 0, kOneTask, 0);
+          cfgs.back().nw = nw;
+        }
+  } else if (sweep == "sobel") {  // band x cap x order, and tail bands
     for (int band : {4, 8, 12})
       for (int cap : {0, 2, 4})
         for (int nxcd : {0, 8}) add(0, band, cap, nxcd, kOneTask, 0);
@@ -283,7 +301,7 @@ int main(int argc, char** argv) {
   // correctness of every non-default task mode / band split: byte-equal to the
   // one-task launch (run twice: a queue must come back reset)
   for (const SepCfg& c : cfgs)
-    if (c.mode != kOneTask) {
+    if (c.mode != kOneTask || c.nw != kWaves) {
       const int64_t bad = check_same(c);
       std::printf("# %s vs one-task: %lld differing bytes\n", c.name().c_str(), (long long)bad);
       if (bad) return 2;
@@ -295,13 +313,20 @@ int main(int argc, char** argv) {
 
   // per-wave timeline of one cold dispatch (the last of a rotation)
   std::vector<SepCfg> stamped(3);
-  if (g_sobel)
+  if (sweep == "wg") {
+    stamped[0].band = stamped[1].band = stamped[2].band = 16;
+    stamped[1].nw = 2;
+    stamped[1].cap = 4;
+    stamped[2].nw = 1;
+    stamped[2].cap = 8;
+  } else if (g_sobel)
     for (auto& c : stamped) {
       c.saux = 0;
       c.cap = 0;
       c.nxcd = 8;
     }
-  if (g_sobel) {
+  if (sweep == "wg") {
+  } else if (g_sobel) {
     stamped[0].band = 4;
     stamped[1].band = 8;
     stamped[2].band = 12;
@@ -318,7 +343,7 @@ int main(int argc, char** argv) {
     int grid = 0;
     for (int i = 0; i < F; ++i) launch_sep(c, g_frames[i], st[0], nullptr, &grid);
     uint32_t* ds = nullptr;
-    const size_t nw = (size_t)grid * kWaves;
+    const size_t nw = (size_t)grid * c.nw;
     CK(hipMalloc(&ds, nw * 16));
     CK(hipMemset(ds, 0, nw * 16));
     launch_sep(c, g_frames[0], st[0], ds);
