@@ -30,6 +30,7 @@ struct Msg {
   int src_dev = -1;
   hipEvent_t ready = nullptr;  // recorded on the sender's stream (device mode)
   hipEvent_t done = nullptr;   // recorded on the receiver's stream after the copy
+  bool own_done = false;       // `done` created by a receiver on another device
   bool consumed = false;
 };
 
@@ -126,8 +127,17 @@ class LocalComm final : public Comm {
     m->bytes = bytes;
     if (hub_->device()) {
       HIP_CHECK(hipGetDevice(&m->src_dev));
-      HIP_CHECK(hipEventCreateWithFlags(&m->ready, hipEventDisableTiming));
-      HIP_CHECK(hipEventRecord(m->ready, s));
+      // one `ready` record per stream and group (the halo exchange sends both
+      // edges from one stream); `done` is recorded by the receiver
+      for (const auto& sd : sends_)
+        if (sd.s == s) m->ready = sd.m->ready;
+      if (!m->ready) {
+        m->ready = take_event();
+        HIP_CHECK(hipEventRecord(m->ready, s));
+        group_events_.push_back(m->ready);
+      }
+      m->done = take_event();
+      group_events_.push_back(m->done);
     }
     hub_->post(rank_, peer, m);
     sends_.push_back({m, peer, s});
@@ -145,8 +155,24 @@ class LocalComm final : public Comm {
   }
   void barrier() override { hub_->barrier(); }
   void abort(const std::string& why) override { hub_->abort(why); }
+  ~LocalComm() override {
+    for (hipEvent_t e : free_events_) (void)hipEventDestroy(e);
+  }
 
  private:
+  // Events come from a per-rank pool and go back once every wait on them is
+  // enqueued (a create + destroy pair per message cost ~10 HIP calls a rank per
+  // halo exchange, with 4 rank threads contending for the runtime).
+  hipEvent_t take_event() {
+    if (!free_events_.empty()) {
+      hipEvent_t e = free_events_.back();
+      free_events_.pop_back();
+      return e;
+    }
+    hipEvent_t e = nullptr;
+    HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return e;
+  }
   struct PendingSend {
     std::shared_ptr<Msg> m;
     int peer;
@@ -163,20 +189,27 @@ class LocalComm final : public Comm {
   }
   void group_end_impl() {
     try {
+      int dev = 0;
+      if (hub_->device() && !recvs_.empty()) HIP_CHECK(hipGetDevice(&dev));
+      hipStream_t waited_s = nullptr;
+      hipEvent_t waited_e = nullptr;
       for (auto& r : recvs_) {
         auto m = hub_->take(r.peer, rank_);
         STRIPE_CHECK(m->bytes == r.bytes, "size mismatch: rank " << r.peer << " sent " << m->bytes
                                                                  << " B, rank " << rank_ << " expects " << r.bytes);
         if (hub_->device()) {
-          int dev = 0;
-          HIP_CHECK(hipGetDevice(&dev));
-          HIP_CHECK(hipStreamWaitEvent(r.s, m->ready, 0));
+          if (r.s != waited_s || m->ready != waited_e) HIP_CHECK(hipStreamWaitEvent(r.s, m->ready, 0));
+          waited_s = r.s;
+          waited_e = m->ready;
           if (m->src_dev == dev)
             HIP_CHECK(hipMemcpyAsync(r.buf, m->ptr, r.bytes, hipMemcpyDeviceToDevice, r.s));
           else
             HIP_CHECK(hipMemcpyPeerAsync(r.buf, dev, m->ptr, m->src_dev, r.bytes, r.s));
-          HIP_CHECK(hipEventCreateWithFlags(&m->done, hipEventDisableTiming));
-          HIP_CHECK(hipEventRecord(m->done, r.s));
+          if (m->src_dev != dev) {  // an event is recorded on its own device's streams only
+            HIP_CHECK(hipEventCreateWithFlags(&m->done, hipEventDisableTiming));
+            m->own_done = true;
+          }
+          HIP_CHECK(hipEventRecord(m->done, r.s));  // the sender's pooled event, same device
         } else {
           std::memcpy(r.buf, m->ptr, r.bytes);
         }
@@ -187,12 +220,13 @@ class LocalComm final : public Comm {
         hub_->wait_consumed(sd.m, sd.peer);
         if (hub_->device()) {
           HIP_CHECK(hipStreamWaitEvent(sd.s, sd.m->done, 0));
-          // the events may be destroyed once enqueued waits reference them
-          HIP_CHECK(hipEventDestroy(sd.m->ready));
-          HIP_CHECK(hipEventDestroy(sd.m->done));
+          if (sd.m->own_done) HIP_CHECK(hipEventDestroy(sd.m->done));
         }
       }
       sends_.clear();
+      // every wait on this group's events is enqueued: they may be re-recorded
+      free_events_.insert(free_events_.end(), group_events_.begin(), group_events_.end());
+      group_events_.clear();
     } catch (const std::exception& e) {
       hub_->abort(std::string("rank ") + std::to_string(rank_) + ": " + e.what());
       throw;
@@ -204,6 +238,8 @@ class LocalComm final : public Comm {
   bool in_group_ = false;
   std::vector<PendingSend> sends_;
   std::vector<PendingRecv> recvs_;
+  std::vector<hipEvent_t> free_events_;   // pooled, unreferenced
+  std::vector<hipEvent_t> group_events_;  // taken by the open group's sends
 };
 
 class CallbackComm final : public Comm {
