@@ -291,6 +291,16 @@ __host__ __device__ constexpr int convq_rows_staged(int nq) {
   return (16 * MT + 4 * nq + (C == 3 ? 3 : 9) - 1) / (C == 3 ? 3 : 9) * (C == 3 ? 3 : 9);
 }
 
+// LDS bytes of one staging buffer of the i8 kernel: the planes, or the output
+// tile the epilogue re-tiles through the same space (16-byte multiple)
+template <int C, int MT>
+__host__ __device__ constexpr int convq_buf_bytes(int nq) {
+  return ((C * convq_rows_staged<C, MT>(nq) * kQPS > 16 * MT * (kCTN * C + 16)
+               ? C * convq_rows_staged<C, MT>(nq) * kQPS
+               : 16 * MT * (kCTN * C + 16)) +
+          15) / 16 * 16;
+}
+
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 struct ConvI8Args {
@@ -302,72 +312,91 @@ struct ConvI8Args {
 
 // ND weight digits: 3 (24-bit weights, the exact default) or 2 (16-bit,
 // "conv:K:w..:lsb": every output within 1 LSB of the f64 result, 2/3 of the
-// MFMAs and accumulators)
-template <int C, int MT, int ND>
+// MFMAs and accumulators).
+// NT output tiles (16 MT rows each, one above the other) per workgroup.  With
+// NT > 1 the planes are double-buffered: while the MFMA loop of tile i reads
+// one buffer, the waves stage tile i + 1's window into the other in kG / kBatch
+// batches (a batch's loads are issued right after a k-step's B loads and
+// written three k-steps later, so the in-order vmcnt drain of the B ring never
+// waits on a fresh HBM load), and the epilogue of tile i re-tiles its output
+// through the buffer tile i has finished with.  NT = 1 (the default) stages,
+// computes and stores one tile: 75 % MFMA busy on 16K conv:31, and still
+// faster than NT = 4, which fits the registers only at 2 m-tiles
+// (profiles/r5/conv/README.md).
+template <int C, int MT, int ND, int NT = 1>
 __global__ __launch_bounds__(256, 2) void k_conv_i8(ConvI8Args ca) {
   const KArgs& a = ca.a;
   const int R = ca.R, nq = ca.nq;
-  extern __shared__ __attribute__((aligned(16))) uint8_t qplane[];  // [C][rows_in][kQPS]
+  extern __shared__ __attribute__((aligned(16))) uint8_t qplane[];  // NT buffers of [C][rows_in][kQPS] (or the output tile)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int x0 = blockIdx.x * kCTN;
-  const int yb = a.ry0 + blockIdx.y * (16 * MT);
-  if (yb >= a.ry1) return;
+  const int yb0 = a.ry0 + blockIdx.y * (NT * 16 * MT);
+  if (yb0 >= a.ry1) return;
   const int rows_in = convq_rows_staged<C, MT>(nq);
   const int pstride = rows_in * kQPS;
+  constexpr int kOS = kCTN * C + 16;
+  const int bufsz = convq_buf_bytes<C, MT>(nq);
 
-  // ---- stage pixels [x0 - 16, x0 + 80) of rows yb - R .. as x - 128 ----
+  // ---- staging: pixels [x0 - 16, x0 + 80) of rows yb - R .. as x - 128 ----
   // The window starts 16 pixels left of the tile (not R): its first byte is
   // then 16-byte aligned for RGB and gray alike (3 (x0 - 16) = 192 k - 48), so
   // RGB goes in as 12-byte units (4 pixels) de-interleaved by byte permutes
   // (6 perms + 3 dword stores per unit instead of 12 byte stores) and gray as
   // 16-byte rows pieces; the taps shift by 16 - R in the B fragments.
-  {
-    const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);
-    constexpr int UB = C == 3 ? 12 : 16;              // bytes per unit
-    constexpr int U = kCWin * C / UB;                  // units per staged row: 24 (RGB) / 6 (gray)
-    constexpr int kMaxRows = convq_rows_staged<C, MT>(10);  // K <= 33
-    constexpr int kG = (kMaxRows * U + 255) / 256;     // unit loads per thread
-    const int nunits = rows_in * U;
-    const bool inner = rows_inside(a, yb - R, a.ry1 - 1 + R);
-    const uint32_t colb = (uint32_t)((x0 - 16) * C);
-    typedef uint32_t u3 __attribute__((ext_vector_type(3)));
-    typedef uint32_t u4v __attribute__((ext_vector_type(4)));
-    typedef std::conditional_t<C == 3, u3, u4v> unit_t;
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);
+  constexpr int UB = C == 3 ? 12 : 16;              // bytes per unit
+  constexpr int U = kCWin * C / UB;                  // units per staged row: 24 (RGB) / 6 (gray)
+  constexpr int kMaxRows = convq_rows_staged<C, MT>(10);  // K <= 33
+  constexpr int kG = (kMaxRows * U + 255) / 256;     // unit loads per thread
+  constexpr int kBatch = (kG + 2) / 3;               // units per staging batch (NT > 1)
+  constexpr int kNB = (kG + kBatch - 1) / kBatch;    // batches
+  const int nunits = rows_in * U;
+  const uint32_t colb = (uint32_t)((x0 - 16) * C);
+  typedef uint32_t u3 __attribute__((ext_vector_type(3)));
+  typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+  typedef std::conditional_t<C == 3, u3, u4v> unit_t;
+  // load of unit u of the tile whose first output row is yb (rows past the last
+  // needed input row feed only unstored outputs / zero weights: clamped, so no
+  // read leaves the stripe + halo; units past the window: masked)
+  auto load_unit = [&](int yb, bool inner, int u) __attribute__((always_inline)) {
+    const int r = u / U, k = u % U;
+    const int y = min(yb - R + r, a.ry1 - 1 + R);
+    const uint32_t roff = inner ? a.in_org + (uint32_t)((int64_t)y * a.in_pitch) : in_row_off(a, y);
+    const uint32_t off = u < nunits ? roff + colb + (uint32_t)(UB * k) : kOOB;
+    if constexpr (C == 3) return __builtin_amdgcn_raw_buffer_load_b96(rin, off, 0, 0);
+    else return __builtin_amdgcn_raw_buffer_load_b128(rin, off, 0, 0);
+  };
+  auto store_unit = [&](uint8_t* planes, int u, const unit_t& v) __attribute__((always_inline)) {
+    const int r = u / U, k = u % U;
+    if constexpr (C == 3) {
+      // R0 G0 B0 R1 | G1 B1 R2 G2 | B2 R3 G3 B3 -> R0..R3, G0..G3, B0..B3 (x - 128)
+      const uint32_t d0 = v.x ^ 0x80808080u, d1 = v.y ^ 0x80808080u, d2 = v.z ^ 0x80808080u;
+      const uint32_t p01 = __builtin_amdgcn_perm(d1, d0, 0x04010300u);  // R0 R1 G0 G1
+      const uint32_t p12 = __builtin_amdgcn_perm(d2, d1, 0x06030502u);  // R2 R3 G2 G3
+      const uint32_t rr = __builtin_amdgcn_perm(p12, p01, 0x05040100u);
+      const uint32_t gg = __builtin_amdgcn_perm(p12, p01, 0x07060302u);
+      const uint32_t pb = __builtin_amdgcn_perm(d2, d1, 0x07040401u);   // B1 B2 -- B3
+      const uint32_t bb = __builtin_amdgcn_perm(pb, d0, 0x07050402u);   // B0 B1 B2 B3
+      uint8_t* row = planes + r * kQPS + 4 * k;
+      *reinterpret_cast<uint32_t*>(row) = rr;
+      *reinterpret_cast<uint32_t*>(row + pstride) = gg;
+      *reinterpret_cast<uint32_t*>(row + 2 * pstride) = bb;
+    } else {
+      *reinterpret_cast<u4v*>(planes + r * kQPS + 16 * k) = v ^ 0x80808080u;
+    }
+  };
+  auto inner_of = [&](int yb) { return rows_inside(a, yb - R, a.ry1 - 1 + R); };
+  {  // the first tile, before any MFMA
+    const bool inner = inner_of(yb0);
     unit_t d[kG];
 #pragma unroll
-    for (int i = 0; i < kG; ++i) {
-      const int u = tid + 256 * i;
-      const int r = u / U, k = u % U;
-      // rows past the last needed input row feed only unstored outputs / zero
-      // weights: clamp so no read leaves the stripe + halo
-      const int y = min(yb - R + r, a.ry1 - 1 + R);
-      const uint32_t roff = inner ? a.in_org + (uint32_t)((int64_t)y * a.in_pitch) : in_row_off(a, y);
-      const uint32_t off = u < nunits ? roff + colb + (uint32_t)(UB * k) : kOOB;
-      if constexpr (C == 3) d[i] = __builtin_amdgcn_raw_buffer_load_b96(rin, off, 0, 0);
-      else d[i] = __builtin_amdgcn_raw_buffer_load_b128(rin, off, 0, 0);
-    }
+    for (int i = 0; i < kG; ++i) d[i] = load_unit(yb0, inner, tid + 256 * i);
 #pragma unroll
     for (int i = 0; i < kG; ++i) {
       const int u = tid + 256 * i;
       if (u >= nunits) break;  // lane-divergent only in the last load
-      const int r = u / U, k = u % U;
-      if constexpr (C == 3) {
-        // R0 G0 B0 R1 | G1 B1 R2 G2 | B2 R3 G3 B3 -> R0..R3, G0..G3, B0..B3 (x - 128)
-        const uint32_t d0 = d[i].x ^ 0x80808080u, d1 = d[i].y ^ 0x80808080u, d2 = d[i].z ^ 0x80808080u;
-        const uint32_t p01 = __builtin_amdgcn_perm(d1, d0, 0x04010300u);  // R0 R1 G0 G1
-        const uint32_t p12 = __builtin_amdgcn_perm(d2, d1, 0x06030502u);  // R2 R3 G2 G3
-        const uint32_t rr = __builtin_amdgcn_perm(p12, p01, 0x05040100u);
-        const uint32_t gg = __builtin_amdgcn_perm(p12, p01, 0x07060302u);
-        const uint32_t pb = __builtin_amdgcn_perm(d2, d1, 0x07040401u);   // B1 B2 -- B3
-        const uint32_t bb = __builtin_amdgcn_perm(pb, d0, 0x07050402u);   // B0 B1 B2 B3
-        uint8_t* row = qplane + r * kQPS + 4 * k;
-        *reinterpret_cast<uint32_t*>(row) = rr;
-        *reinterpret_cast<uint32_t*>(row + pstride) = gg;
-        *reinterpret_cast<uint32_t*>(row + 2 * pstride) = bb;
-      } else {
-        *reinterpret_cast<u4v*>(qplane + r * kQPS + 16 * k) = d[i] ^ 0x80808080u;
-      }
+      store_unit(qplane, u, d[i]);
     }
   }
   __syncthreads();
@@ -380,109 +409,147 @@ __global__ __launch_bounds__(256, 2) void k_conv_i8(ConvI8Args ca) {
     const int e = 4 * s + g;
     aoff[s] = (m + e / 3) * kQPS + 16 * (e % 3) + 16 * wave;
   }
-
-  i32x4 acc[ND][C][MT];
-#pragma unroll
-  for (int d = 0; d < ND; ++d)
-#pragma unroll
-    for (int c = 0; c < C; ++c)
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) acc[d][c][mt] = i32x4{0, 0, 0, 0};
-
-  // k-step stream t = 3 q + s: B(t) (3 digits) through a 3-slot register ring
+  // k-step stream t = 3 q + s: B(t) (ND digits) through a 3-slot register ring
   // two steps ahead, A(t + 1) read from the planes while step t multiplies
   const __amdgpu_buffer_rsrc_t rtw = make_rsrc(ca.tw, (uint32_t)nq * 3u * ND * 1024u);
   const uint32_t tl = 16u * (uint32_t)lane;
   const int nsteps = 3 * nq;
-  i32x4 bq[3][ND];
-  auto load_b = [&](int t, int slot) __attribute__((always_inline)) {
-    const uint32_t off = (uint32_t)min(t, nsteps - 1) * (ND * 1024u) + tl;  // past the end: re-read (unused)
-#pragma unroll
-    for (int dg = 0; dg < ND; ++dg)
-      bq[slot][dg] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(rtw, off + 1024u * dg, 0, 0));
-  };
-  i32x4 af[2][C][MT];
-  auto read_a = [&](int q, int s, int buf) __attribute__((always_inline)) {
-    const uint8_t* pl = qplane + 4 * q * kQPS + aoff[s];
-#pragma unroll
-    for (int c = 0; c < C; ++c)
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-        af[buf][c][mt] = *reinterpret_cast<const i32x4*>(pl + c * pstride + 16 * mt * kQPS);
-  };
-  load_b(0, 0);
-  load_b(1, 1);
-  read_a(0, 0, 0);
-  // 6 steps = 2 quads per body (nq is even: the host pads a zero-weight quad)
-  for (int q0 = 0; q0 < nsteps; q0 += 6) {
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      const int t = q0 + i;
-      load_b(t + 2, (i + 2) % 3);
-      read_a(min((q0 / 3) + (i + 1) / 3, nq - 1), (i + 1) % 3, (i + 1) & 1);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int dg = 0; dg < ND; ++dg)
-#pragma unroll
-        for (int c = 0; c < C; ++c)
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-            acc[dg][c][mt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[i & 1][c][mt], bq[i % 3][dg], acc[dg][c][mt], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  __syncthreads();  // every wave's last fragment read before the planes are reused
-
-  // ---- epilogue: sum(x W) exactly in f64, * 2^-S, round half even, saturate;
-  // the tile leaves through LDS as 16-byte row chunks ----
-  constexpr int kOS = kCTN * C + 16;
-  uint8_t* otile = qplane;
+  const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
+  const int E = a.W * C;
   const float s0 = (float)ca.scale, s1 = (float)(ca.scale * 256.0), s2 = (float)(ca.scale * 65536.0);
   const float bias = (float)ca.bias;
+
+#pragma nounroll
+  for (int it = 0; it < NT; ++it) {
+    const int yb = yb0 + it * (16 * MT);
+    if (yb >= a.ry1) break;  // workgroup-uniform
+    uint8_t* cur = qplane + (it & 1) * bufsz;
+    uint8_t* nxt = qplane + ((it + 1) & 1) * bufsz;
+    const int ybn = yb + 16 * MT;
+    const bool more = NT > 1 && it + 1 < NT && ybn < a.ry1;
+    const bool inner_n = more && inner_of(ybn);
+
+    i32x4 acc[ND][C][MT];
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
+    for (int d = 0; d < ND; ++d)
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+      for (int c = 0; c < C; ++c)
 #pragma unroll
-      for (int c = 0; c < C; ++c) {
-        // a digit sum |D| <= K^2 * 128 * 128 reaches 1.78e7 > 2^24 at K = 33,
-        // so each goes to f32 as two exact parts (D - (D & 255) keeps <= 17
-        // significant bits, D & 255 <= 8); the scales are powers of two, the
-        // f32 FMAs round the result to ~2^-15 (an output changes only within
-        // ~1e-4 of a tie), and v_cvt_pk_u8_f32 rounds half to even and saturates
-        auto part = [&](int d, float s, float acc_in) __attribute__((always_inline)) {
-          const int D = acc[d][c][mt][r];
-          const int lo8 = D & 255;
-          return __builtin_fmaf((float)(D - lo8), s, __builtin_fmaf((float)lo8, s, acc_in));
-        };
-        const float lo2 = part(1, s1, part(0, s0, bias));
-        const float v = ND == 3 ? part(ND - 1, s2, lo2) : lo2;
-        otile[(16 * mt + 4 * g + r) * kOS + (16 * wave + m) * C + c] = (uint8_t)__builtin_amdgcn_cvt_pk_u8_f32(v, 0, 0u);
-      }
-  __syncthreads();
-  const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
-  constexpr int NCO = kCTN * C / 16;
-  const int E = a.W * C;
+        for (int mt = 0; mt < MT; ++mt) acc[d][c][mt] = i32x4{0, 0, 0, 0};
+    i32x4 bq[3][ND];
+    auto load_b = [&](int t, int slot) __attribute__((always_inline)) {
+      const uint32_t off = (uint32_t)min(t, nsteps - 1) * (ND * 1024u) + tl;  // past the end: re-read (unused)
 #pragma unroll
-  for (int k = 0; k < (16 * MT * NCO + 255) / 256; ++k) {
-    const int q = tid + 256 * k;
-    if (q >= 16 * MT * NCO) break;
-    const int row = q / NCO, ch = q % NCO;
-    const int y = yb + row;
-    const int b = x0 * C + 16 * ch;
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    const u32x4 v = *reinterpret_cast<const u32x4*>(otile + row * kOS + 16 * ch);
-    const uint32_t roff = a.out_org + (uint32_t)((int64_t)y * a.out_pitch) + (uint32_t)b;
-    if (y < a.ry1) {
-      if (b + 16 <= E) {
-        __builtin_amdgcn_raw_buffer_store_b128(v, rout, roff, 0, 0);
-      } else if (b < E) {
+      for (int dg = 0; dg < ND; ++dg)
+        bq[slot][dg] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(rtw, off + 1024u * dg, 0, 0));
+    };
+    i32x4 af[2][C][MT];
+    auto read_a = [&](int q, int s, int buf) __attribute__((always_inline)) {
+      const uint8_t* pl = cur + 4 * q * kQPS + aoff[s];
 #pragma unroll
-        for (int i = 0; i < 16; ++i)
-          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v[i >> 2] >> (8 * (i & 3))), rout,
-                                               b + i < E ? roff + (uint32_t)i : kOOB, 0, 0);
+      for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+          af[buf][c][mt] = *reinterpret_cast<const i32x4*>(pl + c * pstride + 16 * mt * kQPS);
+    };
+    unit_t sb[kBatch];  // the staging batch in flight (NT > 1)
+    load_b(0, 0);
+    load_b(1, 1);
+    read_a(0, 0, 0);
+    // 6 steps = 2 quads per body (nq is even: the host pads a zero-weight quad)
+#pragma nounroll
+    for (int q0 = 0; q0 < nsteps; q0 += 6) {
+      const int j = q0 / 6;  // body index: staging batch j rides on body j
+      const bool stage = NT > 1 && more && j < kNB;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const int t = q0 + i;
+        load_b(t + 2, (i + 2) % 3);
+        if (NT > 1 && i == 0 && stage) {
+#pragma unroll
+          for (int b = 0; b < kBatch; ++b) sb[b] = load_unit(ybn, inner_n, tid + 256 * (j * kBatch + b));
+        }
+        if (NT > 1 && i == 3 && stage) {
+#pragma unroll
+          for (int b = 0; b < kBatch; ++b) {
+            const int u = tid + 256 * (j * kBatch + b);
+            if (j * kBatch + b < kG && u < nunits) store_unit(nxt, u, sb[b]);
+          }
+        }
+        read_a(min((q0 / 3) + (i + 1) / 3, nq - 1), (i + 1) % 3, (i + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int dg = 0; dg < ND; ++dg)
+#pragma unroll
+          for (int c = 0; c < C; ++c)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+              acc[dg][c][mt] =
+                  __builtin_amdgcn_mfma_i32_16x16x64_i8(af[i & 1][c][mt], bq[i % 3][dg], acc[dg][c][mt], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
+    if constexpr (NT > 1) {
+      // batches the loop had no body for (short windows): staged here
+      for (int j = nsteps / 6; more && j < kNB; ++j) {
+#pragma unroll
+        for (int b = 0; b < kBatch; ++b) sb[b] = load_unit(ybn, inner_n, tid + 256 * (j * kBatch + b));
+#pragma unroll
+        for (int b = 0; b < kBatch; ++b) {
+          const int u = tid + 256 * (j * kBatch + b);
+          if (j * kBatch + b < kG && u < nunits) store_unit(nxt, u, sb[b]);
+        }
+      }
+    }
+    __syncthreads();  // every wave's last fragment read of `cur` (and staging write of `nxt`) is done
+
+    // ---- epilogue: sum(x W) exactly in f64, * 2^-S, round half even, saturate;
+    // the tile leaves through LDS (`cur`, done with) as 16-byte row chunks ----
+    uint8_t* otile = cur;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          // a digit sum |D| <= K^2 * 128 * 128 reaches 1.78e7 > 2^24 at K = 33,
+          // so each goes to f32 as two exact parts (D - (D & 255) keeps <= 17
+          // significant bits, D & 255 <= 8); the scales are powers of two, the
+          // f32 FMAs round the result to ~2^-15 (an output changes only within
+          // ~1e-4 of a tie), and v_cvt_pk_u8_f32 rounds half to even and saturates
+          auto part = [&](int d, float s, float acc_in) __attribute__((always_inline)) {
+            const int D = acc[d][c][mt][r];
+            const int lo8 = D & 255;
+            return __builtin_fmaf((float)(D - lo8), s, __builtin_fmaf((float)lo8, s, acc_in));
+          };
+          const float lo2 = part(1, s1, part(0, s0, bias));
+          const float v = ND == 3 ? part(ND - 1, s2, lo2) : lo2;
+          otile[(16 * mt + 4 * g + r) * kOS + (16 * wave + m) * C + c] = (uint8_t)__builtin_amdgcn_cvt_pk_u8_f32(v, 0, 0u);
+        }
+    __syncthreads();
+    constexpr int NCO = kCTN * C / 16;
+#pragma unroll
+    for (int k = 0; k < (16 * MT * NCO + 255) / 256; ++k) {
+      const int q = tid + 256 * k;
+      if (q >= 16 * MT * NCO) break;
+      const int row = q / NCO, ch = q % NCO;
+      const int y = yb + row;
+      const int b = x0 * C + 16 * ch;
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 v = *reinterpret_cast<const u32x4*>(otile + row * kOS + 16 * ch);
+      const uint32_t roff = a.out_org + (uint32_t)((int64_t)y * a.out_pitch) + (uint32_t)b;
+      if (y < a.ry1) {
+        if (b + 16 <= E) {
+          __builtin_amdgcn_raw_buffer_store_b128(v, rout, roff, 0, 0);
+        } else if (b < E) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v[i >> 2] >> (8 * (i & 3))), rout,
+                                                 b + i < E ? roff + (uint32_t)i : kOOB, 0, 0);
+        }
+      }
+    }
+    if (NT > 1) __syncthreads();  // `cur` (the output tile) read before the next tile stages into it
   }
 }
 
@@ -690,27 +757,40 @@ void launch_conv_mfma(const Pass& p, const PassConsts& pc, const PassLaunch& L, 
     }();
     int mt = p.cmid == 3 ? dev::convq_mt<3>() : dev::convq_mt<1>();
     if (env_mt > 0) mt = env_mt;
+    // output tiles per workgroup: 1, or 4 with STRIPE_CONV_NT=4 (the next
+    // tile's staging under the current tile's MFMAs, k_conv_i8 NT).  Measured
+    // on 16K RGB conv:31 (profiles/r5/conv/): 4 tiles at 2 m-tiles 2.32-2.36 ms
+    // exact / 1.85 ms lsb against 2.09-2.10 / 1.54-1.55 ms for one tile at 3
+    // m-tiles (4 tiles at 3 m-tiles spill): one tile stays the default
+    static const int env_nt = [] {
+      const char* e = std::getenv("STRIPE_CONV_NT");
+      return e ? std::atoi(e) : 0;
+    }();
+    const int nt = env_nt >= 4 ? 4 : 1;
     using KFn = void (*)(dev::ConvI8Args);
     KFn fn = nullptr;
-    int rows_in = 0;
-#define STRIPE_CONVQ(CC, MM, DD)                                     \
-    if (p.cmid == CC && mt == MM && nd == DD) {                      \
-      fn = dev::k_conv_i8<CC, MM, DD>;                               \
-      rows_in = dev::convq_rows_staged<CC, MM>(ci.nq);               \
+    size_t lds = 0;
+    // (multi-tile instances only where they stay spill-free: RGB at 2
+    // m-tiles, gray at 4 or 6)
+    if (nt == 4) mt = p.cmid == 3 ? 2 : std::min(mt, 6);
+#define STRIPE_CONVQ(CC, MM, DD, NT)                                                                         \
+    if (p.cmid == CC && mt == MM && nd == DD && nt == NT) {                                                  \
+      fn = dev::k_conv_i8<CC, MM, DD, NT>;                                                                   \
+      lds = (size_t)(NT > 1 ? 2 : 1) * dev::convq_buf_bytes<CC, MM>(ci.nq);                                  \
     }
-    STRIPE_CONVQ(3, 2, 3) STRIPE_CONVQ(3, 3, 3) STRIPE_CONVQ(1, 4, 3) STRIPE_CONVQ(1, 6, 3) STRIPE_CONVQ(1, 8, 3)
-    STRIPE_CONVQ(3, 2, 2) STRIPE_CONVQ(3, 3, 2) STRIPE_CONVQ(1, 6, 2)
+    STRIPE_CONVQ(3, 2, 3, 1) STRIPE_CONVQ(3, 3, 3, 1) STRIPE_CONVQ(1, 4, 3, 1) STRIPE_CONVQ(1, 6, 3, 1)
+    STRIPE_CONVQ(1, 8, 3, 1) STRIPE_CONVQ(3, 2, 2, 1) STRIPE_CONVQ(3, 3, 2, 1) STRIPE_CONVQ(1, 6, 2, 1)
+    STRIPE_CONVQ(3, 2, 3, 4) STRIPE_CONVQ(3, 2, 2, 4) STRIPE_CONVQ(1, 4, 3, 4) STRIPE_CONVQ(1, 6, 3, 4)
+    STRIPE_CONVQ(1, 6, 2, 4)
 #undef STRIPE_CONVQ
     STRIPE_CHECK(fn != nullptr, "no i8 conv kernel for " << p.cmid << " channels x " << mt << " m-tiles x " << nd
                                                           << " digits");
-    const size_t lds = std::max((size_t)p.cmid * rows_in * dev::kQPS,  // planes
-                                (size_t)16 * mt * (dev::kCTN * p.cmid + 16));  // output tile
     for (int r = 0; r < L.nrange; ++r) {
       const int y0 = L.ry[2 * r], y1 = L.ry[2 * r + 1];
       if (y1 <= y0) continue;
       a.ry0 = y0;
       a.ry1 = y1;
-      const dim3 grid((unsigned)div_up(L.W, dev::kCTN), (unsigned)div_up(y1 - y0, 16 * mt));
+      const dim3 grid((unsigned)div_up(L.W, dev::kCTN), (unsigned)div_up(div_up(y1 - y0, 16 * mt), nt));
       fn<<<grid, 256, lds, s>>>(ci);
       HIP_CHECK(hipGetLastError());
     }

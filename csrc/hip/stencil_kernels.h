@@ -740,7 +740,9 @@ __device__ __forceinline__ void sep_task(const KArgs& a, const WaveTask& t, cons
 // STAMP: the per-wave timeline of KArgs::stamps (diagnostic instances,
 // tools/sepx.hip).  Both are compile-time, so the one-task instances carry
 // neither the loop nor the stamp code.  NW: waves per workgroup (one-task
-// mode; the engine launches kWaves, tools/sepx.hip's `wg` sweep varies it).
+// mode; the engine launches kWaves: one- and two-wave workgroups at the same
+// waves per CU were 4-7 % slower on the cold share and the 16K frame,
+// tools/sepx.hip `wg` sweep, profiles/r5/cold/sepx_wg_*.txt).
 // (skip border + expand epilogue, a rare combination: 2 VGPRs over the 128 of
 // 4 waves/SIMD with the gray prologue -> 3 waves rather than a scratch spill)
 enum KMode { kOneTask = 0, kTailBands = 1, kQueue = 2 };
@@ -1030,34 +1032,10 @@ inline int stencil_cap(bool nt, int wgs, int family_default) {
   return nt ? family_default : 0;
 }
 
-// Waves per workgroup of the plain (no prologue / expand) separable launches:
-// kWaves, or 1 with STRIPE_SEP_NW=1 (A/B runs; the occupancy cap is then
-// scaled to the same waves per CU).
-inline int env_sep_nw() {
-  static const int v = [] {
-    const char* e = std::getenv("STRIPE_SEP_NW");
-    return e && std::atoi(e) == 1 ? 1 : kWaves;
-  }();
-  return v;
-}
-
 template <int C, class F, int PRO, bool EXP = false>
 void launch_one(bool skip, bool nt, int wgs, KArgs a, int tiles, int n0, int n1, int band, hipStream_t s) {
   using K = void (*)(KArgs);
   dim3 grid;
-  if constexpr (F::SEP && PRO == PRO_NONE && !EXP) {
-    if (env_sep_nw() == 1) {
-      const K fns[4] = {k_sep<C, F, PRO, false, 0, EXP, kOneTask, false, 1>,
-                        k_sep<C, F, PRO, false, kNtAux, EXP, kOneTask, false, 1>,
-                        k_sep<C, F, PRO, true, 0, EXP, kOneTask, false, 1>,
-                        k_sep<C, F, PRO, true, kNtAux, EXP, kOneTask, false, 1>};
-      const K fn = fns[2 * skip + nt];
-      plan_bands(a, grid, tiles, n0, n1, band, F::R, 0);
-      grid = dim3((unsigned)((int64_t)tiles * a.nbands));
-      fn<<<grid, kW, nt_lds_reserve((const void*)fn, kWaves * stencil_cap(nt, wgs, kNtWgsSep)), s>>>(a);
-      return;
-    }
-  }
   if constexpr (F::SEP) {
     const K fns[4] = {k_sep<C, F, PRO, false, 0, EXP>, k_sep<C, F, PRO, false, kNtAux, EXP>,
                       k_sep<C, F, PRO, true, 0, EXP>, k_sep<C, F, PRO, true, kNtAux, EXP>};

@@ -43,7 +43,7 @@ class LocalHub {
   void post(int src, int dst, const std::shared_ptr<Msg>& m) {
     std::lock_guard<std::mutex> lk(mu_);
     box_[{src, dst}].push_back(m);
-    cv_.notify_all();
+    changed();
   }
   std::shared_ptr<Msg> take(int src, int dst) {
     std::unique_lock<std::mutex> lk(mu_);
@@ -56,7 +56,7 @@ class LocalHub {
   void mark_consumed(const std::shared_ptr<Msg>& m) {
     std::lock_guard<std::mutex> lk(mu_);
     m->consumed = true;
-    cv_.notify_all();
+    changed();
   }
   void wait_consumed(const std::shared_ptr<Msg>& m, int dst) {
     std::unique_lock<std::mutex> lk(mu_);
@@ -68,7 +68,7 @@ class LocalHub {
     if (++bar_count_ == world_) {
       bar_count_ = 0;
       ++bar_gen_;
-      cv_.notify_all();
+      changed();
       return;
     }
     wait(lk, [&] { return bar_gen_ != gen; }, "barrier");
@@ -77,12 +77,27 @@ class LocalHub {
     std::lock_guard<std::mutex> lk(mu_);
     if (!aborted_) abort_msg_ = why;
     aborted_ = true;
-    cv_.notify_all();
+    changed();
   }
 
  private:
+  void changed() {  // under mu_
+    ver_.fetch_add(1, std::memory_order_release);
+    cv_.notify_all();
+  }
+  // The rank threads run in lockstep, so the awaited post is usually a few
+  // microseconds away: spin on the hub's version counter (lock released) for
+  // up to ~50 us before sleeping on the condition variable, whose futex wake
+  // costs tens of microseconds per exchange.
   template <class Pred>
   void wait(std::unique_lock<std::mutex>& lk, Pred pred, const std::string& what) {
+    const auto spin_end = std::chrono::steady_clock::now() + std::chrono::microseconds(50);
+    while (!pred() && !aborted_ && std::chrono::steady_clock::now() < spin_end) {
+      const uint64_t v = ver_.load(std::memory_order_acquire);
+      lk.unlock();
+      for (int k = 0; k < 256 && ver_.load(std::memory_order_acquire) == v; ++k) __builtin_ia32_pause();
+      lk.lock();
+    }
     const auto deadline = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s_);
     while (!pred()) {
       if (aborted_) fail("communicator aborted (" + abort_msg_ + ") while waiting for " + what);
@@ -100,6 +115,7 @@ class LocalHub {
   const double timeout_s_;
   std::mutex mu_;
   std::condition_variable cv_;
+  std::atomic<uint64_t> ver_{0};  // bumped on every state change (spinning waiters)
   std::map<std::pair<int, int>, std::deque<std::shared_ptr<Msg>>> box_;
   int bar_count_ = 0;
   long bar_gen_ = 0;
