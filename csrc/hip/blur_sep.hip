@@ -162,7 +162,7 @@ struct PlGeom {
 // within 1 LSB of the f64 result (the host bounds the error per weight set and
 // keeps the exact kernel when it cannot promise that).
 // (launch bounds: OCC waves per SIMD = OCC * 256 / THREADS workgroups per CU)
-template <int C, bool EDGE, int NX_, int PFD, int OCC, bool LSB = false, int NW = 1>
+template <int C, bool EDGE, int NX_, int PFD, int OCC, bool LSB = false, int NW = 1, bool EARLY = true>
 __global__ __launch_bounds__(blur_threads(NW), OCC * 256 / blur_threads(NW)) void k_blur_pl(SepArgs sa) {
   using G = PlGeom<C, NX_, NW>;
   constexpr int NX = G::NX;
@@ -324,13 +324,19 @@ __global__ __launch_bounds__(blur_threads(NW), OCC * 256 / blur_threads(NW)) voi
     colok[i] = npx[i] == 4 ? 0u : kOOB;
   }
   f4 acc[C][NX][2];  // running vertical sums of the current output group
+  // ES (shared double-buffered windows, two pairs prefetched): pair k + 1 is
+  // staged into the other window buffer in the middle of step k's tiles, so
+  // its conversion VALU and LDS writes run beside step k's MFMAs instead of
+  // between the barrier and the first MFMA (buffer (k + 1) & 1 held pair
+  // k - 1, whose readers all passed step k's barrier)
+  constexpr bool ES = EARLY && NW > 1 && PFD == 2;
   auto step = [&](auto fin_c, auto start_c, auto buf_c, int k) __attribute__((always_inline)) {
     constexpr bool FIN = decltype(fin_c)::value, START = decltype(start_c)::value;
     // the window of pair k: the wave's own tile, or buffer k & 1 of the shared
     // one (written here, read after the barrier; the other buffer's readers of
     // pair k - 1 all passed this pair's barrier before it is written again)
     uint8_t* const wt = NW == 1 ? wl : wl + (k & 1) * G::TILE;
-    stage(buf_c, wt);
+    if constexpr (!ES) stage(buf_c, wt);
     if constexpr (NW == 1) {
       sep_lds_sync();
     } else {
@@ -458,6 +464,10 @@ __global__ __launch_bounds__(blur_threads(NW), OCC * 256 / blur_threads(NW)) voi
       if (t + 1 < T) hmfma(F[(t + 1) & 1], X[(t + 1) & 1]);
       if (t + 2 < T) hread(t + 2, F[t & 1]);
       vert(t, X[t & 1]);
+      if constexpr (ES) {
+        if (t == (T > 1 ? 1 : 0) && k + 1 <= ngroups)
+          stage(std::integral_constant<int, 1 - decltype(buf_c)::value>{}, wl + ((k + 1) & 1) * G::TILE);
+      }
     }
     if constexpr (NW == 1) sep_lds_sync();  // fragment reads done before the next pair overwrites the planes
   };
@@ -472,6 +482,7 @@ __global__ __launch_bounds__(blur_threads(NW), OCC * 256 / blur_threads(NW)) voi
     step(T_{}, F_{}, B0{}, ngroups);
   } else {
     prefetch(1, B1{});  // pair 1 exists: ngroups >= 1
+    if constexpr (ES) stage(B0{}, wl);  // pair 0; later pairs are staged a step early
     // pair k sits in buffer k & 1 (static: the loop runs pairs of steps)
     step(F_{}, T_{}, B0{}, 0);
     int k = 1;
@@ -666,12 +677,16 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
   sa.bias = (float)pc.conv_bias;
   // A/B variants of the RGB non-edge kernel (STRIPE_BLUR_VARIANT=n): 1 = two
   // independent 4-wave workgroups per CU (NW 4, two pairs in flight), 2 = the
-  // same with one pair in flight, 3 = the 8-wave windows with one pair in flight
+  // same with one pair in flight, 3 = the 8-wave windows staging each pair
+  // between the barrier and the MFMAs (round 4's default, EARLY = false)
+#define STRIPE_BLUR_LATE(LSB)                                                                        \
+  Cfg { 2, 2, 8, dev::k_blur_pl<3, false, 2, 2, 2, LSB, 8, false>, (size_t)dev::PlGeom<3, 2, 8>::LDS }
   static const Cfg variants[2][4] = {
       {STRIPE_BLUR_CFGW(3, false, 2, 2, 2, false, 8), STRIPE_BLUR_CFGW(3, false, 2, 2, 2, false, 4),
-       STRIPE_BLUR_CFGW(3, false, 2, 1, 2, false, 4), STRIPE_BLUR_CFGW(3, false, 2, 1, 2, false, 8)},
+       STRIPE_BLUR_CFGW(3, false, 2, 1, 2, false, 4), STRIPE_BLUR_LATE(false)},
       {STRIPE_BLUR_CFGW(3, false, 2, 2, 2, true, 8), STRIPE_BLUR_CFGW(3, false, 2, 2, 2, true, 4),
-       STRIPE_BLUR_CFGW(3, false, 2, 1, 2, true, 4), STRIPE_BLUR_CFGW(3, false, 2, 1, 2, true, 8)}};
+       STRIPE_BLUR_CFGW(3, false, 2, 1, 2, true, 4), STRIPE_BLUR_LATE(true)}};
+#undef STRIPE_BLUR_LATE
   static const int env_variant = [] {
     const char* e = std::getenv("STRIPE_BLUR_VARIANT");
     return e ? std::atoi(e) : 0;
