@@ -160,7 +160,11 @@ int Engine::choose_depth() const {
     if (const char* e = std::getenv("STRIPE_HALO_DEPTH")) k = std::atoi(e);
   }
   if (plan_.cin != plan_.cout) k = 1;                          // not iterable: one chain per run
-  if (k <= 0) k = std::min(8, 1 + (minrows / 100) / S);       // redundant rows <= ~1 % of the stripe
+  // redundant rows <= ~1 % of the stripe, at most 32 steps per exchange (the
+  // cap was 8 until round 5: 4 local ranks on 8192^2 sobel, 2048-row
+  // stripes, step 0.043-0.045 ms at depth 8, 0.033-0.035 at 16, 0.034 at 21
+  // (this rule's pick), 0.029-0.030 at 32, profiles/r5/cfg3/README.md)
+  if (k <= 0) k = std::min(32, 1 + (minrows / 100) / S);
   // every neighbour must own the k*S rows it sends (and keep its own interior)
   k = std::min(k, minrows / (2 * S));
   return k >= 1 ? k : 0;
