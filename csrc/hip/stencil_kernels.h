@@ -59,6 +59,7 @@ struct WaveTask {
   int xt;     // tile column
   int ys, ye; // rows
   bool valid;
+  int dir = 1;  // 1: rows ys .. ye - 1 top-down; -1: bottom-up (kQuad launches)
 };
 
 // Row range of band `by` of a persistent launch: range 0 in `band`-row bands
@@ -91,6 +92,29 @@ __device__ __forceinline__ WaveTask task_at(const KArgs& a, int w) {
     else band_range(a, bt, t.ys, t.ye);
     t.valid = t.ys < t.ye;
   }
+  return t;
+}
+
+// kQuad task: a workgroup owns 4 vertically consecutive bands of one tile
+// column (wave v: band 4 q + v) and even bands run bottom-up, odd bands
+// top-down, so the two readers of every boundary's halo rows inside the
+// workgroup read them at the same moment (both first or both last) on one CU:
+// the second read is an L2 (or L1) hit instead of another fabric read.  The
+// boundary to the next quad is read last by both of its readers.
+__device__ __forceinline__ WaveTask quad_task(const KArgs& a) {
+  WaveTask t;
+  t.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  t.lane = threadIdx.x & 63;
+  const int g = xcd_remap((int)blockIdx.x, (int)gridDim.x, a.nxcd);
+  t.xt = g % a.ntx;
+  const int bt = 4 * (g / a.ntx) + t.wave;
+  t.valid = bt < a.nbands;
+  t.ys = t.ye = 0;
+  if (t.valid) {
+    band_range(a, bt, t.ys, t.ye);
+    t.valid = t.ys < t.ye;
+  }
+  t.dir = (bt & 1) ? 1 : -1;
   return t;
 }
 
@@ -548,12 +572,20 @@ __device__ __forceinline__ void sep_task(const KArgs& a, const WaveTask& t, cons
   using T = SepTraits<F>;
   const int lane = t.lane;
   const int ys = t.ys, ye = t.ye;
+  // rows are stepped in logical order y = ys .. ye - 1; a bottom-up task
+  // (t.dir < 0) maps logical row y to physical row ys + ye - 1 - y.  The
+  // vertical taps are symmetric (sobel's difference taps flip sign under a
+  // magnitude), so the outputs are the same bits in either direction.
+  constexpr bool kRev = SepTraits<F>::SYM;  // kQuad instances only (static_assert there)
+  const int pbase = kRev && t.dir < 0 ? ys + ye - 1 : 0;
+  const int psign = kRev && t.dir < 0 ? -1 : 1;
+  auto phys = [&](int y) __attribute__((always_inline)) { return pbase + psign * y; };
   const int cb = t.xt * (kOutChunks * 16) - 16 + lane * 16;
   const uint32_t lane_in = cb < a.E + 16 ? (uint32_t)(cb * CIN) : kOOB;
   const OutLanes lout = out_lanes<EXP>(a, lane, cb - 16 * lane);
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);
   const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
-  const uint32_t last_row = in_row_off(a, ye - 1 + R);
+  const uint32_t last_row = in_row_off(a, phys(ye - 1 + R));
   // @skip: the prologue bytes of the last 4 input rows (slot (r - ys) mod 4),
   // so an output row's centre bytes come from registers, not a second load
   constexpr int kRing = SKIP ? 4 : 1;
@@ -576,7 +608,7 @@ __device__ __forceinline__ void sep_task(const KArgs& a, const WaveTask& t, cons
   for (int i = 0; i < K - 1; ++i) {  // prime with rows ys-R .. ys+R-1
     uint32_t u[8];
     RawChunk<PRO> rr;
-    load_raw<PRO>(rin, in_row_off(a, ys - R + i), lane_in, rr);
+    load_raw<PRO>(rin, in_row_off(a, phys(ys - R + i)), lane_in, rr);
     cook_pairs<PRO>(a, rr, luts, u);
     if constexpr (SKIP) {
       if (i >= R) keep_centre(u, cen[(i - R) % kRing]);
@@ -597,15 +629,21 @@ __device__ __forceinline__ void sep_task(const KArgs& a, const WaveTask& t, cons
   constexpr int kPF = is_gray(PRO) ? 2 : 4;
   RawChunk<PRO> nx[kPF];
 #pragma unroll
-  for (int i = 0; i < kPF; ++i) load_raw<PRO>(rin, ys + i < ye ? in_row_off(a, ys + i + R) : last_row, lane_in, nx[i]);
+  for (int i = 0; i < kPF; ++i)
+    load_raw<PRO>(rin, ys + i < ye ? in_row_off(a, phys(ys + i + R)) : last_row, lane_in, nx[i]);
 
   const bool inner = rows_inside(a, ys - R, ye - 1 + R);
+  // input row feeding step y + kPF (ahead_row_off, through phys)
+  auto ahead_off = [&](int y) __attribute__((always_inline)) -> uint32_t {
+    if (inner) return a.in_org + (uint32_t)phys(min(y + kPF, ye - 1) + R) * (uint32_t)a.in_pitch;
+    return y + kPF < ye ? in_row_off(a, phys(y + kPF + R)) : last_row;
+  };
   // (i: the step's index in its unrolled group; the group starts at a multiple
   // of kRing rows past ys, so ring slots are compile-time)
   auto row_step = [&](int y, int i, const VState<F>& prev, VState<F>& next, RawChunk<PRO>& nb, bool valid) {
     uint32_t u[8], vv[8], dd[8];
     cook_pairs<PRO>(a, nb, luts, u);
-    load_raw<PRO>(rin, ahead_row_off(a, inner, y, kPF, ye, R, last_row), lane_in, nb);
+    load_raw<PRO>(rin, ahead_off(y), lane_in, nb);
     if constexpr (SKIP) keep_centre(u, cen[(i + R) % kRing]);  // input row y + R
     if constexpr (F::SOBEL) {
       vpush_sobel<F>(u, prev, next, vv, dd);
@@ -703,10 +741,10 @@ __device__ __forceinline__ void sep_task(const KArgs& a, const WaveTask& t, cons
 #pragma unroll
       for (int q = 0; q < 4; ++q) o[q] = pack4(ob[4 * q], ob[4 * q + 1], ob[4 * q + 2], ob[4 * q + 3]);
     }
-    if constexpr (SKIP) apply_skip(a, a.row0 + y, R, keep, cen[i % kRing], o);
+    if constexpr (SKIP) apply_skip(a, a.row0 + phys(y), R, keep, cen[i % kRing], o);
     if (a.has_epi) lut16(luts + 512, o);
     // rows past the band (tail of the 4-row group) are computed but not stored
-    store_out<EXP, SAUX>(o, rout, valid, a.out_org + (uint32_t)((int64_t)y * a.out_pitch), lout, xb, lane);
+    store_out<EXP, SAUX>(o, rout, valid, a.out_org + (uint32_t)((int64_t)phys(y) * a.out_pitch), lout, xb, lane);
   };
 
   // rows go in groups of kG with no branch around any step, ping-ponging the
@@ -736,7 +774,9 @@ __device__ __forceinline__ void sep_task(const KArgs& a, const WaveTask& t, cons
 //              the workgroups dispatched last carry the short tasks, so the
 //              launch's tail is one short task long;
 //   kQueue     a grid of the resident workgroups claiming tasks from the work
-//              queue (KArgs::queue) until none is left.
+//              queue (KArgs::queue) until none is left;
+//   kQuad      one task per wave, a workgroup = 4 stacked bands of one tile
+//              column in alternating directions (quad_task).
 // STAMP: the per-wave timeline of KArgs::stamps (diagnostic instances,
 // tools/sepx.hip).  Both are compile-time, so the one-task instances carry
 // neither the loop nor the stamp code.  NW: waves per workgroup (one-task
@@ -745,12 +785,14 @@ __device__ __forceinline__ void sep_task(const KArgs& a, const WaveTask& t, cons
 // tools/sepx.hip `wg` sweep, profiles/r5/cold/sepx_wg_*.txt).
 // (skip border + expand epilogue, a rare combination: 2 VGPRs over the 128 of
 // 4 waves/SIMD with the gray prologue -> 3 waves rather than a scratch spill)
-enum KMode { kOneTask = 0, kTailBands = 1, kQueue = 2 };
+enum KMode { kOneTask = 0, kTailBands = 1, kQueue = 2, kQuad = 3 };
 template <int C, class F, int PRO, bool SKIP, int SAUX, bool EXP = false, int MODE = kOneTask, bool STAMP = false,
           int NW = kWaves>
 __global__ __launch_bounds__(NW * kW, (F::K >= 7 ? 2 : (SKIP && EXP ? 3 : 4))) void k_sep(KArgs a) {
   constexpr bool PERSIST = MODE == kQueue;
   static_assert(NW == kWaves || MODE == kOneTask, "task modes assume kWaves-wave workgroups");
+  static_assert(MODE != kQuad || kWaves == 4, "kQuad: one band per wave of a 4-wave workgroup");
+  static_assert(MODE != kQuad || SepTraits<F>::SYM, "a bottom-up band needs symmetric vertical taps");
   const uint32_t t_start = STAMP ? stamp_now() : 0u;
   __shared__ __attribute__((aligned(16))) uint4 xbuf[EXP ? NW : 1][EXP ? 3 * kW : 1];
   __shared__ uint8_t luts[768];
@@ -770,6 +812,9 @@ __global__ __launch_bounds__(NW * kW, (F::K >= 7 ? 2 : (SKIP && EXP ? 3 : 4))) v
       task = nw + kQueueShards * (int)__builtin_amdgcn_readfirstlane(next) + shard;
     }
     queue_retire(a.queue, shard);
+  } else if constexpr (MODE == kQuad) {
+    const WaveTask t = quad_task(a);
+    if (t.valid) sep_task<C, F, PRO, SKIP, SAUX, EXP>(a, t, luts, xbuf[EXP ? t.wave : 0]);
   } else if constexpr (MODE == kTailBands) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const WaveTask t = task_at<true>(a, xcd_remap((int)blockIdx.x, (int)gridDim.x, a.nxcd) * kWaves + wave);
