@@ -678,7 +678,9 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
   // A/B variants of the RGB non-edge kernel (STRIPE_BLUR_VARIANT=n): 1 = two
   // independent 4-wave workgroups per CU (NW 4, two pairs in flight), 2 = the
   // same with one pair in flight, 3 = the 8-wave windows staging each pair
-  // between the barrier and the MFMAs (round 4's default, EARLY = false)
+  // between the barrier and the MFMAs (round 4's default, EARLY = false).
+  // (Three pairs in flight, lsb, 254 registers: 0.376 vs 0.354 ms on 16K,
+  // 0.047 vs 0.042 on the stripe, profiles/r5/blur/pfd3_*.txt: removed.)
 #define STRIPE_BLUR_LATE(LSB)                                                                        \
   Cfg { 2, 2, 8, dev::k_blur_pl<3, false, 2, 2, 2, LSB, 8, false>, (size_t)dev::PlGeom<3, 2, 8>::LDS }
   static const Cfg variants[2][4] = {
