@@ -439,6 +439,7 @@ def main():
         "streams": nstreams,
         "scopes": scopes,
         "tuned": {"band_rows": dp.engine.bands, "occupancy_caps": dp.engine.caps, "policies": dp.engine.policies,
+                  "task_orders": dp.engine.orders,
                   "cold": cold, "streaming_policy": fs.streaming},
         "cache": fs.cache,
         "halo_depth": 1,
@@ -515,7 +516,7 @@ def main():
         if k <= 1:
             scopes["resident_deep"] = {"same_as": "resident_warm", "halo_depth": k}
             return
-        dd.engine.set_tuning(dp.engine.bands, dp.engine.caps, dp.engine.policies)
+        dd.engine.set_tuning(dp.engine.bands, dp.engine.caps, dp.engine.policies, dp.engine.orders)
         n = k * int(math.ceil(deep_steps / k))  # whole exchange blocks
         dd.load_synthetic(a.seed)
         dd.run(2 * k)

@@ -450,7 +450,7 @@ int cmd_bench(const Args& a) {
               fr.back()->load_synthetic(seed + (uint64_t)f);
             }
             fr[0]->tune();
-            for (int f = 1; f < nframes; ++f) fr[f]->set_tuning(fr[0]->bands(), fr[0]->caps(), fr[0]->policies());
+            for (int f = 1; f < nframes; ++f) fr[f]->set_tuning(fr[0]->bands(), fr[0]->caps(), fr[0]->policies(), fr[0]->orders());
             const bool it_ok = fr[0]->plan().cin == fr[0]->plan().cout;
             auto fstep = [&](int i) {
               Engine& fe = *fr[(size_t)(i % nframes)];

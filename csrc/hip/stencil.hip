@@ -191,17 +191,17 @@ void launch_stencil(const Pass& p, const PassConsts& pc, const PassLaunch& L, hi
   a.nxcd = nt ? 0 : dev::kXcdCount;
   using namespace sdef;
   switch (p.sid) {
-    case StencilId::Emboss3: dev::launch_filter<Emboss3>(p, a, tiles, n0, n1, band, nt, L.wgs, s); break;
-    case StencilId::Emboss5: dev::launch_filter<Emboss5>(p, a, tiles, n0, n1, band, nt, L.wgs, s); break;
-    case StencilId::Sharpen: dev::launch_filter<Sharpen>(p, a, tiles, n0, n1, band, nt, L.wgs, s); break;
-    case StencilId::Laplace: dev::launch_filter<Laplace>(p, a, tiles, n0, n1, band, nt, L.wgs, s); break;
-    case StencilId::Sobel: dev::launch_filter<Sobel>(p, a, tiles, n0, n1, band, nt, L.wgs, s); break;
-    case StencilId::SobelL2: dev::launch_filter<SobelL2>(p, a, tiles, n0, n1, band, nt, L.wgs, s); break;
-    case StencilId::Gaussian3: dev::launch_filter<Gaussian3>(p, a, tiles, n0, n1, band, nt, L.wgs, s); break;
-    case StencilId::Gaussian5: dev::launch_filter<Gaussian5>(p, a, tiles, n0, n1, band, nt, L.wgs, s); break;
-    case StencilId::Gaussian7: dev::launch_filter<Gaussian7>(p, a, tiles, n0, n1, band, nt, L.wgs, s); break;
-    case StencilId::Box3: dev::launch_filter<Box3>(p, a, tiles, n0, n1, band, nt, L.wgs, s); break;
-    case StencilId::Box5: dev::launch_filter<Box5>(p, a, tiles, n0, n1, band, nt, L.wgs, s); break;
+    case StencilId::Emboss3: dev::launch_filter<Emboss3>(p, a, tiles, n0, n1, band, nt, L.wgs, s, L.order); break;
+    case StencilId::Emboss5: dev::launch_filter<Emboss5>(p, a, tiles, n0, n1, band, nt, L.wgs, s, L.order); break;
+    case StencilId::Sharpen: dev::launch_filter<Sharpen>(p, a, tiles, n0, n1, band, nt, L.wgs, s, L.order); break;
+    case StencilId::Laplace: dev::launch_filter<Laplace>(p, a, tiles, n0, n1, band, nt, L.wgs, s, L.order); break;
+    case StencilId::Sobel: dev::launch_filter<Sobel>(p, a, tiles, n0, n1, band, nt, L.wgs, s, L.order); break;
+    case StencilId::SobelL2: dev::launch_filter<SobelL2>(p, a, tiles, n0, n1, band, nt, L.wgs, s, L.order); break;
+    case StencilId::Gaussian3: dev::launch_filter<Gaussian3>(p, a, tiles, n0, n1, band, nt, L.wgs, s, L.order); break;
+    case StencilId::Gaussian5: dev::launch_filter<Gaussian5>(p, a, tiles, n0, n1, band, nt, L.wgs, s, L.order); break;
+    case StencilId::Gaussian7: dev::launch_filter<Gaussian7>(p, a, tiles, n0, n1, band, nt, L.wgs, s, L.order); break;
+    case StencilId::Box3: dev::launch_filter<Box3>(p, a, tiles, n0, n1, band, nt, L.wgs, s, L.order); break;
+    case StencilId::Box5: dev::launch_filter<Box5>(p, a, tiles, n0, n1, band, nt, L.wgs, s, L.order); break;
     default: fail("unknown stencil");
   }
   HIP_CHECK(hipGetLastError());

@@ -118,6 +118,42 @@ __device__ __forceinline__ WaveTask quad_task(const KArgs& a) {
   return t;
 }
 
+// kRuns task: a workgroup = kWaves adjacent tile columns of one band, as in
+// the one-task launch, but the workgroups dispatched to one XCD (blockIdx % 8)
+// walk down runs of kRunLen bands of one column group, consecutive bands one
+// dispatch slot (8 workgroups) apart, even bands bottom-up and odd bands
+// top-down: the two readers of a boundary's halo rows run on one XCD and read
+// them at the same moment (both first or both last), so one of the two reads
+// is an L2 hit.  Runs are dealt to the XCDs round-robin (balanced); only every
+// kRunLen-th boundary is still read twice through the fabric.
+constexpr int kRunLen = 8;
+__device__ __forceinline__ WaveTask runs_task(const KArgs& a) {
+  WaveTask t;
+  t.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  t.lane = threadIdx.x & 63;
+  const int b = (int)blockIdx.x;
+  const int x = b % kXcdCount, j = b / kXcdCount;
+  const int g = (j / kRunLen) * kXcdCount + x;  // global run
+  const int ncg = (a.ntx + kWaves - 1) / kWaves;  // column groups
+  const int cg = g % ncg;
+  const int bt = (g / ncg) * kRunLen + j % kRunLen;
+  t.xt = kWaves * cg + t.wave;
+  t.valid = bt < a.nbands && t.xt < a.ntx;
+  t.ys = t.ye = 0;
+  if (t.valid) {
+    band_range(a, bt, t.ys, t.ye);
+    t.valid = t.ys < t.ye;
+  }
+  t.dir = (bt & 1) ? 1 : -1;
+  return t;
+}
+// grid of a kRuns launch: every run of every column group
+inline int64_t runs_grid(int ntx, int nbands) {
+  const int64_t ncg = (ntx + kWaves - 1) / kWaves;
+  const int64_t nruns = ncg * ((nbands + kRunLen - 1) / kRunLen);
+  return (int64_t)kXcdCount * kRunLen * ((nruns + kXcdCount - 1) / kXcdCount);
+}
+
 // The task of this wave in a one-task-per-wave launch (XCD-aware workgroup order).
 template <int NW = kWaves>
 __device__ __forceinline__ WaveTask wave_task(const KArgs& a) {
@@ -776,7 +812,9 @@ __device__ __forceinline__ void sep_task(const KArgs& a, const WaveTask& t, cons
 //   kQueue     a grid of the resident workgroups claiming tasks from the work
 //              queue (KArgs::queue) until none is left;
 //   kQuad      one task per wave, a workgroup = 4 stacked bands of one tile
-//              column in alternating directions (quad_task).
+//              column in alternating directions (quad_task);
+//   kRuns      one task per wave, XCD-local runs of bands in alternating
+//              directions (runs_task).
 // STAMP: the per-wave timeline of KArgs::stamps (diagnostic instances,
 // tools/sepx.hip).  Both are compile-time, so the one-task instances carry
 // neither the loop nor the stamp code.  NW: waves per workgroup (one-task
@@ -785,14 +823,14 @@ __device__ __forceinline__ void sep_task(const KArgs& a, const WaveTask& t, cons
 // tools/sepx.hip `wg` sweep, profiles/r5/cold/sepx_wg_*.txt).
 // (skip border + expand epilogue, a rare combination: 2 VGPRs over the 128 of
 // 4 waves/SIMD with the gray prologue -> 3 waves rather than a scratch spill)
-enum KMode { kOneTask = 0, kTailBands = 1, kQueue = 2, kQuad = 3 };
+enum KMode { kOneTask = 0, kTailBands = 1, kQueue = 2, kQuad = 3, kRuns = 4 };
 template <int C, class F, int PRO, bool SKIP, int SAUX, bool EXP = false, int MODE = kOneTask, bool STAMP = false,
           int NW = kWaves>
 __global__ __launch_bounds__(NW * kW, (F::K >= 7 ? 2 : (SKIP && EXP ? 3 : 4))) void k_sep(KArgs a) {
   constexpr bool PERSIST = MODE == kQueue;
   static_assert(NW == kWaves || MODE == kOneTask, "task modes assume kWaves-wave workgroups");
   static_assert(MODE != kQuad || kWaves == 4, "kQuad: one band per wave of a 4-wave workgroup");
-  static_assert(MODE != kQuad || SepTraits<F>::SYM, "a bottom-up band needs symmetric vertical taps");
+  static_assert((MODE != kQuad && MODE != kRuns) || SepTraits<F>::SYM, "a bottom-up band needs symmetric vertical taps");
   const uint32_t t_start = STAMP ? stamp_now() : 0u;
   __shared__ __attribute__((aligned(16))) uint4 xbuf[EXP ? NW : 1][EXP ? 3 * kW : 1];
   __shared__ uint8_t luts[768];
@@ -812,8 +850,8 @@ __global__ __launch_bounds__(NW * kW, (F::K >= 7 ? 2 : (SKIP && EXP ? 3 : 4))) v
       task = nw + kQueueShards * (int)__builtin_amdgcn_readfirstlane(next) + shard;
     }
     queue_retire(a.queue, shard);
-  } else if constexpr (MODE == kQuad) {
-    const WaveTask t = quad_task(a);
+  } else if constexpr (MODE == kQuad || MODE == kRuns) {
+    const WaveTask t = MODE == kQuad ? quad_task(a) : runs_task(a);
     if (t.valid) sep_task<C, F, PRO, SKIP, SAUX, EXP>(a, t, luts, xbuf[EXP ? t.wave : 0]);
   } else if constexpr (MODE == kTailBands) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1078,9 +1116,23 @@ inline int stencil_cap(bool nt, int wgs, int family_default) {
 }
 
 template <int C, class F, int PRO, bool EXP = false>
-void launch_one(bool skip, bool nt, int wgs, KArgs a, int tiles, int n0, int n1, int band, hipStream_t s) {
+void launch_one(bool skip, bool nt, int wgs, KArgs a, int tiles, int n0, int n1, int band, hipStream_t s,
+                int order = 0) {
   using K = void (*)(KArgs);
   dim3 grid;
+  if constexpr (F::SEP && PRO == PRO_NONE && !EXP) {
+    if constexpr (SepTraits<F>::SYM) {
+      if (order == 1) {  // kRuns (runs_task); the remap is its own
+        const K fns[4] = {k_sep<C, F, PRO, false, 0, EXP, kRuns>, k_sep<C, F, PRO, false, kNtAux, EXP, kRuns>,
+                          k_sep<C, F, PRO, true, 0, EXP, kRuns>, k_sep<C, F, PRO, true, kNtAux, EXP, kRuns>};
+        const K fn = fns[2 * skip + nt];
+        plan_bands(a, grid, tiles, n0, n1, band, F::R, 0);
+        grid = dim3((unsigned)runs_grid(tiles, a.nbands));
+        fn<<<grid, kNT, nt_lds_reserve((const void*)fn, stencil_cap(nt, wgs, kNtWgsSep)), s>>>(a);
+        return;
+      }
+    }
+  }
   if constexpr (F::SEP) {
     const K fns[4] = {k_sep<C, F, PRO, false, 0, EXP>, k_sep<C, F, PRO, false, kNtAux, EXP>,
                       k_sep<C, F, PRO, true, 0, EXP>, k_sep<C, F, PRO, true, kNtAux, EXP>};
@@ -1105,7 +1157,7 @@ void launch_gray_out(bool expand, bool skip, bool nt, int wgs, const KArgs& a, i
 
 template <class F>
 void launch_filter(const Pass& p, const KArgs& a, int tiles, int n0, int n1, int band, bool nt, int wgs,
-                   hipStream_t s) {
+                   hipStream_t s, int order) {
   const bool gray = p.pro.gray;
   const bool lut = p.pro.has_post;
   const bool skip = p.border == Border::Skip;
@@ -1113,11 +1165,12 @@ void launch_filter(const Pass& p, const KArgs& a, int tiles, int n0, int n1, int
   if (p.cmid == 3) {
     STRIPE_CHECK(!gray && !ex, "gray prologue / expand epilogue need a 1-channel stencil");
     if (lut) launch_one<3, F, PRO_LUT>(skip, nt, wgs, a, tiles, n0, n1, band, s);
-    else launch_one<3, F, PRO_NONE>(skip, nt, wgs, a, tiles, n0, n1, band, s);
+    else launch_one<3, F, PRO_NONE>(skip, nt, wgs, a, tiles, n0, n1, band, s, order);
   } else {
     if (gray && a.gmode == 1) launch_gray_out<PRO_GRAYLUT, F>(ex, skip, nt, wgs, a, tiles, n0, n1, band, s);
     else if (gray) launch_gray_out<PRO_GRAY, F>(ex, skip, nt, wgs, a, tiles, n0, n1, band, s);
     else if (lut) launch_gray_out<PRO_LUT, F>(ex, skip, nt, wgs, a, tiles, n0, n1, band, s);
+    else if (!ex) launch_one<1, F, PRO_NONE>(skip, nt, wgs, a, tiles, n0, n1, band, s, order);
     else launch_gray_out<PRO_NONE, F>(ex, skip, nt, wgs, a, tiles, n0, n1, band, s);
   }
 }
@@ -1125,7 +1178,7 @@ void launch_filter(const Pass& p, const KArgs& a, int tiles, int n0, int n1, int
 
 // Every filter F has launch_filter<F> compiled in exactly one stencil_inst_*.hip.
 #define STRIPE_LAUNCH_FILTER_SIG(F) \
-  void launch_filter<sdef::F>(const Pass&, const KArgs&, int, int, int, int, bool, int, hipStream_t)
+  void launch_filter<sdef::F>(const Pass&, const KArgs&, int, int, int, int, bool, int, hipStream_t, int)
 #define STRIPE_EXTERN_LAUNCH_FILTER(F) extern template STRIPE_LAUNCH_FILTER_SIG(F);
 #define STRIPE_INSTANTIATE_LAUNCH_FILTER(F) template STRIPE_LAUNCH_FILTER_SIG(F);
 #define STRIPE_STENCIL_FILTERS(X) \

@@ -166,6 +166,7 @@ class Engine {
   std::vector<int> bands() const;
   std::vector<int> caps() const;
   std::vector<int> policies() const;
+  std::vector<int> orders() const;
   // Run the band / occupancy-cap autotune now (EngineConfig::autotune; otherwise
   // the first run() does it): keeps the tuning out of a timed region.
   void tune() {
@@ -174,7 +175,7 @@ class Engine {
   // Adopt another engine's tuning (same chain and stripe shape; skips autotune).
   // `policies` may be empty (keep each pass's memory policy).
   void set_tuning(const std::vector<int>& bands, const std::vector<int>& caps,
-                  const std::vector<int>& policies = {});
+                  const std::vector<int>& policies = {}, const std::vector<int>& orders = {});
 
   // ---- output ----
   void store_packed(void* dst, bool dst_device);          // own output stripe, packed
@@ -247,6 +248,7 @@ class Engine {
     int band = 0;  // tuned stencil band height (0: kernel default / cfg.band)
     int wgs = -1;  // tuned occupancy cap (resident workgroups per CU; -1: family default)
     int nt = -1;   // tuned memory policy (PassLaunch::nt; -1: cold ? streaming : size rule)
+    int order = 0; // tuned separable task order (PassLaunch::order)
   };
   void autotune_bands();
   bool tuned_ = false;

@@ -58,6 +58,10 @@ struct PassLaunch {
                                  // workgroup order), 0 cache-resident (default stores, XCD-aware
                                  // order), -1 chosen by the launch's size against the
                                  // Infinity Cache
+  int order = 0;                 // separable stencil task order: 0 one band of one tile
+                                 // column per wave, band-major; 1 XCD-local runs of bands
+                                 // in alternating directions (kRuns, plain separable
+                                 // filters: halo rows read twice within one L2)
   // Allocation view for buffer-descriptor kernels (branch-free OOB masking):
   // origin = base + org, zero row origin = in_base + in_zero; sizes < 2 GiB.
   const uint8_t* in_base = nullptr;

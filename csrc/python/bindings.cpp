@@ -567,6 +567,7 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("bands", &Engine::bands)
       .def_property_readonly("caps", &Engine::caps)
       .def_property_readonly("policies", &Engine::policies)
+      .def_property_readonly("orders", &Engine::orders)
       .def("run_timed", [](Engine& e, int it, int per, bool rewind_each) {
         py::gil_scoped_release rel;
         return e.run_timed(it, per, rewind_each);
@@ -585,7 +586,7 @@ PYBIND11_MODULE(_C, m) {
         e.run_to_host(reinterpret_cast<void*>(p), chunks);
       }, py::arg("ptr"), py::arg("chunks") = 8)
       .def("set_tuning", &Engine::set_tuning, py::arg("bands"), py::arg("caps"),
-           py::arg("policies") = std::vector<int>{})
+           py::arg("policies") = std::vector<int>{}, py::arg("orders") = std::vector<int>{})
       .def("tune", [](Engine& e) {
         py::gil_scoped_release nogil;
         e.tune();

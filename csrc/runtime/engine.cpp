@@ -477,6 +477,7 @@ PassLaunch Engine::make_launch(const Pass& p, const uint8_t* in, uint8_t* out, i
   L.zero_row = zero_.data() + kMarginBytes;
   L.band = prt_[pi].band > 0 ? prt_[pi].band : cfg_.band;
   L.wgs = prt_[pi].wgs;
+  L.order = prt_[pi].order;
   // memory policy: the tuned one, else streaming for a cache-cold stripe, else
   // the launch's size rule
   L.nt = prt_[pi].nt >= 0 ? prt_[pi].nt : (cfg_.cold ? 1 : -1);

@@ -35,17 +35,37 @@ std::vector<int> Engine::policies() const {
   return b;
 }
 
+std::vector<int> Engine::orders() const {
+  std::vector<int> b;
+  for (const auto& p : prt_) b.push_back(p.order);
+  return b;
+}
+
 void Engine::set_tuning(const std::vector<int>& bands, const std::vector<int>& caps,
-                        const std::vector<int>& policies) {
+                        const std::vector<int>& policies, const std::vector<int>& orders) {
   STRIPE_CHECK(bands.size() == prt_.size() && caps.size() == prt_.size() &&
-                   (policies.empty() || policies.size() == prt_.size()),
+                   (policies.empty() || policies.size() == prt_.size()) &&
+                   (orders.empty() || orders.size() == prt_.size()),
                "tuning needs one entry per pass");
   for (size_t i = 0; i < prt_.size(); ++i) {
     prt_[i].band = bands[i];
     prt_[i].wgs = caps[i];
     if (!policies.empty()) prt_[i].nt = policies[i];
+    if (!orders.empty()) {
+      STRIPE_CHECK(orders[i] == 0 || orders[i] == 1, "task order must be 0 or 1");
+      prt_[i].order = orders[i];
+    }
   }
   tuned_ = true;
+}
+
+// STRIPE_SEP_ORDER=0|1 pins the separable task order (A/B runs); unset: tuned.
+static int env_sep_order() {
+  static const int v = [] {
+    const char* e = std::getenv("STRIPE_SEP_ORDER");
+    return e ? std::atoi(e) : -1;
+  }();
+  return v;
 }
 
 // Time each candidate band height, then each occupancy cap at the best band,
@@ -135,10 +155,11 @@ void Engine::autotune_bands() {
     // taller bands by ~5 % on 20-90 us kernels); bursts of a 40-300 us kernel
     // still jitter by a few percent, about the gap between bands
     constexpr int kBurst = 4;
-    auto time_it = [&](int band, int wgs, int nt) {
+    auto time_it = [&](int band, int wgs, int nt, int order = 0) {
       L.band = band;
       L.wgs = wgs;
       L.nt = nt;
+      L.order = order;
       std::vector<float> t;
       for (int rep = 0; rep < 6; ++rep) {
         HIP_CHECK(hipEventRecord(e0, s_compute_));
@@ -203,12 +224,39 @@ void Engine::autotune_bands() {
         }
       }
     }
+    // task order of a separable pass: XCD-local runs of bands in alternating
+    // directions (kRuns) move ~20 % fewer L2 fill bytes (16K RGB gaussian5,
+    // FETCH_SIZE 1.31x -> 1.06x of the input) but change the DRAM access
+    // pattern: kept only where it times faster, at the best band or 12 rows
+    // (16K RGB: 270-272 us at 12 rows vs 277 us one-task at 16, cold N=8
+    // share: no gain, profiles/r5/cold/README.md)
+    int best_order = 0;
+    if (p.kind == PassKind::Separable) {
+      if (env_sep_order() >= 0) {
+        best_order = env_sep_order() == 1 ? 1 : 0;
+      } else {
+        int band_o = best_band;
+        const int cands_o[2] = {best_band, best_band == 12 ? 0 : 12};
+        for (int b : cands_o) {
+          if (b <= 0) continue;
+          const float t = time_it(b, best_wgs, best_nt, 1);
+          if (t < best * 0.985f) {  // beyond the bursts' jitter
+            best = t;
+            best_order = 1;
+            band_o = b;
+          }
+        }
+        best_band = band_o;
+      }
+    }
     prt_[i].band = best_band;
     prt_[i].wgs = best_wgs;
     prt_[i].nt = best_nt;
+    prt_[i].order = best_order;
     STRIPE_LOG(Info, rank_, "autotune pass " << i << (cfg_.cold ? " (cold)" : "") << ": band " << best_band
-                                             << " rows, occupancy cap " << best_wgs << ", policy " << best_nt << " ("
-                                             << best * 1e3f << " us per launch)");
+                                             << " rows, occupancy cap " << best_wgs << ", policy " << best_nt
+                                             << ", task order " << best_order << " (" << best * 1e3f
+                                             << " us per launch)");
   }
   if (!scratch.empty()) HIP_CHECK(hipStreamSynchronize(s_compute_));  // before the scratch stripes are freed
 }

@@ -381,7 +381,7 @@ class FrameStream:
         e0 = self.head.engine
         e0.tune()
         for f in self.frames[1:]:
-            f.engine.set_tuning(e0.bands, e0.caps, e0.policies)
+            f.engine.set_tuning(e0.bands, e0.caps, e0.policies, e0.orders)
 
     SCHEDULES = ("pipeline", "overlap", "serial")
 

@@ -5,7 +5,7 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Icsrc/include -Icsrc/hip \
 //         -o bin/sepx tools/sepx.hip
-//   bin/sepx [rows] [frames] [stamp_csv_prefix] [sweep: tail | policy | sobel | wg | quad | sobelquad]
+//   bin/sepx [rows] [frames] [stamp_csv_prefix] [sweep: tail | policy | sobel | wg | quad | sobelquad | runs | fetch]
 //
 // Every measurement rotates over `frames` independent in/out buffer pairs
 // (default: enough that frames x (in + out) > 3 x 256 MiB), so each launch
@@ -71,6 +71,7 @@ template <int C, class Flt, int SAUX>
 static SepFn sep_fn_aux(int mode, bool stamp) {
   if (mode == kQueue) return sep_fn_mode<C, Flt, SAUX, kQueue>(stamp);
   if (mode == kQuad) return sep_fn_mode<C, Flt, SAUX, kQuad>(stamp);
+  if (mode == kRuns) return sep_fn_mode<C, Flt, SAUX, kRuns>(stamp);
   if (mode == kTailBands) return sep_fn_mode<C, Flt, SAUX, kTailBands>(stamp);
   return sep_fn_mode<C, Flt, SAUX, kOneTask>(stamp);
 }
@@ -99,7 +100,7 @@ struct SepCfg {
   int saux = 2, band = 12, cap = 2, nxcd = 0, mode = kOneTask, tail = 0;
   int nw = kWaves;  // waves per workgroup; cap counts workgroups per CU
   std::string name() const {
-    static const char* modes[] = {"one-task", "tail-bands", "queue", "quad"};
+    static const char* modes[] = {"one-task", "tail-bands", "queue", "quad", "runs"};
     char b[128];
     std::snprintf(b, sizeof b, "sep aux=%2d band=%2d cap=%d xcd=%d %s tail=%d%s", saux, band, cap, nxcd, modes[mode],
                   tail, nw == kWaves ? "" : (" wg=" + std::to_string(nw)).c_str());
@@ -133,7 +134,9 @@ static void launch_sep(const SepCfg& c, const Frame& f, hipStream_t s, uint32_t*
   dim3 grid;
   const SepFn fn = sep_fn(c.saux, c.mode, stamps != nullptr, c.nw);
   plan_bands(a, grid, tiles, g_rows, 0, c.band, g_sobel ? 1 : 2, 0);
-  grid.x = (unsigned)(c.mode == kQuad ? (int64_t)tiles * div_up(a.nbands, 4) : div_up((int64_t)tiles * a.nbands, c.nw));
+  grid.x = (unsigned)(c.mode == kQuad   ? (int64_t)tiles * div_up(a.nbands, 4)
+                      : c.mode == kRuns ? runs_grid(tiles, a.nbands)
+                                        : div_up((int64_t)tiles * a.nbands, c.nw));
   a.nxcd = c.nxcd;
   const size_t dyn = nt_lds_reserve((const void*)fn, c.cap);
   if (c.mode == kQueue) {
@@ -229,6 +232,7 @@ int main(int argc, char** argv) {
   const std::string csv = argc > 3 ? argv[3] : "";
   const std::string sweep = argc > 4 ? argv[4] : "tail";
   const bool quad = sweep == "quad" || sweep == "sobelquad";
+  const bool runs = sweep == "runs" || sweep == "fetch";
   if (sweep == "sobel" || sweep == "sobelquad") {  // config 3's share: 8192 x rows gray sobel, margins kept (iterated pass)
     g_sobel = true;
     g_W = 8192;
@@ -274,7 +278,16 @@ int main(int argc, char** argv) {
     c.tail = tail;
     cfgs.push_back(c);
   };
-  if (quad) {  // 4 stacked bands per workgroup in alternating directions vs one task per wave
+  if (sweep == "fetch") {  // one config per kernel name, for counter runs: SEPX_BAND rows
+    const char* e = std::getenv("SEPX_BAND");
+    const int band = e ? std::atoi(e) : 16;
+    add(2, band, 2, 0, kOneTask, 0);
+    add(2, band, 2, 0, kRuns, 0);
+  } else if (runs) {  // XCD-local band runs in alternating directions vs one task per wave
+    for (int band : {12, 16, 24, 32}) add(2, band, 2, 0, kOneTask, 0);
+    for (int band : {8, 12, 16, 24, 32})
+      for (int cap : {2, 3}) add(2, band, cap, 0, kRuns, 0);
+  } else if (quad) {  // 4 stacked bands per workgroup in alternating directions vs one task per wave
     for (int band : {4, 12, 16}) add(g_sobel ? 0 : 2, band, g_sobel ? 0 : 2, 0, kOneTask, 0);
     for (int band : {4, 8, 12, 16, 24, 32})
       for (int cap : {2, 3}) add(g_sobel ? 0 : 2, band, cap, 0, kQuad, 0);
@@ -320,7 +333,13 @@ int main(int argc, char** argv) {
 
   // per-wave timeline of one cold dispatch (the last of a rotation)
   std::vector<SepCfg> stamped(3);
-  if (quad) {
+  if (runs) {
+    stamped[0].band = 16;
+    stamped[1].band = 16;
+    stamped[1].mode = kRuns;
+    stamped[2].band = 32;
+    stamped[2].mode = kRuns;
+  } else if (quad) {
     stamped[0].band = 16;
     stamped[1].band = 16;
     stamped[1].mode = kQuad;
@@ -338,7 +357,7 @@ int main(int argc, char** argv) {
       c.cap = 0;
       c.nxcd = 8;
     }
-  if (sweep == "wg" || quad) {
+  if (sweep == "wg" || quad || runs) {
   } else if (g_sobel) {
     stamped[0].band = 4;
     stamped[1].band = 8;
