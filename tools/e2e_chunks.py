@@ -7,9 +7,13 @@ both-directions floor until per-chunk launch overhead takes over.
 """
 import argparse
 import json
+import os
+import sys
 import time
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import mpi_cuda_imagemanipulation_amd as m
 
