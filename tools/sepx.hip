@@ -5,7 +5,8 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Icsrc/include -Icsrc/hip \
 //         -o bin/sepx tools/sepx.hip
-//   bin/sepx [rows] [frames] [stamp_csv_prefix] [sweep: tail | policy | sobel | wg | quad | sobelquad | runs | fetch]
+//   bin/sepx [rows] [frames] [stamp_csv_prefix] [sweep: tail | policy | sobel | wg | quad | sobelquad | runs | fetch |
+//             pattern]
 //
 // Every measurement rotates over `frames` independent in/out buffer pairs
 // (default: enough that frames x (in + out) > 3 x 256 MiB), so each launch
@@ -49,6 +50,86 @@ __global__ __launch_bounds__(256) void k_copy_lin(const uint8_t* in, uint8_t* ou
   const uint32_t off = ((uint32_t)blockIdx.x * 256u + threadIdx.x) * 16u;
   const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(ri, off, 0, 2);
   __builtin_amdgcn_raw_buffer_store_b128(v, ro, off, 0, AUX);
+}
+
+// The stencil's memory access pattern without its arithmetic: each wave
+// streams rows ys - R .. ye - 1 + R of its 1 KiB tile column (four rows in
+// flight, as k_sep) and stores rows ys .. ye - 1 of lanes 1 .. 62.  Same task
+// mapping, same store policy: the difference to k_sep is the compute, the
+// difference to the linear copy is the pattern.
+template <int R>
+__global__ __launch_bounds__(256) void k_band_copy(KArgs a) {
+  const WaveTask t = wave_task(a);
+  if (!t.valid) return;
+  const int lane = t.lane;
+  const int cb = t.xt * (kOutChunks * 16) - 16 + lane * 16;
+  const uint32_t lane_in = cb < a.E + 16 ? (uint32_t)cb : kOOB;
+  const bool st = lane >= 1 && lane <= kW - 2 && cb < a.E;
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);
+  const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
+  auto row_off = [&](int y) { return in_row_off(a, min(y, t.ye - 1 + R)); };
+  u32x4 r[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r[i] = __builtin_amdgcn_raw_buffer_load_b128(rin, row_off(t.ys - R + i) + lane_in, 0, 0);
+  for (int y0 = t.ys - R; y0 < t.ye + R; y0 += 4) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int y = y0 + i;
+      const u32x4 v = r[i];
+      r[i] = __builtin_amdgcn_raw_buffer_load_b128(rin, row_off(y + 4) + lane_in, 0, 0);
+      if (y >= t.ys && y < t.ye && st)
+        __builtin_amdgcn_raw_buffer_store_b128(v, rout, a.out_org + (uint32_t)((int64_t)y * a.out_pitch) + (uint32_t)cb,
+                                               0, kNtAux);
+    }
+  }
+}
+
+// k_band_copy generalised: LB bytes per lane per row (a wave row of 64 LB
+// bytes), PF rows in flight per wave, every lane stores (pattern only).
+template <int R, int LB, int PF>
+__global__ __launch_bounds__(256) void k_band_copy2(KArgs a) {
+  const WaveTask t = wave_task(a);
+  if (!t.valid) return;
+  constexpr int NL = LB / 16;
+  // NL contiguous 1 KiB blocks per wave row: lane l owns 16 bytes of each
+  const int cb = t.xt * (kW * LB) + t.lane * 16;
+  const uint32_t lane_in = cb < a.E ? (uint32_t)cb : kOOB;
+  const bool st = cb < a.E;
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);
+  const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
+  auto row_off = [&](int y) { return in_row_off(a, min(y, t.ye - 1 + R)); };
+  u32x4 r[PF][NL];
+#pragma unroll
+  for (int i = 0; i < PF; ++i)
+#pragma unroll
+    for (int k = 0; k < NL; ++k)
+      r[i][k] = __builtin_amdgcn_raw_buffer_load_b128(rin, row_off(t.ys - R + i) + lane_in + 1024 * k, 0, 0);
+  for (int y0 = t.ys - R; y0 < t.ye + R; y0 += PF) {
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      const int y = y0 + i;
+      u32x4 v[NL];
+#pragma unroll
+      for (int k = 0; k < NL; ++k) {
+        v[k] = r[i][k];
+        r[i][k] = __builtin_amdgcn_raw_buffer_load_b128(rin, row_off(y + PF) + lane_in + 1024 * k, 0, 0);
+      }
+      if (y >= t.ys && y < t.ye && st)
+#pragma unroll
+        for (int k = 0; k < NL; ++k)
+          if (cb + 1024 * k < a.E) __builtin_amdgcn_raw_buffer_store_b128(
+              v[k], rout, a.out_org + (uint32_t)((int64_t)y * a.out_pitch) + (uint32_t)cb + 1024 * k, 0, kNtAux);
+    }
+  }
+}
+
+struct PatCfg {
+  int lb, pf, band, cap;
+};
+static void (*pat_fn(const PatCfg& c))(KArgs) {
+  if (c.lb == 16) return c.pf == 2 ? k_band_copy2<2, 16, 2> : c.pf == 4 ? k_band_copy2<2, 16, 4> : k_band_copy2<2, 16, 8>;
+  if (c.lb == 32) return c.pf == 2 ? k_band_copy2<2, 32, 2> : c.pf == 4 ? k_band_copy2<2, 32, 4> : k_band_copy2<2, 32, 8>;
+  return c.pf == 2 ? k_band_copy2<2, 64, 2> : k_band_copy2<2, 64, 4>;
 }
 
 struct Frame {
@@ -100,7 +181,7 @@ struct SepCfg {
   int saux = 2, band = 12, cap = 2, nxcd = 0, mode = kOneTask, tail = 0;
   int nw = kWaves;  // waves per workgroup; cap counts workgroups per CU
   std::string name() const {
-    static const char* modes[] = {"one-task", "tail-bands", "queue", "quad", "runs"};
+    static const char* modes[] = {"one-task", "tail-bands", "queue", "quad", "runs", "", "", "", "", "band-copy"};
     char b[128];
     std::snprintf(b, sizeof b, "sep aux=%2d band=%2d cap=%d xcd=%d %s tail=%d%s", saux, band, cap, nxcd, modes[mode],
                   tail, nw == kWaves ? "" : (" wg=" + std::to_string(nw)).c_str());
@@ -132,7 +213,7 @@ static void launch_sep(const SepCfg& c, const Frame& f, hipStream_t s, uint32_t*
   a.stamps = stamps;
   const int tiles = (int)div_up(a.E, kOutChunks * 16);
   dim3 grid;
-  const SepFn fn = sep_fn(c.saux, c.mode, stamps != nullptr, c.nw);
+  const SepFn fn = c.mode == 9 ? k_band_copy<2> : sep_fn(c.saux, c.mode, stamps != nullptr, c.nw);
   plan_bands(a, grid, tiles, g_rows, 0, c.band, g_sobel ? 1 : 2, 0);
   grid.x = (unsigned)(c.mode == kQuad   ? (int64_t)tiles * div_up(a.nbands, 4)
                       : c.mode == kRuns ? runs_grid(tiles, a.nbands)
@@ -147,6 +228,30 @@ static void launch_sep(const SepCfg& c, const Frame& f, hipStream_t s, uint32_t*
   }
   if (grid_out) *grid_out = (int)grid.x;
   fn<<<grid, c.nw * kW, dyn, s>>>(a);
+}
+
+static void launch_pat(const PatCfg& c, const Frame& f, hipStream_t s) {
+  KArgs a{};
+  a.in = f.in + g_org;
+  a.out = f.out + g_org;
+  a.in_pitch = a.out_pitch = g_pitch;
+  a.W = g_W;
+  a.E = g_W * g_C;
+  a.rows = g_rows;
+  a.Hg = g_rows;
+  a.in_base = f.in;
+  a.out_base = f.out;
+  a.in_bytes = a.out_bytes = (uint32_t)g_bytes;
+  a.in_org = a.out_org = (uint32_t)g_org;
+  a.in_zero = kMarginBytes;
+  a.ry0 = 0;
+  a.ry1 = g_rows;
+  const int tiles = (int)div_up(a.E, kW * c.lb);
+  dim3 grid;
+  plan_bands(a, grid, tiles, g_rows, 0, c.band, 2, 0);
+  a.nxcd = 0;
+  void (*fn)(KArgs) = pat_fn(c);
+  fn<<<grid, kNT, nt_lds_reserve((const void*)fn, c.cap), s>>>(a);
 }
 
 static void launch_copy(int aux, const Frame& f, hipStream_t s) {
@@ -278,7 +383,14 @@ int main(int argc, char** argv) {
     c.tail = tail;
     cfgs.push_back(c);
   };
-  if (sweep == "fetch") {  // one config per kernel name, for counter runs: SEPX_BAND rows
+  if (sweep == "pattern") {  // the stencil's access pattern without its arithmetic
+    for (int band : {12, 16, 32}) {
+      add(2, band, 2, 0, 9, 0);
+      add(2, band, 2, 0, kOneTask, 0);
+    }
+    add(2, 16, 0, 0, 9, 0);
+    add(2, 16, 3, 0, 9, 0);
+  } else if (sweep == "fetch") {  // one config per kernel name, for counter runs: SEPX_BAND rows
     const char* e = std::getenv("SEPX_BAND");
     const int band = e ? std::atoi(e) : 16;
     add(2, band, 2, 0, kOneTask, 0);
@@ -318,10 +430,26 @@ int main(int argc, char** argv) {
         for (int tail : {4, 8}) add(2, band, cap, 0, kTailBands, tail);
     add(2, 16, 2, 0, kQueue, 4);
   }
+  if (sweep == "pattern2") {  // access pattern only: bytes per lane x rows in flight x band
+    for (int aux : {2, 16}) report("copy aux=" + std::to_string(aux), [&](const Frame& f, hipStream_t s) {
+      launch_copy(aux, f, s);
+    });
+    for (int lb : {16, 32, 64})
+      for (int pf : {2, 4, 8})
+        for (int band : {8, 12, 16})
+          for (int cap : {1, 2}) {
+            if (lb == 64 && pf == 8) continue;
+            const PatCfg c{lb, pf, band, cap};
+            char name[96];
+            std::snprintf(name, sizeof name, "pattern wave-row=%dKiB rows-in-flight=%d band=%2d cap=%d", lb / 16, pf, band, cap);
+            report(name, [&](const Frame& f, hipStream_t s) { launch_pat(c, f, s); });
+          }
+    return 0;
+  }
   // correctness of every non-default task mode / band split: byte-equal to the
   // one-task launch (run twice: a queue must come back reset)
   for (const SepCfg& c : cfgs)
-    if (c.mode != kOneTask || c.nw != kWaves) {
+    if ((c.mode != kOneTask || c.nw != kWaves) && c.mode != 9) {
       const int64_t bad = check_same(c);
       std::printf("# %s vs one-task: %lld differing bytes\n", c.name().c_str(), (long long)bad);
       if (bad) return 2;
@@ -332,8 +460,9 @@ int main(int argc, char** argv) {
   for (const SepCfg& c : cfgs) report(c.name(), [&](const Frame& f, hipStream_t s) { launch_sep(c, f, s); });
 
   // per-wave timeline of one cold dispatch (the last of a rotation)
-  std::vector<SepCfg> stamped(3);
-  if (runs) {
+  std::vector<SepCfg> stamped(sweep == "pattern" ? 0 : 3);
+  if (sweep == "pattern") {
+  } else if (runs) {
     stamped[0].band = 16;
     stamped[1].band = 16;
     stamped[1].mode = kRuns;
@@ -357,7 +486,7 @@ int main(int argc, char** argv) {
       c.cap = 0;
       c.nxcd = 8;
     }
-  if (sweep == "wg" || quad || runs) {
+  if (sweep == "wg" || quad || runs || sweep == "pattern") {
   } else if (g_sobel) {
     stamped[0].band = 4;
     stamped[1].band = 8;
