@@ -124,9 +124,11 @@ __global__ __launch_bounds__(256) void k_band_copy2(KArgs a) {
 }
 
 struct PatCfg {
-  int lb, pf, band, cap;
+  int lb, pf, band, cap, r = 2;
 };
 static void (*pat_fn(const PatCfg& c))(KArgs) {
+  if (c.r == 0) return c.pf == 4 ? k_band_copy2<0, 16, 4> : k_band_copy2<0, 16, 8>;
+  if (c.r == 1) return k_band_copy2<1, 16, 4>;
   if (c.lb == 16) return c.pf == 2 ? k_band_copy2<2, 16, 2> : c.pf == 4 ? k_band_copy2<2, 16, 4> : k_band_copy2<2, 16, 8>;
   if (c.lb == 32) return c.pf == 2 ? k_band_copy2<2, 32, 2> : c.pf == 4 ? k_band_copy2<2, 32, 4> : k_band_copy2<2, 32, 8>;
   return c.pf == 2 ? k_band_copy2<2, 64, 2> : k_band_copy2<2, 64, 4>;
@@ -429,6 +431,21 @@ int main(int argc, char** argv) {
       for (int cap : {2, 3})
         for (int tail : {4, 8}) add(2, band, cap, 0, kTailBands, tail);
     add(2, 16, 2, 0, kQueue, 4);
+  }
+  if (sweep == "pattern-halo") {  // the pattern with 0 / 1 / 2 halo rows per side (1 KiB wave rows)
+    for (int aux : {2, 16}) report("copy aux=" + std::to_string(aux), [&](const Frame& f, hipStream_t s) {
+      launch_copy(aux, f, s);
+    });
+    for (int band : {8, 16, 32, 64})
+      for (int r : {0, 1, 2}) {
+        const PatCfg c{16, 4, band, 2, r};
+        char name[96];
+        std::snprintf(name, sizeof name, "pattern halo=%d band=%2d (1 KiB rows, 4 in flight, cap 2)", r, band);
+        report(name, [&](const Frame& f, hipStream_t s) { launch_pat(c, f, s); });
+      }
+    const PatCfg c8{16, 8, 64, 2, 0};
+    report("pattern halo=0 band=64 (8 in flight)", [&](const Frame& f, hipStream_t s) { launch_pat(c8, f, s); });
+    return 0;
   }
   if (sweep == "pattern2") {  // access pattern only: bytes per lane x rows in flight x band
     for (int aux : {2, 16}) report("copy aux=" + std::to_string(aux), [&](const Frame& f, hipStream_t s) {
