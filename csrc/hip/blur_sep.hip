@@ -751,7 +751,13 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
     a.nbands = a.nb0 + (n1 ? (int)div_up(a.ry3 - sa.a2, band) : 0);
     const dim3 grid((unsigned)(cf.nw == 1 ? div_up((int64_t)sa.nstrips * a.nbands, dev::kSepWaves)
                                           : nstrips_w / cf.nw * a.nbands));
-    cf.fn<<<grid, 64 * (cf.nw == 1 ? dev::kSepWaves : cf.nw), cf.lds, s>>>(sa);
+    // lsb on a cache-resident pass (an N=8 stripe): staging each pair between
+    // the barrier and the MFMAs (EARLY = false) is ~2 % faster there (0.0408-
+    // 0.0416 vs 0.0420-0.0425 ms), the early staging on streaming frames and in
+    // the exact mode (profiles/r5/blur/README.md)
+    void (*fn)(dev::SepArgs) = cf.fn;
+    if (lsb && !streaming && &cf == &cfgs[1][1][0]) fn = variants[1][3].fn;
+    fn<<<grid, 64 * (cf.nw == 1 ? dev::kSepWaves : cf.nw), cf.lds, s>>>(sa);
     HIP_CHECK(hipGetLastError());
   }
   if (p.out_margin_px > 0)

@@ -277,14 +277,17 @@ void k_conv_mfma(ConvArgs ca) {
 // tools/mfma_i8_probe.hip), and 16-pixel segments never straddle a 48-pixel row.
 constexpr int kQPS = 96;  // i8 plane row bytes (>= kCWin)
 
-template <int C>
 // m-tiles (16 output rows) per wave: measured 16K conv:31, RGB 2 / 3: 2.059 /
 // 2.037 ms on one box, 2.145-2.165 / 2.186-2.191 on another while MT = 3
 // spilled 4 registers (round 3); spill-free since, MT = 3 is 1-2 % ahead on
 // both precisions (round 4, profiles/r4/blur/conv_mt.txt: exact 2.122-2.163
 // vs 2.157-2.177 ms, lsb 1.575-1.590 vs 1.610-1.616); gray 4 / 6 / 8: 0.771 /
 // 0.683 / 0.717 ms
-constexpr int convq_mt() { return C == 3 ? 3 : 6; }
+// RGB :lsb (2 digits) at 4: 1.505-1.507 vs 1.582-1.586 ms on 16K, 0.185 vs
+// 0.199-0.203 ms per N=8 stripe (round 5, profiles/r5/conv/mt4_lsb_*.txt);
+// 3 digits at 4 spill
+template <int C>
+constexpr int convq_mt(int nd) { return C == 3 ? (nd == 2 ? 4 : 3) : 6; }
 
 template <int C, int MT>
 __host__ __device__ constexpr int convq_rows_staged(int nq) {
@@ -755,7 +758,7 @@ void launch_conv_mfma(const Pass& p, const PassConsts& pc, const PassLaunch& L, 
       const char* e = std::getenv("STRIPE_CONV_MT");
       return e ? std::atoi(e) : 0;
     }();
-    int mt = p.cmid == 3 ? dev::convq_mt<3>() : dev::convq_mt<1>();
+    int mt = p.cmid == 3 ? dev::convq_mt<3>(nd) : dev::convq_mt<1>(nd);
     if (env_mt > 0) mt = env_mt;
     // output tiles per workgroup: 1, or 4 with STRIPE_CONV_NT=4 (the next
     // tile's staging under the current tile's MFMAs, k_conv_i8 NT).  Measured
@@ -773,16 +776,24 @@ void launch_conv_mfma(const Pass& p, const PassConsts& pc, const PassLaunch& L, 
     // (multi-tile instances only where they stay spill-free: RGB at 2
     // m-tiles, gray at 4 or 6)
     if (nt == 4) mt = p.cmid == 3 ? 2 : std::min(mt, 6);
+    auto pick = [&]() {
 #define STRIPE_CONVQ(CC, MM, DD, NT)                                                                         \
     if (p.cmid == CC && mt == MM && nd == DD && nt == NT) {                                                  \
       fn = dev::k_conv_i8<CC, MM, DD, NT>;                                                                   \
       lds = (size_t)(NT > 1 ? 2 : 1) * dev::convq_buf_bytes<CC, MM>(ci.nq);                                  \
     }
-    STRIPE_CONVQ(3, 2, 3, 1) STRIPE_CONVQ(3, 3, 3, 1) STRIPE_CONVQ(1, 4, 3, 1) STRIPE_CONVQ(1, 6, 3, 1)
-    STRIPE_CONVQ(1, 8, 3, 1) STRIPE_CONVQ(3, 2, 2, 1) STRIPE_CONVQ(3, 3, 2, 1) STRIPE_CONVQ(1, 6, 2, 1)
-    STRIPE_CONVQ(3, 2, 3, 4) STRIPE_CONVQ(3, 2, 2, 4) STRIPE_CONVQ(1, 4, 3, 4) STRIPE_CONVQ(1, 6, 3, 4)
-    STRIPE_CONVQ(1, 6, 2, 4)
+      STRIPE_CONVQ(3, 2, 3, 1) STRIPE_CONVQ(3, 3, 3, 1) STRIPE_CONVQ(3, 4, 2, 1) STRIPE_CONVQ(1, 4, 3, 1)
+      STRIPE_CONVQ(1, 6, 3, 1) STRIPE_CONVQ(1, 8, 3, 1) STRIPE_CONVQ(3, 2, 2, 1) STRIPE_CONVQ(3, 3, 2, 1)
+      STRIPE_CONVQ(1, 6, 2, 1) STRIPE_CONVQ(3, 2, 3, 4) STRIPE_CONVQ(3, 2, 2, 4) STRIPE_CONVQ(1, 4, 3, 4)
+      STRIPE_CONVQ(1, 6, 3, 4) STRIPE_CONVQ(1, 6, 2, 4)
 #undef STRIPE_CONVQ
+    };
+    pick();
+    if (!fn && env_mt > 0) {  // an A/B override with no instance for this pass: the default
+      mt = p.cmid == 3 ? dev::convq_mt<3>(nd) : dev::convq_mt<1>(nd);
+      if (nt == 4) mt = p.cmid == 3 ? 2 : std::min(mt, 6);
+      pick();
+    }
     STRIPE_CHECK(fn != nullptr, "no i8 conv kernel for " << p.cmid << " channels x " << mt << " m-tiles x " << nd
                                                           << " digits");
     for (int r = 0; r < L.nrange; ++r) {
