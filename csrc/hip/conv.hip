@@ -283,11 +283,12 @@ constexpr int kQPS = 96;  // i8 plane row bytes (>= kCWin)
 // both precisions (round 4, profiles/r4/blur/conv_mt.txt: exact 2.122-2.163
 // vs 2.157-2.177 ms, lsb 1.575-1.590 vs 1.610-1.616); gray 4 / 6 / 8: 0.771 /
 // 0.683 / 0.717 ms
-// RGB :lsb (2 digits) at 4: 1.505-1.507 vs 1.582-1.586 ms on 16K, 0.185 vs
-// 0.199-0.203 ms per N=8 stripe (round 5, profiles/r5/conv/mt4_lsb_*.txt);
-// 3 digits at 4 spill
+// Round 5 (profiles/r5/conv/README.md): with single-buffered A fragments
+// (k_conv_i8 A1) RGB fits 4 m-tiles at 3 digits and 5 at 2: exact 2.03-2.06
+// vs 2.14-2.16 ms on 16K (0.245-0.252 vs 0.267-0.270 per N=8 stripe), lsb
+// 1.443-1.447 vs 1.517-1.546 (0.180-0.181 vs 0.186-0.187).
 template <int C>
-constexpr int convq_mt(int nd) { return C == 3 ? (nd == 2 ? 4 : 3) : 6; }
+constexpr int convq_mt(int nd) { return C == 3 ? (nd == 2 ? 5 : 4) : 6; }
 
 template <int C, int MT>
 __host__ __device__ constexpr int convq_rows_staged(int nq) {
@@ -326,7 +327,11 @@ struct ConvI8Args {
 // computes and stores one tile: 75 % MFMA busy on 16K conv:31, and still
 // faster than NT = 4, which fits the registers only at 2 m-tiles
 // (profiles/r5/conv/README.md).
-template <int C, int MT, int ND, int NT = 1>
+// A1: one A fragment set instead of two: each fragment is re-read for the next
+// k-step right after its last MFMA of this one (the rest of the step's MFMAs
+// cover the LDS latency), freeing C MT x 4 registers -- what 3 digits at 4
+// m-tiles need to fit without scratch.
+template <int C, int MT, int ND, int NT = 1, bool A1 = false>
 __global__ __launch_bounds__(256, 2) void k_conv_i8(ConvI8Args ca) {
   const KArgs& a = ca.a;
   const int R = ca.R, nq = ca.nq;
@@ -446,14 +451,14 @@ __global__ __launch_bounds__(256, 2) void k_conv_i8(ConvI8Args ca) {
       for (int dg = 0; dg < ND; ++dg)
         bq[slot][dg] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(rtw, off + 1024u * dg, 0, 0));
     };
-    i32x4 af[2][C][MT];
+    i32x4 af[A1 ? 1 : 2][C][MT];
     auto read_a = [&](int q, int s, int buf) __attribute__((always_inline)) {
       const uint8_t* pl = cur + 4 * q * kQPS + aoff[s];
 #pragma unroll
       for (int c = 0; c < C; ++c)
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
-          af[buf][c][mt] = *reinterpret_cast<const i32x4*>(pl + c * pstride + 16 * mt * kQPS);
+          af[A1 ? 0 : buf][c][mt] = *reinterpret_cast<const i32x4*>(pl + c * pstride + 16 * mt * kQPS);
     };
     unit_t sb[kBatch];  // the staging batch in flight (NT > 1)
     load_b(0, 0);
@@ -479,17 +484,34 @@ __global__ __launch_bounds__(256, 2) void k_conv_i8(ConvI8Args ca) {
             if (j * kBatch + b < kG && u < nunits) store_unit(nxt, u, sb[b]);
           }
         }
-        read_a(min((q0 / 3) + (i + 1) / 3, nq - 1), (i + 1) % 3, (i + 1) & 1);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int dg = 0; dg < ND; ++dg)
+        if constexpr (A1) {
+          // fragment (c, mt): its ND MFMAs, then its next-step read in place
+          const uint8_t* pl = cur + 4 * min((q0 / 3) + (i + 1) / 3, nq - 1) * kQPS + aoff[(i + 1) % 3];
+          __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int c = 0; c < C; ++c)
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt)
-              acc[dg][c][mt] =
-                  __builtin_amdgcn_mfma_i32_16x16x64_i8(af[i & 1][c][mt], bq[i % 3][dg], acc[dg][c][mt], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
+            for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+              for (int dg = 0; dg < ND; ++dg)
+                acc[dg][c][mt] =
+                    __builtin_amdgcn_mfma_i32_16x16x64_i8(af[0][c][mt], bq[i % 3][dg], acc[dg][c][mt], 0, 0, 0);
+              af[0][c][mt] = *reinterpret_cast<const i32x4*>(pl + c * pstride + 16 * mt * kQPS);
+            }
+          __builtin_amdgcn_sched_barrier(0);
+        } else {
+          read_a(min((q0 / 3) + (i + 1) / 3, nq - 1), (i + 1) % 3, (i + 1) & 1);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int dg = 0; dg < ND; ++dg)
+#pragma unroll
+            for (int c = 0; c < C; ++c)
+#pragma unroll
+              for (int mt = 0; mt < MT; ++mt)
+                acc[dg][c][mt] =
+                    __builtin_amdgcn_mfma_i32_16x16x64_i8(af[i & 1][c][mt], bq[i % 3][dg], acc[dg][c][mt], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
     }
     if constexpr (NT > 1) {
@@ -776,7 +798,23 @@ void launch_conv_mfma(const Pass& p, const PassConsts& pc, const PassLaunch& L, 
     // (multi-tile instances only where they stay spill-free: RGB at 2
     // m-tiles, gray at 4 or 6)
     if (nt == 4) mt = p.cmid == 3 ? 2 : std::min(mt, 6);
+    // single-buffered A fragments (k_conv_i8 A1) wherever an instance exists;
+    // STRIPE_CONV_A1=0 for A/B runs against the double-buffered kernels
+    static const bool env_a1 = [] {
+      const char* e = std::getenv("STRIPE_CONV_A1");
+      return !(e && std::atoi(e) == 0);
+    }();
     auto pick = [&]() {
+      if (env_a1 && nt == 1) {
+#define STRIPE_CONVQ1(CC, MM, DD)                                                                            \
+    if (p.cmid == CC && mt == MM && nd == DD) {                                                              \
+      fn = dev::k_conv_i8<CC, MM, DD, 1, true>;                                                              \
+      lds = (size_t)dev::convq_buf_bytes<CC, MM>(ci.nq);                                                     \
+    }
+        STRIPE_CONVQ1(3, 4, 3) STRIPE_CONVQ1(3, 5, 2)
+#undef STRIPE_CONVQ1
+        if (fn) return;
+      }
 #define STRIPE_CONVQ(CC, MM, DD, NT)                                                                         \
     if (p.cmid == CC && mt == MM && nd == DD && nt == NT) {                                                  \
       fn = dev::k_conv_i8<CC, MM, DD, NT>;                                                                   \
@@ -789,8 +827,8 @@ void launch_conv_mfma(const Pass& p, const PassConsts& pc, const PassLaunch& L, 
 #undef STRIPE_CONVQ
     };
     pick();
-    if (!fn && env_mt > 0) {  // an A/B override with no instance for this pass: the default
-      mt = p.cmid == 3 ? dev::convq_mt<3>(nd) : dev::convq_mt<1>(nd);
+    if (!fn) {  // an A/B override with no instance for this pass: the double-buffered defaults
+      mt = p.cmid == 3 ? (nd == 2 ? 4 : 3) : 6;
       if (nt == 4) mt = p.cmid == 3 ? 2 : std::min(mt, 6);
       pick();
     }

@@ -1,0 +1,133 @@
+#!/bin/bash
+# Round 5's GPU studies in one script (each wrote what profiles/r5/<dir>/
+# keeps; that directory's README names the study):
+#   bash tools/gpu/gpu_r5_study.sh <study> [out-subdir]
+# studies:
+#   bench    driver bench command (N=1, 2 frames; 1 frame / 1 stream; the N=8
+#            share) and a kernel trace of the share           -> r5/bench
+#   cold     sepx task modes / store policy / stamps, cold share + 16K frame,
+#            kernel trace                                       -> r5/cold
+#   shapes   sepx workgroup shapes (wg), stacked bands (quad), XCD-local
+#            band runs (runs) + their L2 fill bytes              -> r5/cold
+#   pattern  the stencil's access pattern without arithmetic    -> r5/cold
+#   order    separable task order through the engine: tests, bench, kbench
+#                                                                -> r5/order
+#   sobel    config 3's sobel share (warm / cold), quad order   -> r5/cfg3
+#   cfg3     4 local ranks: halo depths, auto vs explicit       -> r5/cfg3
+#   conv     conv:31 tiles per workgroup, m-tiles, A-fragment buffering
+#                                                                -> r5/conv
+#   convprof conv:31 counters (exact, lsb)                      -> r5/conv
+#   blur     blur:31 staging order A/B, counters                -> r5/blur
+#   jpeg     JPEG pixel stages: vectorised vs legacy kernels    -> r5/jpeg
+#   e2e      e2e pipeline chunk count                           -> r5/e2e
+# Every GPU step runs under its own timeout; a failing step ends the script.
+set -o pipefail
+S=${1:?study}
+R=$(pwd)
+O=$R/gpurun_out/r5/${2:-$S}
+mkdir -p $O
+export TMPDIR=/tmp
+C31="$(python3 -c "print('conv:31:' + ';'.join(str(((i*7)%13-4)/400.0) for i in range(961)))")"
+KB="python tools/kbench.py"
+gpu_tests() {  # $1: pytest selection
+  timeout -k 10 600 python -u -m pytest $1 -m gpu -q --timeout 200 --timeout-method thread > $O/tests_$S.txt 2>&1
+}
+case $S in
+bench)
+  gpu_tests tests || exit 2
+  timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/bench_n1.json 2> $O/bench_n1.err || exit 3
+  timeout -k 10 300 python bench.py --steps 20 --warmup 5 --frames 1 --streams 1 > $O/bench_n1_f1s1.json 2> $O/bench_n1_f1s1.err || exit 3
+  timeout -k 10 300 python bench.py --steps 20 --warmup 5 --height 2048 > $O/bench_stripe.json 2> $O/bench_stripe.err || exit 3
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_stripe -o stripe -- python3 bench.py --steps 20 --warmup 5 --height 2048 --dist-steps 0 --ref-steps 0 --e2e-steps 0 --deep-steps 0 > $O/prof_stripe.log 2>&1 || exit 4
+  ;;
+cold)
+  for sw in tail policy; do
+    timeout -k 10 300 bin/sepx 2048 0 $O/stamps_$sw $sw > $O/sepx_2048_$sw.txt 2>&1 || exit 2
+    timeout -k 10 300 bin/sepx 16384 1 "" $sw > $O/sepx_16384_$sw.txt 2>&1 || exit 2
+  done
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_sepx -o sepx -- bin/sepx 2048 0 > $O/prof_sepx.txt 2>&1 || exit 3
+  ;;
+shapes)
+  for sw in wg quad runs; do
+    timeout -k 10 300 bin/sepx 2048 0 $O/stamps_$sw $sw > $O/sepx_${sw}_2048.txt 2>&1 || exit 2
+    timeout -k 10 300 bin/sepx 16384 1 "" $sw > $O/sepx_${sw}_16k.txt 2>&1 || exit 2
+  done
+  cd /tmp
+  for b in 16 32; do
+    export SEPX_BAND=$b
+    timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch$b -o run -- $R/bin/sepx 16384 1 "" fetch > $O/pmc_fetch$b.log 2>&1 || exit 3
+    python3 $R/tools/prof_summary.py $O/pmc_fetch$b/run_results.db > $O/fetch_runs_band$b.txt 2>&1 || exit 3
+  done
+  ;;
+pattern)
+  timeout -k 10 300 bin/sepx 16384 1 "" pattern > $O/pattern_bandcopy_16k.txt 2>&1 || exit 2
+  timeout -k 10 300 bin/sepx 2048 0 "" pattern > $O/pattern_bandcopy_2048.txt 2>&1 || exit 2
+  timeout -k 10 300 bin/sepx 16384 1 "" pattern2 > $O/pattern_sweep_16k.txt 2>&1 || exit 2
+  timeout -k 10 300 bin/sepx 16384 1 "" pattern-halo > $O/pattern_halo_16k.txt 2>&1 || exit 2
+  ;;
+order)
+  gpu_tests "tests/test_r5_order.py tests/test_gpu_r3.py tests/test_gpu_engine.py" || exit 2
+  for r in 1 2; do
+    for o in 0 1 t; do
+      if [ $o = t ]; then unset STRIPE_SEP_ORDER; else export STRIPE_SEP_ORDER=$o; fi
+      timeout -k 10 300 python bench.py --steps 100 --warmup 10 > $O/bench_o${o}_$r.json 2> $O/bench_o${o}_$r.err || exit 3
+    done
+  done
+  unset STRIPE_SEP_ORDER
+  for o in 0 1 0 1; do
+    STRIPE_SEP_ORDER=$o timeout -k 10 200 $KB --chains "gaussian5|gaussian3" --shape 16384x16384x3 --bands=-1 --iters 30 >> $O/kb_16k_o$o.txt 2>&1 || exit 4
+    STRIPE_SEP_ORDER=$o timeout -k 10 200 $KB --chains "gaussian5" --shape 16384x2048x3 --bands=-1 --iters 50 >> $O/kb_stripe_o$o.txt 2>&1 || exit 4
+  done
+  ;;
+sobel)
+  timeout -k 10 300 bin/sepx 2048 1 $O/stamps_sobel sobel > $O/sepx_sobel_warm.txt 2>&1 || exit 2
+  timeout -k 10 300 bin/sepx 2048 0 "" sobel > $O/sepx_sobel_cold.txt 2>&1 || exit 2
+  timeout -k 10 300 bin/sepx 2048 1 "" sobelquad > $O/sepx_sobelquad_warm.txt 2>&1 || exit 2
+  ;;
+cfg3)
+  STRIPE_LOG=debug timeout -k 10 120 bin/stripe bench --synthetic 8192x8192x1 --chain sobel --ranks 4 --iters 5 --warmup 1 --scope resident --backend local 2>&1 | grep -i depth > $O/local_auto_depthlog.txt
+  for d in 1 8 16 21 32 0 1 8 16 21 32 0; do
+    echo "depth $d" >> $O/local_depth_sweep.txt
+    timeout -k 10 120 bin/stripe bench --synthetic 8192x8192x1 --chain sobel --ranks 4 --iters 64 --warmup 8 --scope resident --backend local --halo-depth $d 2>&1 | grep -v amdgpu.ids >> $O/local_depth_sweep.txt || exit 2
+  done
+  ;;
+conv)
+  gpu_tests "tests/test_oracle_conv.py tests/test_gpu_large.py" || exit 2
+  for r in 1 2; do
+    for v in d db nt4; do
+      # d: single-buffered A, 4 / 5 m-tiles (default); db: double-buffered A,
+      # 3 / 4 m-tiles (STRIPE_CONV_A1=0); nt4: 4 tiles per workgroup
+      case $v in d) E="" ;; db) E="STRIPE_CONV_A1=0" ;; nt4) E="STRIPE_CONV_NT=4 STRIPE_CONV_A1=0" ;; esac
+      env $E timeout -k 10 200 $KB --chains "$C31|$C31:lsb" --shape 16384x16384x3 --iters 6 >> $O/conv31_16k_$v.txt 2>&1 || exit 3
+      env $E timeout -k 10 200 $KB --chains "$C31|$C31:lsb" --shape 16384x2048x3 --iters 20 >> $O/conv31_stripe_$v.txt 2>&1 || exit 3
+    done
+  done
+  ;;
+convprof)
+  timeout -k 10 900 bash scripts/profile.sh "$C31|" 16384x16384x3 $O/prof_conv31 > $O/prof_conv31.txt 2>&1 || exit 4
+  timeout -k 10 900 bash scripts/profile.sh "$C31:lsb|" 16384x16384x3 $O/prof_conv31_lsb > $O/prof_conv31_lsb.txt 2>&1 || exit 4
+  ;;
+blur)
+  gpu_tests tests/test_oracle_conv.py || exit 2
+  for v in 0 3 0 3; do
+    STRIPE_BLUR_VARIANT=$v timeout -k 10 120 $KB --chains "blur:31|blur:31:lsb" --shape 16384x16384x3 --iters 30 >> $O/v${v}_16k.txt 2>&1 || exit 3
+    STRIPE_BLUR_VARIANT=$v timeout -k 10 120 $KB --chains "blur:31|blur:31:lsb" --shape 16384x2048x3 --iters 60 >> $O/v${v}_stripe.txt 2>&1 || exit 3
+  done
+  timeout -k 10 600 bash scripts/profile.sh "blur:31|" 16384x16384x3 $O/prof_blur31 > $O/prof_blur31.txt 2>&1 || exit 4
+  timeout -k 10 600 bash scripts/profile.sh "blur:31:lsb|" 16384x16384x3 $O/prof_blur31_lsb > $O/prof_blur31_lsb.txt 2>&1 || exit 4
+  ;;
+jpeg)
+  cd /tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_jpeg_new -o run -- python3 $R/tools/jpegbench.py --size 8192 --reps 3 > $O/jpegbench_new.json 2> $O/jpegbench_new.err || exit 2
+  export STRIPE_JPEG_COLOR=1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_jpeg_old -o run -- python3 $R/tools/jpegbench.py --size 8192 --reps 3 > $O/jpegbench_old.json 2> $O/jpegbench_old.err || exit 2
+  ;;
+e2e)
+  timeout -k 10 400 python tools/e2e_chunks.py > $O/chunks_16k.json 2> $O/chunks.err || exit 2
+  ;;
+*)
+  echo "unknown study $S" >&2
+  exit 1
+  ;;
+esac
+echo done
