@@ -449,6 +449,12 @@ int cmd_bench(const Args& a) {
               fr.back()->set_stage_timing(false);
               fr.back()->load_synthetic(seed + (uint64_t)f);
             }
+            // one GPU per rank (not `local` ranks sharing one): each frame on a
+            // stream with a hardware queue of its own (Engine::dedicated_stream)
+            if ((backend != "local" || N == 1) && cfg.backend == BackendKind::Device)
+              for (int f = 0; f < nframes; ++f)
+                fr[(size_t)f]->use_external_stream(
+                    Engine::dedicated_stream(std::max(0, fr[(size_t)f]->config().device), f % 8));
             fr[0]->tune();
             for (int f = 1; f < nframes; ++f) fr[f]->set_tuning(fr[0]->bands(), fr[0]->caps(), fr[0]->policies(), fr[0]->orders());
             const bool it_ok = fr[0]->plan().cin == fr[0]->plan().cout;

@@ -136,6 +136,13 @@ class Engine {
   hipStream_t stream() const { return s_compute_; }
   // Run everything on an externally owned stream (e.g. torch's current stream).
   void use_external_stream(hipStream_t s);
+  // Stream `index` (0 .. 7) of `device` on a hardware queue of its own (a
+  // CU-masked stream with every CU enabled): created on first use, kept for
+  // the process.  Plain streams share the GPU_MAX_HW_QUEUES queues
+  // round-robin, so two frames meant to overlap can land on one queue and
+  // serialise -- 35.6 vs 41.4 us per step of a cold N=8 share after any other
+  // library created streams (profiles/r5/streams/README.md).
+  static hipStream_t dedicated_stream(int device, int index);
 
   // ---- input ----
   void load_synthetic(uint64_t seed);                     // own stripe, generated in place

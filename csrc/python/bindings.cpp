@@ -324,6 +324,30 @@ PYBIND11_MODULE(_C, m) {
     return d;
   }, py::arg("comm"), py::arg("device"), py::arg("bytes"), py::arg("frames") = 4, py::arg("streams") = 2,
      py::arg("iters") = 500);
+  // A HIP stream on a hardware queue of its own: a CU-masked stream (all CUs
+  // enabled) gets a dedicated HSA queue, where plain streams share the
+  // GPU_MAX_HW_QUEUES queues round-robin -- two frames meant to overlap may
+  // otherwise land on one queue and serialise.  Returns the handle (int).
+  m.def("dedicated_stream", [](int device, int index) {
+    return reinterpret_cast<uintptr_t>(Engine::dedicated_stream(device, index));
+  }, py::arg("device"), py::arg("index"));
+  m.def("stream_create", [](int device, bool dedicated) {
+    HIP_CHECK(hipSetDevice(device));
+    hipStream_t s = nullptr;
+    if (dedicated) {
+      int cus = 0;
+      HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+      std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0xFFFFFFFFu);
+      HIP_CHECK(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+    } else {
+      HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    }
+    return reinterpret_cast<uintptr_t>(s);
+  }, py::arg("device"), py::arg("dedicated") = true);
+  m.def("stream_destroy", [](uintptr_t s) {
+    HIP_CHECK(hipStreamSynchronize(reinterpret_cast<hipStream_t>(s)));
+    HIP_CHECK(hipStreamDestroy(reinterpret_cast<hipStream_t>(s)));
+  }, py::arg("stream"));
   // Same-box streaming floor of the benchmark record: hand-written linear copy
   // of `bytes` rotating over `frames` buffer pairs (csrc/hip/pointwise.hip).
   m.def("copy_roofline", [](int device, int64_t bytes, int frames, int reps) {

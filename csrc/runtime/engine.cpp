@@ -7,6 +7,7 @@
 #include "engine_internal.h"
 
 #include <algorithm>
+#include <map>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -186,6 +187,27 @@ Engine::~Engine() {
     if (own_compute_ && s_compute_) (void)hipStreamDestroy(s_compute_);
     (void)hipGetLastError();  // teardown errors must not leak into the caller's next HIP check
   }
+}
+
+hipStream_t Engine::dedicated_stream(int device, int index) {
+  constexpr int kMax = 8;
+  STRIPE_CHECK(index >= 0 && index < kMax, "dedicated stream index " << index << " out of [0, " << kMax << ")");
+  static std::mutex mu;
+  static std::map<std::pair<int, int>, hipStream_t> pool;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = pool.find({device, index});
+  if (it != pool.end()) return it->second;
+  int prev = 0;
+  HIP_CHECK(hipGetDevice(&prev));
+  HIP_CHECK(hipSetDevice(device));
+  int cus = 0;
+  HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+  std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0xFFFFFFFFu);
+  hipStream_t s = nullptr;
+  HIP_CHECK(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+  HIP_CHECK(hipSetDevice(prev));
+  pool[{device, index}] = s;
+  return s;
 }
 
 void Engine::use_external_stream(hipStream_t s) {

@@ -318,7 +318,17 @@ class FrameStream:
         self.streams = []
         self.nstreams = 1
         if ctx.device:
-            self.streams = [torch.cuda.Stream() for _ in range(nmax)]
+            # the frames' streams on hardware queues of their own (process-wide,
+            # C.dedicated_stream): pool streams share GPU_MAX_HW_QUEUES queues
+            # round-robin, and once another library has created streams two of
+            # them can land on one queue (cold N=8 share: 41.4 us a step on two
+            # such streams, 35.6 us on dedicated queues, profiles/r5/streams/);
+            # STRIPE_FRAME_QUEUES=pool keeps torch's pool streams (A/B)
+            if os.environ.get("STRIPE_FRAME_QUEUES", "dedicated") == "pool":
+                self.streams = [torch.cuda.Stream() for _ in range(nmax)]
+            else:
+                self.streams = [torch.cuda.ExternalStream(C.dedicated_stream(ctx.gpu, k), device=ctx.gpu)
+                                for k in range(nmax)]
             for f in self.frames:
                 f.engine.stage_timing = stage_timing
         self.set_streams(nmax)
