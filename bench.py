@@ -290,7 +290,9 @@ def main():
         sched = dict(fs.pick_schedule(max_over_ranks, barrier), requested="auto")
         if world == 1:
             sched["chosen"] = "none (one rank: no exchange)"
-    nstreams = fs.nstreams  # the probe may have settled on one stream
+    nstreams = fs.nstreams  # the probe may have settled on one stream (and picked the stream set)
+    streams = fs.streams
+    stream = streams[0] if streams else None
     log.info("halo schedule: %s on %d stream(s) %s", sched["chosen"], nstreams, sched["ms"])
     step = fs.step
     sync_frames = fs.synchronize

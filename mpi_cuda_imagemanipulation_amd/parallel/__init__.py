@@ -317,18 +317,24 @@ class FrameStream:
                        for i in range(frames)]
         self.streams = []
         self.nstreams = 1
+        self.queues = "none"
+        self._sets = {}
         if ctx.device:
-            # the frames' streams on hardware queues of their own (process-wide,
-            # C.dedicated_stream): pool streams share GPU_MAX_HW_QUEUES queues
-            # round-robin, and once another library has created streams two of
-            # them can land on one queue (cold N=8 share: 41.4 us a step on two
-            # such streams, 35.6 us on dedicated queues, profiles/r5/streams/);
-            # STRIPE_FRAME_QUEUES=pool keeps torch's pool streams (A/B)
-            if os.environ.get("STRIPE_FRAME_QUEUES", "dedicated") == "pool":
-                self.streams = [torch.cuda.Stream() for _ in range(nmax)]
-            else:
-                self.streams = [torch.cuda.ExternalStream(C.dedicated_stream(ctx.gpu, k), device=ctx.gpu)
-                                for k in range(nmax)]
+            # two stream sets: torch's pool streams, which share GPU_MAX_HW_QUEUES
+            # hardware queues round-robin (once another library has created
+            # streams, two of them can land on one queue: cold N=8 share 41.4
+            # us a step), and streams with hardware queues of their own
+            # (process-wide, C.dedicated_stream: 35.6 us), which in turn made
+            # cross-stream event schedules slower on some boxes
+            # (profiles/r5/streams/).  pick_schedule measures both;
+            # STRIPE_FRAME_QUEUES=pool|dedicated pins one.
+            self._sets["dedicated"] = [torch.cuda.ExternalStream(C.dedicated_stream(ctx.gpu, k), device=ctx.gpu)
+                                       for k in range(nmax)]
+            self._sets["pool"] = [torch.cuda.Stream() for _ in range(nmax)]
+            pin = os.environ.get("STRIPE_FRAME_QUEUES", "")
+            self.queue_options = [pin] if pin in self._sets else (["dedicated", "pool"] if nmax > 1 else ["dedicated"])
+            self.queues = self.queue_options[0]
+            self.streams = self._sets[self.queues]
             for f in self.frames:
                 f.engine.stage_timing = stage_timing
         self.set_streams(nmax)
@@ -363,6 +369,14 @@ class FrameStream:
         else:
             cache = "warm"
         return frames, streaming, cold, cache
+
+    def set_queues(self, kind: str):
+        """Use the "dedicated" or the "pool" stream set (same stream count)."""
+        if not getattr(self, "_sets", {}):
+            return
+        self.queues = kind
+        self.streams = self._sets[kind]
+        self.set_streams(self.nstreams)
 
     def set_streams(self, n: int):
         """Queue frame f on stream f mod n (n <= the streams created)."""
@@ -408,8 +422,10 @@ class FrameStream:
         """Time every halo schedule (interior / boundary overlap, the
         three-stream pipeline, the plain serial one),
         with the frames on one stream or alternating over two, on the real
-        transport, and keep the fastest; returns {"chosen", "streams", "ms"}
-        ("ms" keys: schedule, or schedule@streams when both counts are tried).
+        transport, and keep the fastest; two streams come from either stream
+        set (dedicated hardware queues or torch's pool, set_queues); returns
+        {"chosen", "streams", "queues", "ms"} ("ms" keys: schedule, or
+        schedule@streams[/queues] when several are tried).
         Which one wins depends on the link and RCCL's per-exchange cost, which
         one GPU cannot show, so the job measures it where it runs.
         reduce_max(ms) -> max over ranks and barrier() keep every rank on the
@@ -430,18 +446,30 @@ class FrameStream:
                     eff.append(self.schedule)
             scheds = eff
         opts = list(self.stream_options)
-        cands = [(s, ns) for ns in opts for s in scheds]
-        key = (lambda c: f"{c[0]}@{c[1]}") if len(opts) > 1 else (lambda c: c[0])
+        sets = getattr(self, "_sets", {})
+        qopts = list(getattr(self, "queue_options", ["dedicated"])) if sets else ["none"]
+        # one stream: the queue kind makes no difference (the dedicated set)
+        cands = [(s, ns, q) for ns in opts for s in scheds for q in (qopts if ns > 1 else qopts[:1])]
+
+        def key(c):
+            k = c[0] if len(opts) == 1 else f"{c[0]}@{c[1]}"
+            return k + (f"/{c[2]}" if c[1] > 1 and len(qopts) > 1 else "")
+
         if len(cands) == 1:
             self.set_schedule(scheds[0])
+            if sets:
+                self.set_queues(cands[0][2])
             self.set_streams(opts[0])
-            return {"chosen": self.schedule, "streams": self.nstreams, "ms": {}}
+            return {"chosen": self.schedule, "streams": self.nstreams, "queues": getattr(self, "queues", "none"),
+                    "ms": {}}
         n = steps if steps > 0 else max(60, 4 * len(self.frames))
         best = {}
         for _ in range(rounds):
             for c in cands:
                 self.synchronize()
                 self.set_schedule(c[0])
+                if sets:
+                    self.set_queues(c[2])
                 self.set_streams(c[1])
                 for i in range(2 * len(self.frames)):
                     self.step(i)
@@ -456,8 +484,11 @@ class FrameStream:
         chosen = min(cands, key=lambda c: best[c])
         self.synchronize()
         self.set_schedule(chosen[0])
+        if sets:
+            self.set_queues(chosen[2])
         self.set_streams(chosen[1])
-        return {"chosen": chosen[0], "streams": self.nstreams, "ms": {key(c): round(v, 5) for c, v in best.items()}}
+        return {"chosen": chosen[0], "streams": self.nstreams, "queues": getattr(self, "queues", "none"),
+                "ms": {key(c): round(v, 5) for c, v in best.items()}}
 
     def stream_of(self, i: int):
         return self.streams[(i % len(self.frames)) % self.nstreams] if self.streams else None

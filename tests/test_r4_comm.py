@@ -359,7 +359,8 @@ def test_frame_stream_pick_schedule_single_candidate(C, monkeypatch):
     fs = parallel.FrameStream(ctx, m.models.Pipeline("gaussian5", halo_depth=1), 64, 40, 3)
     calls = []
     got = fs.pick_schedule(lambda v: calls.append(v) or v)
-    assert got == {"chosen": "serial", "streams": 1, "ms": {}} and not calls and fs.schedule == "serial"
+    assert got == {"chosen": "serial", "streams": 1, "queues": "none", "ms": {}} and not calls
+    assert fs.schedule == "serial"
 
 
 def test_frame_stream_pick_schedule_takes_fastest_max_over_ranks():

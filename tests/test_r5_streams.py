@@ -1,0 +1,85 @@
+"""FrameStream stream sets: torch's pool streams (shared hardware queues) or
+streams with hardware queues of their own (C.dedicated_stream); the schedule
+probe measures both with two streams and keeps the fastest
+(profiles/r5/streams/README.md)."""
+import time
+
+import pytest
+
+import mpi_cuda_imagemanipulation_amd as m
+from mpi_cuda_imagemanipulation_amd import parallel
+
+
+def _stand_in(cost):
+    from types import SimpleNamespace
+
+    frames = [SimpleNamespace(engine=SimpleNamespace(halo_schedule="serial")) for _ in range(4)]
+    fs = parallel.FrameStream.__new__(parallel.FrameStream)
+    fs.frames = frames
+    fs._sets = {"dedicated": ["d0", "d1"], "pool": ["p0", "p1"]}
+    fs.queue_options = ["dedicated", "pool"]
+    fs.queues = "dedicated"
+    fs.streams = fs._sets["dedicated"]
+    fs.stream_options = [1, 2]
+    fs.nstreams = 1
+    applied = []
+
+    def set_streams(n):
+        fs.nstreams = n
+        applied.append((tuple(fs.streams), n))
+
+    fs.set_streams = set_streams
+    fs.step = lambda i=None: time.sleep(cost(frames[0].engine.halo_schedule, fs.nstreams, fs.queues))
+    fs.synchronize = lambda: None
+    return fs, frames
+
+
+def test_probe_picks_stream_set():
+    # two streams on the pool set are fastest here: the probe must land there
+    def cost(sched, n, q):
+        base = {"pipeline": 0.004, "overlap": 0.003, "serial": 0.002}[sched]
+        return base / 2 if (n == 2 and q == "pool") else base
+
+    fs, frames = _stand_in(cost)
+    got = fs.pick_schedule(steps=2, rounds=1)
+    assert got["chosen"] == "serial" and got["streams"] == 2 and got["queues"] == "pool"
+    assert fs.streams == ["p0", "p1"] and fs.nstreams == 2
+    # one stream is timed once (the queue kind makes no difference there)
+    assert set(got["ms"]) == {f"{s}@1" for s in fs.SCHEDULES} | {f"{s}@2/{q}" for s in fs.SCHEDULES
+                                                                  for q in ("dedicated", "pool")}
+
+
+def test_probe_keeps_dedicated_when_faster():
+    def cost(sched, n, q):
+        return 0.001 if (sched == "overlap" and n == 2 and q == "dedicated") else 0.003
+
+    fs, _ = _stand_in(cost)
+    got = fs.pick_schedule(steps=2, rounds=1)
+    assert (got["chosen"], got["streams"], got["queues"]) == ("overlap", 2, "dedicated")
+    assert fs.streams == ["d0", "d1"]
+
+
+def test_pinned_queue_kind(monkeypatch):
+    # host engines have no stream sets: the pin is ignored, nothing breaks
+    monkeypatch.setenv("STRIPE_FRAME_QUEUES", "pool")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    ctx = parallel.init("gloo")
+    fs = parallel.FrameStream(ctx, m.models.Pipeline("gaussian5", halo_depth=1), 64, 40, 3)
+    assert fs.streams == [] and fs.queues == "none"
+
+
+@pytest.mark.gpu
+def test_dedicated_streams_are_reused_gpu():
+    import torch
+
+    C = m._C
+    a, b = C.dedicated_stream(0, 0), C.dedicated_stream(0, 1)
+    assert a and b and a != b and C.dedicated_stream(0, 0) == a  # process-wide, created once
+    x = torch.arange(1 << 20, device="cuda", dtype=torch.int32)
+    with torch.cuda.stream(torch.cuda.ExternalStream(a)):
+        y = x * 3
+    torch.cuda.synchronize()
+    assert int(y[-1]) == 3 * ((1 << 20) - 1)
+    with pytest.raises(Exception):
+        C.dedicated_stream(0, 8)
