@@ -160,11 +160,15 @@ int Engine::choose_depth() const {
     if (const char* e = std::getenv("STRIPE_HALO_DEPTH")) k = std::atoi(e);
   }
   if (plan_.cin != plan_.cout) k = 1;                          // not iterable: one chain per run
-  // redundant rows <= ~1 % of the stripe, at most 32 steps per exchange (the
+  // redundant rows <= ~1 % of the stripe (2 % when the exchange is the
+  // in-process `local` hub, ~0.1 ms each), at most 32 steps per exchange (the
   // cap was 8 until round 5: 4 local ranks on 8192^2 sobel, 2048-row
-  // stripes, step 0.043-0.045 ms at depth 8, 0.033-0.035 at 16, 0.034 at 21
-  // (this rule's pick), 0.029-0.030 at 32, profiles/r5/cfg3/README.md)
-  if (k <= 0) k = std::min(32, 1 + (minrows / 100) / S);
+  // stripes, step 0.043-0.045 ms at depth 8, 0.033-0.035 at 16 and 21,
+  // 0.029-0.030 at 32, profiles/r5/cfg3/README.md)
+  if (k <= 0) {
+    const bool local = comm_ && std::strcmp(comm_->backend(), "local") == 0;
+    k = std::min(32, 1 + (minrows / (local ? 50 : 100)) / S);
+  }
   // every neighbour must own the k*S rows it sends (and keep its own interior)
   k = std::min(k, minrows / (2 * S));
   return k >= 1 ? k : 0;
