@@ -311,6 +311,7 @@ struct ConvI8Args {
   KArgs a;
   const i32x4* tw;  // B fragments: [quad][kstep 3][digit ND][lane 64]
   int K, R, nq;     // kernel size, radius, 4-row quads (even)
+  int split;        // 1: the two-part epilogue even where one conversion is exact (A/B)
   double scale, bias;
 };
 
@@ -531,26 +532,35 @@ __global__ __launch_bounds__(256, 2) void k_conv_i8(ConvI8Args ca) {
     // ---- epilogue: sum(x W) exactly in f64, * 2^-S, round half even, saturate;
     // the tile leaves through LDS (`cur`, done with) as 16-byte row chunks ----
     uint8_t* otile = cur;
+    // a digit sum |D| <= K^2 * 128 * 128 is exact in f32 up to K = 32 (<= 2^24):
+    // one conversion and one FMA per digit (7 VALU an output at 3 digits instead
+    // of 19).  At K = 33 it reaches 1.78e7, so each goes to f32 as two exact
+    // parts (D - (D & 255) keeps <= 17 significant bits, D & 255 <= 8).  The
+    // scales are powers of two, the f32 FMAs round the result to ~2^-15 (an
+    // output changes only within ~1e-4 of a tie), and v_cvt_pk_u8_f32 rounds
+    // half to even and saturates.
+    auto epilogue = [&](auto split_c) __attribute__((always_inline)) {
+      constexpr bool SPLIT = decltype(split_c)::value;
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
+      for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
+        for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int c = 0; c < C; ++c) {
-          // a digit sum |D| <= K^2 * 128 * 128 reaches 1.78e7 > 2^24 at K = 33,
-          // so each goes to f32 as two exact parts (D - (D & 255) keeps <= 17
-          // significant bits, D & 255 <= 8); the scales are powers of two, the
-          // f32 FMAs round the result to ~2^-15 (an output changes only within
-          // ~1e-4 of a tie), and v_cvt_pk_u8_f32 rounds half to even and saturates
-          auto part = [&](int d, float s, float acc_in) __attribute__((always_inline)) {
-            const int D = acc[d][c][mt][r];
-            const int lo8 = D & 255;
-            return __builtin_fmaf((float)(D - lo8), s, __builtin_fmaf((float)lo8, s, acc_in));
-          };
-          const float lo2 = part(1, s1, part(0, s0, bias));
-          const float v = ND == 3 ? part(ND - 1, s2, lo2) : lo2;
-          otile[(16 * mt + 4 * g + r) * kOS + (16 * wave + m) * C + c] = (uint8_t)__builtin_amdgcn_cvt_pk_u8_f32(v, 0, 0u);
-        }
+          for (int c = 0; c < C; ++c) {
+            auto part = [&](int d, float s, float acc_in) __attribute__((always_inline)) {
+              const int D = acc[d][c][mt][r];
+              if constexpr (!SPLIT) return __builtin_fmaf((float)D, s, acc_in);
+              const int lo8 = D & 255;
+              return __builtin_fmaf((float)(D - lo8), s, __builtin_fmaf((float)lo8, s, acc_in));
+            };
+            const float lo2 = part(1, s1, part(0, s0, bias));
+            const float v = ND == 3 ? part(ND - 1, s2, lo2) : lo2;
+            otile[(16 * mt + 4 * g + r) * kOS + (16 * wave + m) * C + c] =
+                (uint8_t)__builtin_amdgcn_cvt_pk_u8_f32(v, 0, 0u);
+          }
+    };
+    if (ca.K <= 32 && !ca.split) epilogue(std::false_type{});
+    else epilogue(std::true_type{});
     __syncthreads();
     constexpr int NCO = kCTN * C / 16;
 #pragma unroll
@@ -773,6 +783,11 @@ void launch_conv_mfma(const Pass& p, const PassConsts& pc, const PassLaunch& L, 
     ci.K = p.K;
     ci.R = p.R;
     ci.nq = conv_quads(p.K);
+    static const int env_split = [] {  // STRIPE_CONV_SPLIT=1: two-part epilogue at every K (A/B)
+      const char* e = std::getenv("STRIPE_CONV_SPLIT");
+      return e && std::atoi(e) == 1 ? 1 : 0;
+    }();
+    ci.split = env_split;
     ci.scale = pc.conv_scale;
     ci.bias = pc.conv_bias;
     // m-tiles per wave (STRIPE_CONV_MT overrides for A/B runs)
