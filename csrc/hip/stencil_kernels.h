@@ -865,6 +865,99 @@ __global__ __launch_bounds__(NW * kW, (F::K >= 7 ? 2 : (SKIP && EXP ? 3 : 4))) v
 }
 
 // ------------------------------------------------------------------------------
+// Gray sobel (|Gx| + |Gy|, saturated) on row pairs
+// ------------------------------------------------------------------------------
+// k_sep packs two horizontally adjacent pixels into a u16 pair, so every
+// horizontal tap of a row needs a v_alignbit for the odd neighbour (~160 VALU
+// a row).  Here a dword holds one pixel of two consecutive rows (y, y + 1):
+// the vertical smoothing / difference of both output rows is one packed op,
+// a pixel's horizontal neighbours are whole registers (the lane edges by DPP
+// wave shifts), and a step emits two rows (~122 VALU a row).  Same task
+// mapping, lane layout and stores as k_sep<1, Sobel, PRO_NONE>; bit-identical.
+// Pixel j of a lane (byte j of its 16-byte chunk) of rows a, b as a u16 pair.
+__device__ __forceinline__ uint32_t rows_pair(const u32x4& ra, const u32x4& rb, int j) {
+  const uint32_t k = (uint32_t)(j & 3);
+  return __builtin_amdgcn_perm(rb[j >> 2], ra[j >> 2], k | 0x0C00u | ((4u + k) << 16) | 0x0C000000u);
+}
+
+template <int SAUX>
+__global__ __launch_bounds__(kNT, 4) void k_sobel_rp(KArgs a) {
+  const WaveTask t = wave_task(a);
+  if (!t.valid) return;
+  const int lane = t.lane;
+  const int ys = t.ys, ye = t.ye;
+  const int cb = t.xt * (kOutChunks * 16) - 16 + lane * 16;
+  const uint32_t lane_in = cb < a.E + 16 ? (uint32_t)cb : kOOB;
+  const OutLanes lout = out_lanes<false>(a, lane, cb - 16 * lane);
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);
+  const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
+  // rows past the band's lower halo row (ye) re-read it: they feed unstored outputs
+  auto load = [&](int y) __attribute__((always_inline)) {
+    return __builtin_amdgcn_raw_buffer_load_b128(rin, in_row_off(a, min(y, ye)) + lane_in, 0, kLoadAux);
+  };
+  // A[j] = (r(y - 1), r(y)) of the current step y (the previous step's B)
+  uint32_t A[16];
+  u32x4 r0;  // row y
+  {
+    const u32x4 rm = load(ys - 1);
+    r0 = load(ys);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) A[j] = rows_pair(rm, r0, j);
+  }
+  // rows y + 1, y + 2 of this step and of the next one in flight
+  u32x4 nx[2][2];
+  nx[0][0] = load(ys + 1);
+  nx[0][1] = load(ys + 2);
+  nx[1][0] = load(ys + 3);
+  nx[1][1] = load(ys + 4);
+  auto step = [&](int y, u32x4 (&cur)[2]) __attribute__((always_inline)) {
+    const u32x4 r1 = cur[0], r2 = cur[1];
+    cur[0] = load(y + 5);  // the step after next
+    cur[1] = load(y + 6);
+    uint32_t S[18], D[18];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t mid = rows_pair(r0, r1, j);  // (r(y), r(y + 1))
+      const uint32_t b = rows_pair(r1, r2, j);    // (r(y + 1), r(y + 2))
+      // vertical [1 2 1] of rows y, y + 1: halves <= 1020, no carry across
+      S[j + 1] = A[j] + b + (mid << 1);
+      D[j + 1] = as_u32(as_i16x2(b) - as_i16x2(A[j]));  // [-1 0 1]
+      A[j] = b;
+    }
+    // neighbours across the lane edges: lane l - 1's last pixel, lane l + 1's first
+    S[0] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)S[16], 0x138, 0xf, 0xf, false);
+    D[0] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)D[16], 0x138, 0xf, 0xf, false);
+    S[17] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)S[1], 0x130, 0xf, 0xf, false);
+    D[17] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)D[1], 0x130, 0xf, 0xf, false);
+    uint32_t mg[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const i16x2 gx = as_i16x2(S[j + 2]) - as_i16x2(S[j]);
+      const i16x2 gy = as_i16x2(D[j]) + as_i16x2(D[j + 2]) + (as_i16x2(D[j + 1]) << (short)1);
+      const i16x2 mm = __builtin_elementwise_max(gx, -gx) + __builtin_elementwise_max(gy, -gy);
+      mg[j] = as_u32(__builtin_elementwise_min(mm, (i16x2)(short)255));
+    }
+    uint32_t o0[4], o1[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t p01 = __builtin_amdgcn_perm(mg[4 * q + 1], mg[4 * q], 0x06020400u);
+      const uint32_t p23 = __builtin_amdgcn_perm(mg[4 * q + 3], mg[4 * q + 2], 0x06020400u);
+      o0[q] = __builtin_amdgcn_perm(p23, p01, 0x05040100u);  // row y
+      o1[q] = __builtin_amdgcn_perm(p23, p01, 0x07060302u);  // row y + 1
+    }
+    store_out<false, SAUX>(o0, rout, y < ye, a.out_org + (uint32_t)((int64_t)y * a.out_pitch), lout, nullptr, lane);
+    store_out<false, SAUX>(o1, rout, y + 1 < ye, a.out_org + (uint32_t)((int64_t)(y + 1) * a.out_pitch), lout,
+                           nullptr, lane);
+    r0 = r2;
+  };
+  for (int y = ys; y < ye; y += 4) {
+    step(y, nx[0]);
+    step(y + 2, nx[1]);
+  }
+  band_margins<1, 1>(a, t);
+}
+
+// ------------------------------------------------------------------------------
 // Direct (non-separable) filters: emboss3/5, sharpen, laplace
 // ------------------------------------------------------------------------------
 // The last K input rows live in registers, unpacked to u16 pairs and extended
@@ -1128,6 +1221,21 @@ void launch_one(bool skip, bool nt, int wgs, KArgs a, int tiles, int n0, int n1,
         const K fn = fns[2 * skip + nt];
         plan_bands(a, grid, tiles, n0, n1, band, F::R, 0);
         grid = dim3((unsigned)runs_grid(tiles, a.nbands));
+        fn<<<grid, kNT, nt_lds_reserve((const void*)fn, stencil_cap(nt, wgs, kNtWgsSep)), s>>>(a);
+        return;
+      }
+    }
+  }
+  if constexpr (F::SEP && F::SOBEL && C == 1 && PRO == PRO_NONE && !EXP) {
+    if constexpr (!F::L2) {
+      // gray L1 sobel on row pairs (STRIPE_SOBEL_RP=0: the k_sep form, A/B)
+      static const bool rp = [] {
+        const char* e = std::getenv("STRIPE_SOBEL_RP");
+        return !(e && std::atoi(e) == 0);
+      }();
+      if (rp && !skip) {
+        const K fn = nt ? k_sobel_rp<kNtAux> : k_sobel_rp<0>;
+        plan_bands(a, grid, tiles, n0, n1, band, F::R, 0);
         fn<<<grid, kNT, nt_lds_reserve((const void*)fn, stencil_cap(nt, wgs, kNtWgsSep)), s>>>(a);
         return;
       }
