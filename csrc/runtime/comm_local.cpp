@@ -12,6 +12,7 @@
 #include <deque>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "stripe/comm.h"
@@ -19,6 +20,16 @@
 #include "stripe/trace.h"
 
 namespace stripe {
+
+namespace {
+inline void cpu_relax() {
+#if defined(__x86_64__) || defined(__i386__)
+  __builtin_ia32_pause();
+#else
+  std::this_thread::yield();
+#endif
+}
+}  // namespace
 
 void Comm::wait(hipStream_t s) {
   if (device_buffers() && s) HIP_CHECK(hipStreamSynchronize(s));
@@ -95,7 +106,7 @@ class LocalHub {
     while (!pred() && !aborted_ && std::chrono::steady_clock::now() < spin_end) {
       const uint64_t v = ver_.load(std::memory_order_acquire);
       lk.unlock();
-      for (int k = 0; k < 256 && ver_.load(std::memory_order_acquire) == v; ++k) __builtin_ia32_pause();
+      for (int k = 0; k < 256 && ver_.load(std::memory_order_acquire) == v; ++k) cpu_relax();
       lk.lock();
     }
     const auto deadline = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s_);
