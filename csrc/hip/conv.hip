@@ -287,8 +287,11 @@ constexpr int kQPS = 96;  // i8 plane row bytes (>= kCWin)
 // (k_conv_i8 A1) RGB fits 4 m-tiles at 3 digits and 5 at 2: exact 2.03-2.06
 // vs 2.14-2.16 ms on 16K (0.245-0.252 vs 0.267-0.270 per N=8 stripe), lsb
 // 1.443-1.447 vs 1.517-1.546 (0.180-0.181 vs 0.186-0.187).
+// Gray :lsb at 10 (single-buffered A): 0.472-0.474 vs 0.526-0.533 ms on 16K
+// gray conv:31; gray exact gains nothing past 6 (0.689-0.695 at 10 / 12 vs
+// 0.682-0.697, profiles/r5/conv/gray_mt*.txt).
 template <int C>
-constexpr int convq_mt(int nd) { return C == 3 ? (nd == 2 ? 5 : 4) : 6; }
+constexpr int convq_mt(int nd) { return C == 3 ? (nd == 2 ? 5 : 4) : (nd == 2 ? 10 : 6); }
 
 template <int C, int MT>
 __host__ __device__ constexpr int convq_rows_staged(int nq) {
@@ -826,7 +829,7 @@ void launch_conv_mfma(const Pass& p, const PassConsts& pc, const PassLaunch& L, 
       fn = dev::k_conv_i8<CC, MM, DD, 1, true>;                                                              \
       lds = (size_t)dev::convq_buf_bytes<CC, MM>(ci.nq);                                                     \
     }
-        STRIPE_CONVQ1(3, 4, 3) STRIPE_CONVQ1(3, 5, 2)
+        STRIPE_CONVQ1(3, 4, 3) STRIPE_CONVQ1(3, 5, 2) STRIPE_CONVQ1(1, 10, 2)
 #undef STRIPE_CONVQ1
         if (fn) return;
       }
