@@ -67,6 +67,62 @@ __global__ __launch_bounds__(256) void k_jpeg_idct(const int16_t* __restrict__ c
   }
 }
 
+// IDCT with a lane per block row: a wave owns 8 blocks (lane = 8 b + r).  A
+// lane loads its row's 8 coefficients with one 16-byte load (a block's 128
+// bytes by 8 lanes), runs the row pass in registers, trades rows for columns
+// through LDS for the column pass, and rows back for the store: one 8-byte
+// store of a block row per lane, 8 blocks of a block row side by side (64
+// contiguous bytes per image row) instead of a byte store per thread.  The
+// sums run in the same order with the same operations as k_jpeg_idct (fp
+// contraction is off in this file): bit-identical.
+__global__ __launch_bounds__(256) void k_jpeg_idct8(const int16_t* __restrict__ coef, int64_t nblocks, int bw,
+                                                    uint8_t* __restrict__ plane, int64_t ps) {
+  __shared__ float tt[4][8][65];   // [wave][block][row * 8 + col], padded against bank conflicts
+  __shared__ uint8_t ob[4][8][72];  // [wave][block][row * 9 + col]
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int bl = l >> 3, r = l & 7;
+  const int64_t b = ((int64_t)blockIdx.x * 4 + w) * 8 + bl;
+  const bool ok = b < nblocks;
+  typedef int v4i __attribute__((ext_vector_type(4)));
+  v4i raw = {0, 0, 0, 0};
+  if (ok) raw = *reinterpret_cast<const v4i*>(coef + b * 64 + r * 8);
+  float f[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) f[u] = (float)(int16_t)((uint32_t)raw[u >> 1] >> (16 * (u & 1)));
+  // row pass: t[r][c] = sum_u basis[c][u] f[r][u]
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    float sum = 0.f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) sum += kJpegBasis[c * 8 + u] * f[u];
+    tt[w][bl][r * 8 + c] = sum;
+  }
+  __syncthreads();
+  // column pass for column c = r of this lane's block: o[x][c] = sum_v basis[x][v] t[v][c]
+  const int c = r;
+  float tc[8];
+#pragma unroll
+  for (int v = 0; v < 8; ++v) tc[v] = tt[w][bl][v * 8 + c];
+#pragma unroll
+  for (int x = 0; x < 8; ++x) {
+    float o = 0.f;
+#pragma unroll
+    for (int v = 0; v < 8; ++v) o += kJpegBasis[x * 8 + v] * tc[v];
+    ob[w][bl][x * 9 + c] = jpeg_u8(o + 128.f);
+  }
+  __syncthreads();
+  if (!ok) return;
+  uint32_t lo = 0, hi = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    lo |= (uint32_t)ob[w][bl][r * 9 + k] << (8 * k);
+    hi |= (uint32_t)ob[w][bl][r * 9 + 4 + k] << (8 * k);
+  }
+  const int64_t by = b / bw, bx = b % bw;
+  typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+  *reinterpret_cast<v2u*>(plane + (by * 8 + r) * ps + bx * 8) = v2u{lo, hi};
+}
+
 struct JpegPlaneRef {
   const uint8_t* p;
   int64_t ps;
@@ -441,6 +497,15 @@ bool pin_uploads() {
   return on;
 }
 // STRIPE_JPEG_COLOR=1: the per-pixel colour / planes kernels (A/B switch)
+// STRIPE_JPEG_IDCT=1: the block-per-wave IDCT (k_jpeg_idct) for A/B runs
+bool legacy_idct() {
+  static const bool on = [] {
+    const char* e = std::getenv("STRIPE_JPEG_IDCT");
+    return e && std::atoi(e) == 1;
+  }();
+  return on;
+}
+
 bool legacy_color() {
   static const bool on = [] {
     const char* e = std::getenv("STRIPE_JPEG_COLOR");
@@ -519,7 +584,8 @@ void jpeg_pixels_device(const JpegCoefs& jc, uint8_t* dst, int64_t pitch, hipStr
       else (void)hipGetLastError();  // not registrable: the pageable copy below still works
     }
     HIP_CHECK(hipMemcpyAsync(dcoef, c.coef.data(), cbytes, hipMemcpyHostToDevice, s));
-    dev::k_jpeg_idct<<<blocks_for(nb, 4), 256, 0, s>>>(dcoef, nb, c.bw, planes[(size_t)ci], ps);
+    if (legacy_idct()) dev::k_jpeg_idct<<<blocks_for(nb, 4), 256, 0, s>>>(dcoef, nb, c.bw, planes[(size_t)ci], ps);
+    else dev::k_jpeg_idct8<<<blocks_for(nb, 32), 256, 0, s>>>(dcoef, nb, c.bw, planes[(size_t)ci], ps);
     HIP_CHECK(hipGetLastError());
     st.free_async(dcoef);
     ref[ci] = {planes[(size_t)ci], ps, (jc.W * c.h + jc.hmax - 1) / jc.hmax, (jc.H * c.v + jc.vmax - 1) / jc.vmax,

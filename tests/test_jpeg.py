@@ -465,3 +465,20 @@ def test_vectorised_color_and_planes_match_per_pixel_kernels(tmp_path):
         a, b = np.load(tmp_path / f"dec{k}_new.npy"), np.load(tmp_path / f"dec{k}_old.npy")
         assert a.shape == b.shape and np.array_equal(a, b), k
         assert (tmp_path / f"enc{k}_new.jpg").read_bytes() == (tmp_path / f"enc{k}_old.jpg").read_bytes(), k
+
+
+@pytest.mark.gpu
+def test_row_idct_matches_per_block_kernel(tmp_path):
+    # k_jpeg_idct8 (a lane per block row, 8-byte row stores) against the
+    # per-block IDCT it replaces (STRIPE_JPEG_IDCT=1): same sums in the same
+    # order, so decoded pixels must be bit-identical over every sampling mode
+    script = tmp_path / "w.py"
+    script.write_text(_COLOR_WORKER)
+    for tag, legacy in (("new", "0"), ("old", "1")):
+        env = dict(os.environ, STRIPE_ROOT=ROOT, OUT=str(tmp_path), TAG=tag, STRIPE_JPEG_IDCT=legacy)
+        r = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0 and "DONE" in r.stdout, (r.stdout + r.stderr)[-3000:]
+    n = int([ln for ln in r.stdout.splitlines() if ln.startswith("DONE")][0].split()[1])
+    for k in range(n):
+        a, b = np.load(tmp_path / f"dec{k}_new.npy"), np.load(tmp_path / f"dec{k}_old.npy")
+        assert a.shape == b.shape and np.array_equal(a, b), k

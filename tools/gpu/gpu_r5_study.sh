@@ -19,6 +19,7 @@
 #   convprof conv:31 counters (exact, lsb)                      -> r5/conv
 #   blur     blur:31 staging order A/B, counters                -> r5/blur
 #   jpeg     JPEG pixel stages: vectorised vs legacy kernels    -> r5/jpeg
+#   idct     JPEG IDCT: row-per-lane vs per-block kernel        -> r5/jpeg
 #   e2e      e2e pipeline chunk count                           -> r5/e2e
 # Every GPU step runs under its own timeout; a failing step ends the script.
 set -o pipefail
@@ -121,6 +122,13 @@ jpeg)
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_jpeg_new -o run -- python3 $R/tools/jpegbench.py --size 8192 --reps 3 > $O/jpegbench_new.json 2> $O/jpegbench_new.err || exit 2
   export STRIPE_JPEG_COLOR=1
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_jpeg_old -o run -- python3 $R/tools/jpegbench.py --size 8192 --reps 3 > $O/jpegbench_old.json 2> $O/jpegbench_old.err || exit 2
+  ;;
+idct)
+  gpu_tests tests/test_jpeg.py || exit 2
+  cd /tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_idct_new -o run -- python3 $R/tools/jpegbench.py --size 8192 --reps 3 > $O/idct_new.json 2> $O/idct_new.err || exit 3
+  export STRIPE_JPEG_IDCT=1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_idct_old -o run -- python3 $R/tools/jpegbench.py --size 8192 --reps 3 > $O/idct_old.json 2> $O/idct_old.err || exit 3
   ;;
 e2e)
   timeout -k 10 400 python tools/e2e_chunks.py > $O/chunks_16k.json 2> $O/chunks.err || exit 2
