@@ -19,6 +19,7 @@
 #   convprof conv:31 counters (exact, lsb)                      -> r5/conv
 #   blur     blur:31 staging order A/B, counters                -> r5/blur
 #   jpeg     JPEG pixel stages: vectorised vs legacy kernels    -> r5/jpeg
+#   pitch    row pitch sweep: copy / band walk / stencil            -> r5/cold
 #   idct     JPEG IDCT: row-per-lane vs per-block kernel        -> r5/jpeg
 #   e2e      e2e pipeline chunk count                           -> r5/e2e
 # Every GPU step runs under its own timeout; a failing step ends the script.
@@ -122,6 +123,12 @@ jpeg)
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_jpeg_new -o run -- python3 $R/tools/jpegbench.py --size 8192 --reps 3 > $O/jpegbench_new.json 2> $O/jpegbench_new.err || exit 2
   export STRIPE_JPEG_COLOR=1
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_jpeg_old -o run -- python3 $R/tools/jpegbench.py --size 8192 --reps 3 > $O/jpegbench_old.json 2> $O/jpegbench_old.err || exit 2
+  ;;
+pitch)
+  for pad in 0 256 512 1024 2048 3072 4096 8192; do
+    SEPX_PAD=$pad timeout -k 10 120 bin/sepx 16384 1 "" pitch > $O/pitch_16k_$pad.txt 2>&1 || exit 2
+    SEPX_PAD=$pad timeout -k 10 120 bin/sepx 2048 0 "" pitch > $O/pitch_2048_$pad.txt 2>&1 || exit 2
+  done
   ;;
 idct)
   gpu_tests tests/test_jpeg.py || exit 2

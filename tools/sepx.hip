@@ -6,7 +6,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Icsrc/include -Icsrc/hip \
 //         -o bin/sepx tools/sepx.hip
 //   bin/sepx [rows] [frames] [stamp_csv_prefix] [sweep: tail | policy | sobel | wg | quad | sobelquad | runs | fetch |
-//             pattern]
+//             pattern | pitch (SEPX_PAD=bytes added to the row pitch)]
 //
 // Every measurement rotates over `frames` independent in/out buffer pairs
 // (default: enough that frames x (in + out) > 3 x 256 MiB), so each launch
@@ -347,6 +347,7 @@ int main(int argc, char** argv) {
     g_out_px = 1;
   }
   g_pitch = padded_pitch(g_W, g_C);
+  if (const char* e = std::getenv("SEPX_PAD")) g_pitch += std::atoi(e) & ~255;  // row pitch sweep (256 B steps)
   g_org = 2 * g_pitch + kMarginBytes;
   g_bytes = (int64_t)(g_rows + 4) * g_pitch + 256;
   if (F <= 0) F = std::max<int>(1, (int)div_up(3ll * (256 << 20), 2 * g_bytes));
@@ -385,7 +386,13 @@ int main(int argc, char** argv) {
     c.tail = tail;
     cfgs.push_back(c);
   };
-  if (sweep == "pattern") {  // the stencil's access pattern without its arithmetic
+  if (sweep == "pitch") {  // one row pitch (SEPX_PAD): linear copy, the band walk, the production launch
+    report("copy aux=2", [&](const Frame& f, hipStream_t s) { launch_copy(2, f, s); });
+    const PatCfg c{16, 4, 16, 2, 2};
+    report("pattern halo=2 band=16", [&](const Frame& f, hipStream_t s) { launch_pat(c, f, s); });
+    add(2, 12, 2, 0, kOneTask, 0);
+    add(2, 16, 2, 0, kOneTask, 0);
+  } else if (sweep == "pattern") {  // the stencil's access pattern without its arithmetic
     for (int band : {12, 16, 32}) {
       add(2, band, 2, 0, 9, 0);
       add(2, band, 2, 0, kOneTask, 0);
@@ -477,8 +484,9 @@ int main(int argc, char** argv) {
   for (const SepCfg& c : cfgs) report(c.name(), [&](const Frame& f, hipStream_t s) { launch_sep(c, f, s); });
 
   // per-wave timeline of one cold dispatch (the last of a rotation)
-  std::vector<SepCfg> stamped(sweep == "pattern" ? 0 : 3);
-  if (sweep == "pattern") {
+  const bool nostamp = sweep == "pattern" || sweep == "pitch";
+  std::vector<SepCfg> stamped(nostamp ? 0 : 3);
+  if (nostamp) {
   } else if (runs) {
     stamped[0].band = 16;
     stamped[1].band = 16;
@@ -503,7 +511,7 @@ int main(int argc, char** argv) {
       c.cap = 0;
       c.nxcd = 8;
     }
-  if (sweep == "wg" || quad || runs || sweep == "pattern") {
+  if (sweep == "wg" || quad || runs || nostamp) {
   } else if (g_sobel) {
     stamped[0].band = 4;
     stamped[1].band = 8;
