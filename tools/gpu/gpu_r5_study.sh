@@ -20,6 +20,7 @@
 #   blur     blur:31 staging order A/B, counters                -> r5/blur
 #   jpeg     JPEG pixel stages: vectorised vs legacy kernels    -> r5/jpeg
 #   pitch    row pitch sweep: copy / band walk / stencil            -> r5/cold
+#   tlb      address-translation counters: copy / band walk / stencil -> r5/cold
 #   idct     JPEG IDCT: row-per-lane vs per-block kernel        -> r5/jpeg
 #   e2e      e2e pipeline chunk count                           -> r5/e2e
 # Every GPU step runs under its own timeout; a failing step ends the script.
@@ -129,6 +130,11 @@ pitch)
     SEPX_PAD=$pad timeout -k 10 120 bin/sepx 16384 1 "" pitch > $O/pitch_16k_$pad.txt 2>&1 || exit 2
     SEPX_PAD=$pad timeout -k 10 120 bin/sepx 2048 0 "" pitch > $O/pitch_2048_$pad.txt 2>&1 || exit 2
   done
+  ;;
+tlb)
+  cd /tmp
+  timeout -s KILL 120 rocprofv3 --pmc TCP_UTCL1_REQUEST_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_MISS_UNDER_MISS_sum --output-format csv -d $O/tlb_a -o run -- $R/bin/sepx 16384 1 "" pitch > $O/tlb_a.log 2>&1 || exit 2
+  timeout -s KILL 120 rocprofv3 --pmc TCP_UTCL1_SERIALIZATION_STALL_sum TCP_UTCL1_THRASHING_STALL_sum TCP_UTCL1_STALL_INFLIGHT_MAX_sum TCP_UTCL1_PERMISSION_MISS_sum --output-format csv -d $O/tlb_b -o run -- $R/bin/sepx 16384 1 "" pitch > $O/tlb_b.log 2>&1 || exit 2
   ;;
 idct)
   gpu_tests tests/test_jpeg.py || exit 2
