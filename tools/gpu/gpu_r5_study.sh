@@ -21,6 +21,7 @@
 #   jpeg     JPEG pixel stages: vectorised vs legacy kernels    -> r5/jpeg
 #   pitch    row pitch sweep: copy / band walk / stencil            -> r5/cold
 #   tlb      address-translation counters: copy / band walk / stencil -> r5/cold
+#   convform conv:31 timed as 5-iteration vs 30-iteration bursts     -> r5/conv
 #   idct     JPEG IDCT: row-per-lane vs per-block kernel        -> r5/jpeg
 #   e2e      e2e pipeline chunk count                           -> r5/e2e
 # Every GPU step runs under its own timeout; a failing step ends the script.
@@ -135,6 +136,14 @@ tlb)
   cd /tmp
   timeout -s KILL 120 rocprofv3 --pmc TCP_UTCL1_REQUEST_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_MISS_UNDER_MISS_sum --output-format csv -d $O/tlb_a -o run -- $R/bin/sepx 16384 1 "" pitch > $O/tlb_a.log 2>&1 || exit 2
   timeout -s KILL 120 rocprofv3 --pmc TCP_UTCL1_SERIALIZATION_STALL_sum TCP_UTCL1_THRASHING_STALL_sum TCP_UTCL1_STALL_INFLIGHT_MAX_sum TCP_UTCL1_PERMISSION_MISS_sum --output-format csv -d $O/tlb_b -o run -- $R/bin/sepx 16384 1 "" pitch > $O/tlb_b.log 2>&1 || exit 2
+  ;;
+convform)
+  for r in 1 2; do
+    timeout -k 10 200 $KB --shape 16384x16384x3 --chains "$C31|" --iters 5 --warmup 1 >> $O/cfgform_exact.txt 2>&1 || exit 2
+    timeout -k 10 200 $KB --shape 16384x16384x3 --chains "$C31:lsb|" --iters 5 --warmup 1 >> $O/cfgform_lsb.txt 2>&1 || exit 2
+    timeout -k 10 200 $KB --shape 16384x16384x3 --chains "$C31|$C31:lsb" --iters 6 >> $O/studyform.txt 2>&1 || exit 2
+    timeout -k 10 200 $KB --shape 16384x16384x3 --chains "$C31|$C31:lsb" --iters 30 >> $O/studyform_30.txt 2>&1 || exit 2
+  done
   ;;
 idct)
   gpu_tests tests/test_jpeg.py || exit 2
