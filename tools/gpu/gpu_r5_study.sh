@@ -22,6 +22,7 @@
 #   pitch    row pitch sweep: copy / band walk / stencil            -> r5/cold
 #   tlb      address-translation counters: copy / band walk / stencil -> r5/cold
 #   convform conv:31 timed as 5-iteration vs 30-iteration bursts     -> r5/conv
+#   warm     cache-resident gaussian5 configs, repeated                -> r5/warm
 #   idct     JPEG IDCT: row-per-lane vs per-block kernel        -> r5/jpeg
 #   e2e      e2e pipeline chunk count                           -> r5/e2e
 # Every GPU step runs under its own timeout; a failing step ends the script.
@@ -143,6 +144,13 @@ convform)
     timeout -k 10 200 $KB --shape 16384x16384x3 --chains "$C31:lsb|" --iters 5 --warmup 1 >> $O/cfgform_lsb.txt 2>&1 || exit 2
     timeout -k 10 200 $KB --shape 16384x16384x3 --chains "$C31|$C31:lsb" --iters 6 >> $O/studyform.txt 2>&1 || exit 2
     timeout -k 10 200 $KB --shape 16384x16384x3 --chains "$C31|$C31:lsb" --iters 30 >> $O/studyform_30.txt 2>&1 || exit 2
+  done
+  ;;
+warm)
+  for r in 1 2 3; do
+    timeout -k 10 200 $KB --shape 4096x4096x3 --chains gaussian5 --bands=-1 --iters 50 >> $O/cfg2.txt 2>&1 || exit 2
+    timeout -k 10 200 $KB --shape 16384x2048x3 --chains gaussian5 --bands=-1 --iters 50 >> $O/stripe.txt 2>&1 || exit 2
+    timeout -k 10 200 $KB --shape 16384x2048x3 --chains gaussian5 --bands=4 --iters 50 >> $O/stripe_b4.txt 2>&1 || exit 2
   done
   ;;
 idct)
