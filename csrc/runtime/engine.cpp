@@ -192,8 +192,13 @@ Engine::~Engine() {
 hipStream_t Engine::dedicated_stream(int device, int index) {
   constexpr int kMax = 8;
   STRIPE_CHECK(index >= 0 && index < kMax, "dedicated stream index " << index << " out of [0, " << kMax << ")");
-  static std::mutex mu;
-  static std::map<std::pair<int, int>, hipStream_t> pool;
+  // Leaked on purpose (never destroyed by a static destructor); the streams
+  // are released by an exit handler registered after the HIP runtime (and any
+  // profiler tool) initialised, so it runs before their teardown: a CU-masked
+  // stream still alive when the runtime tears down crashed a process under
+  // rocprofv3 at exit (profiles/r5/bench/README.md)
+  static std::mutex& mu = *new std::mutex;
+  static std::map<std::pair<int, int>, hipStream_t>& pool = *new std::map<std::pair<int, int>, hipStream_t>;
   std::lock_guard<std::mutex> lk(mu);
   auto it = pool.find({device, index});
   if (it != pool.end()) return it->second;
@@ -207,6 +212,18 @@ hipStream_t Engine::dedicated_stream(int device, int index) {
   HIP_CHECK(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
   HIP_CHECK(hipSetDevice(prev));
   pool[{device, index}] = s;
+  static const bool registered = [] {
+    std::atexit([] {
+      std::lock_guard<std::mutex> g(mu);
+      for (auto& kv : pool) {
+        (void)hipStreamSynchronize(kv.second);
+        (void)hipStreamDestroy(kv.second);
+      }
+      pool.clear();
+    });
+    return true;
+  }();
+  (void)registered;
   return s;
 }
 

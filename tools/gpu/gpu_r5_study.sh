@@ -23,6 +23,8 @@
 #   tlb      address-translation counters: copy / band walk / stencil -> r5/cold
 #   convform conv:31 timed as 5-iteration vs 30-iteration bursts     -> r5/conv
 #   warm     cache-resident gaussian5 configs, repeated                -> r5/warm
+#   benchprof the driver's bench command under a kernel trace         -> r5/bench
+#   exitprobe process exit under rocprofv3 with an RCCL communicator -> r5/bench
 #   idct     JPEG IDCT: row-per-lane vs per-block kernel        -> r5/jpeg
 #   e2e      e2e pipeline chunk count                           -> r5/e2e
 # Every GPU step runs under its own timeout; a failing step ends the script.
@@ -151,6 +153,18 @@ warm)
     timeout -k 10 200 $KB --shape 4096x4096x3 --chains gaussian5 --bands=-1 --iters 50 >> $O/cfg2.txt 2>&1 || exit 2
     timeout -k 10 200 $KB --shape 16384x2048x3 --chains gaussian5 --bands=-1 --iters 50 >> $O/stripe.txt 2>&1 || exit 2
     timeout -k 10 200 $KB --shape 16384x2048x3 --chains gaussian5 --bands=4 --iters 50 >> $O/stripe_b4.txt 2>&1 || exit 2
+  done
+  ;;
+benchprof)
+  cd /tmp
+  export STRIPE_FRAME_QUEUES=${QUEUES:-dedicated}
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_n1 -o run -- python3 $R/bench.py --steps 20 --warmup 5 $BENCH_ARGS > $O/bench_n1_prof.json 2> $O/bench_n1_prof.err || exit 2
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_stripe -o run -- python3 $R/bench.py --steps 20 --warmup 5 --height 2048 > $O/bench_stripe_prof.json 2> $O/bench_stripe_prof.err || exit 2
+  ;;
+exitprobe)
+  cd /tmp
+  for mode in ${MODES:-release keep}; do
+    timeout -k 10 120 rocprofv3 --kernel-trace -d $O/p_$mode -o run -- python3 $R/tools/exit_probe.py $mode > $O/$mode.log 2>&1 || exit 2
   done
   ;;
 idct)
