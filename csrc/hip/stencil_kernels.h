@@ -880,7 +880,48 @@ __device__ __forceinline__ uint32_t rows_pair(const u32x4& ra, const u32x4& rb, 
   return __builtin_amdgcn_perm(rb[j >> 2], ra[j >> 2], k | 0x0C00u | ((4u + k) << 16) | 0x0C000000u);
 }
 
-template <int SAUX>
+// Two output rows (y, y + 1) from rows y - 1 .. y + 2: r0 = row y, r1 = y + 1,
+// r2 = y + 2; A[j] holds (r(y - 1), r(y)) on entry and (r(y + 1), r(y + 2))
+// on return; o0 / o1 are the lane's 16 output bytes of rows y / y + 1.
+__device__ __forceinline__ void sobel_rp_step(const u32x4& r0, const u32x4& r1, const u32x4& r2, uint32_t (&A)[16],
+                                              uint32_t (&o0)[4], uint32_t (&o1)[4]) {
+  uint32_t S[18], D[18];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const uint32_t mid = rows_pair(r0, r1, j);  // (r(y), r(y + 1))
+    const uint32_t b = rows_pair(r1, r2, j);    // (r(y + 1), r(y + 2))
+    // vertical [1 2 1] of rows y, y + 1: halves <= 1020, no carry across
+    S[j + 1] = A[j] + b + (mid << 1);
+    D[j + 1] = as_u32(as_i16x2(b) - as_i16x2(A[j]));  // [-1 0 1]
+    A[j] = b;
+  }
+  // neighbours across the lane edges: lane l - 1's last pixel, lane l + 1's first
+  S[0] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)S[16], 0x138, 0xf, 0xf, false);
+  D[0] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)D[16], 0x138, 0xf, 0xf, false);
+  S[17] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)S[1], 0x130, 0xf, 0xf, false);
+  D[17] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)D[1], 0x130, 0xf, 0xf, false);
+  uint32_t mg[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const i16x2 gx = as_i16x2(S[j + 2]) - as_i16x2(S[j]);
+    const i16x2 gy = as_i16x2(D[j]) + as_i16x2(D[j + 2]) + (as_i16x2(D[j + 1]) << (short)1);
+    const i16x2 mm = __builtin_elementwise_max(gx, -gx) + __builtin_elementwise_max(gy, -gy);
+    mg[j] = as_u32(__builtin_elementwise_min(mm, (i16x2)(short)255));
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t p01 = __builtin_amdgcn_perm(mg[4 * q + 1], mg[4 * q], 0x06020400u);
+    const uint32_t p23 = __builtin_amdgcn_perm(mg[4 * q + 3], mg[4 * q + 2], 0x06020400u);
+    o0[q] = __builtin_amdgcn_perm(p23, p01, 0x05040100u);  // row y
+    o1[q] = __builtin_amdgcn_perm(p23, p01, 0x07060302u);  // row y + 1
+  }
+}
+
+// PB = 0: rows streamed two steps ahead (any band height).  PB > 0: the band
+// is PB rows and all PB + 2 input rows are requested up front, so a wave
+// waits for one memory round trip, not one per step (a short-lived wave's
+// life is mostly those waits: profiles/r5/cfg3/README.md).
+template <int SAUX, int PB = 0>
 __global__ __launch_bounds__(kNT, 4) void k_sobel_rp(KArgs a) {
   const WaveTask t = wave_task(a);
   if (!t.valid) return;
@@ -895,64 +936,52 @@ __global__ __launch_bounds__(kNT, 4) void k_sobel_rp(KArgs a) {
   auto load = [&](int y) __attribute__((always_inline)) {
     return __builtin_amdgcn_raw_buffer_load_b128(rin, in_row_off(a, min(y, ye)) + lane_in, 0, kLoadAux);
   };
-  // A[j] = (r(y - 1), r(y)) of the current step y (the previous step's B)
-  uint32_t A[16];
-  u32x4 r0;  // row y
-  {
-    const u32x4 rm = load(ys - 1);
-    r0 = load(ys);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) A[j] = rows_pair(rm, r0, j);
-  }
-  // rows y + 1, y + 2 of this step and of the next one in flight
-  u32x4 nx[2][2];
-  nx[0][0] = load(ys + 1);
-  nx[0][1] = load(ys + 2);
-  nx[1][0] = load(ys + 3);
-  nx[1][1] = load(ys + 4);
-  auto step = [&](int y, u32x4 (&cur)[2]) __attribute__((always_inline)) {
-    const u32x4 r1 = cur[0], r2 = cur[1];
-    cur[0] = load(y + 5);  // the step after next
-    cur[1] = load(y + 6);
-    uint32_t S[18], D[18];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const uint32_t mid = rows_pair(r0, r1, j);  // (r(y), r(y + 1))
-      const uint32_t b = rows_pair(r1, r2, j);    // (r(y + 1), r(y + 2))
-      // vertical [1 2 1] of rows y, y + 1: halves <= 1020, no carry across
-      S[j + 1] = A[j] + b + (mid << 1);
-      D[j + 1] = as_u32(as_i16x2(b) - as_i16x2(A[j]));  // [-1 0 1]
-      A[j] = b;
-    }
-    // neighbours across the lane edges: lane l - 1's last pixel, lane l + 1's first
-    S[0] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)S[16], 0x138, 0xf, 0xf, false);
-    D[0] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)D[16], 0x138, 0xf, 0xf, false);
-    S[17] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)S[1], 0x130, 0xf, 0xf, false);
-    D[17] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)D[1], 0x130, 0xf, 0xf, false);
-    uint32_t mg[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const i16x2 gx = as_i16x2(S[j + 2]) - as_i16x2(S[j]);
-      const i16x2 gy = as_i16x2(D[j]) + as_i16x2(D[j + 2]) + (as_i16x2(D[j + 1]) << (short)1);
-      const i16x2 mm = __builtin_elementwise_max(gx, -gx) + __builtin_elementwise_max(gy, -gy);
-      mg[j] = as_u32(__builtin_elementwise_min(mm, (i16x2)(short)255));
-    }
-    uint32_t o0[4], o1[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t p01 = __builtin_amdgcn_perm(mg[4 * q + 1], mg[4 * q], 0x06020400u);
-      const uint32_t p23 = __builtin_amdgcn_perm(mg[4 * q + 3], mg[4 * q + 2], 0x06020400u);
-      o0[q] = __builtin_amdgcn_perm(p23, p01, 0x05040100u);  // row y
-      o1[q] = __builtin_amdgcn_perm(p23, p01, 0x07060302u);  // row y + 1
-    }
+  auto store2 = [&](int y, const uint32_t (&o0)[4], const uint32_t (&o1)[4]) __attribute__((always_inline)) {
     store_out<false, SAUX>(o0, rout, y < ye, a.out_org + (uint32_t)((int64_t)y * a.out_pitch), lout, nullptr, lane);
     store_out<false, SAUX>(o1, rout, y + 1 < ye, a.out_org + (uint32_t)((int64_t)(y + 1) * a.out_pitch), lout,
                            nullptr, lane);
-    r0 = r2;
   };
-  for (int y = ys; y < ye; y += 4) {
-    step(y, nx[0]);
-    step(y + 2, nx[1]);
+  // A[j] = (r(y - 1), r(y)) of the current step y (the previous step's B)
+  uint32_t A[16];
+  if constexpr (PB > 0) {
+    u32x4 R[PB + 2];  // rows ys - 1 .. ys + PB
+#pragma unroll
+    for (int k = 0; k < PB + 2; ++k) R[k] = load(ys - 1 + k);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) A[j] = rows_pair(R[0], R[1], j);
+#pragma unroll
+    for (int st = 0; st < PB / 2; ++st) {
+      uint32_t o0[4], o1[4];
+      sobel_rp_step(R[2 * st + 1], R[2 * st + 2], R[2 * st + 3], A, o0, o1);
+      store2(ys + 2 * st, o0, o1);
+    }
+  } else {
+    u32x4 r0;  // row y
+    {
+      const u32x4 rm = load(ys - 1);
+      r0 = load(ys);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) A[j] = rows_pair(rm, r0, j);
+    }
+    // rows y + 1, y + 2 of this step and of the next one in flight
+    u32x4 nx[2][2];
+    nx[0][0] = load(ys + 1);
+    nx[0][1] = load(ys + 2);
+    nx[1][0] = load(ys + 3);
+    nx[1][1] = load(ys + 4);
+    auto step = [&](int y, u32x4 (&cur)[2]) __attribute__((always_inline)) {
+      const u32x4 r1 = cur[0], r2 = cur[1];
+      cur[0] = load(y + 5);  // the step after next
+      cur[1] = load(y + 6);
+      uint32_t o0[4], o1[4];
+      sobel_rp_step(r0, r1, r2, A, o0, o1);
+      store2(y, o0, o1);
+      r0 = r2;
+    };
+    for (int y = ys; y < ye; y += 4) {
+      step(y, nx[0]);
+      step(y + 2, nx[1]);
+    }
   }
   band_margins<1, 1>(a, t);
 }
@@ -1233,8 +1262,18 @@ void launch_one(bool skip, bool nt, int wgs, KArgs a, int tiles, int n0, int n1,
         const char* e = std::getenv("STRIPE_SOBEL_RP");
         return !(e && std::atoi(e) == 0);
       }();
+      // STRIPE_SOBEL_PB=8|12: bands of that height with every input row
+      // requested up front (A/B)
+      static const int pb = [] {
+        const char* e = std::getenv("STRIPE_SOBEL_PB");
+        const int v = e ? std::atoi(e) : 0;
+        return v == 8 || v == 12 ? v : 0;
+      }();
       if (rp && !skip) {
-        const K fn = nt ? k_sobel_rp<kNtAux> : k_sobel_rp<0>;
+        K fn = nt ? k_sobel_rp<kNtAux> : k_sobel_rp<0>;
+        if (pb == 8) fn = nt ? k_sobel_rp<kNtAux, 8> : k_sobel_rp<0, 8>;
+        if (pb == 12) fn = nt ? k_sobel_rp<kNtAux, 12> : k_sobel_rp<0, 12>;
+        if (pb) band = pb;
         plan_bands(a, grid, tiles, n0, n1, band, F::R, 0);
         fn<<<grid, kNT, nt_lds_reserve((const void*)fn, stencil_cap(nt, wgs, kNtWgsSep)), s>>>(a);
         return;

@@ -25,6 +25,7 @@
 #   warm     cache-resident gaussian5 configs, repeated                -> r5/warm
 #   benchprof the driver's bench command under a kernel trace         -> r5/bench
 #   exitprobe process exit under rocprofv3 with an RCCL communicator -> r5/bench
+#   sobelpb  gray sobel with every band row requested up front (A/B)  -> r5/cfg3
 #   idct     JPEG IDCT: row-per-lane vs per-block kernel        -> r5/jpeg
 #   e2e      e2e pipeline chunk count                           -> r5/e2e
 # Every GPU step runs under its own timeout; a failing step ends the script.
@@ -165,6 +166,16 @@ exitprobe)
   cd /tmp
   for mode in ${MODES:-release keep}; do
     timeout -k 10 120 rocprofv3 --kernel-trace -d $O/p_$mode -o run -- python3 $R/tools/exit_probe.py $mode > $O/$mode.log 2>&1 || exit 2
+  done
+  ;;
+sobelpb)
+  STRIPE_SOBEL_PB=8 gpu_tests "tests -k sobel" || exit 2
+  for r in 1 2; do
+    for pb in 0 8 12; do
+      B=-1; [ $pb != 0 ] && B=$pb
+      STRIPE_SOBEL_PB=$pb timeout -k 10 200 $KB --shape 8192x2048x1 --chains sobel --bands=$B --iters 200 >> $O/share_pb$pb.txt 2>&1 || exit 3
+      STRIPE_SOBEL_PB=$pb timeout -k 10 200 $KB --shape 8192x8192x1 --chains sobel --bands=$B --iters 200 >> $O/full_pb$pb.txt 2>&1 || exit 3
+    done
   done
   ;;
 idct)
