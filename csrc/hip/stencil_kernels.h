@@ -900,11 +900,15 @@ __device__ __forceinline__ void sobel_rp_step(const u32x4& r0, const u32x4& r1, 
   D[0] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)D[16], 0x138, 0xf, 0xf, false);
   S[17] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)S[1], 0x130, 0xf, 0xf, false);
   D[17] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)D[1], 0x130, 0xf, 0xf, false);
+  // horizontal [1 2 1] of D as two pair sums shared by neighbouring pixels
+  i16x2 T[17];
+#pragma unroll
+  for (int j = 0; j < 17; ++j) T[j] = as_i16x2(D[j]) + as_i16x2(D[j + 1]);
   uint32_t mg[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
     const i16x2 gx = as_i16x2(S[j + 2]) - as_i16x2(S[j]);
-    const i16x2 gy = as_i16x2(D[j]) + as_i16x2(D[j + 2]) + (as_i16x2(D[j + 1]) << (short)1);
+    const i16x2 gy = T[j] + T[j + 1];
     const i16x2 mm = __builtin_elementwise_max(gx, -gx) + __builtin_elementwise_max(gy, -gy);
     mg[j] = as_u32(__builtin_elementwise_min(mm, (i16x2)(short)255));
   }
@@ -1262,14 +1266,17 @@ void launch_one(bool skip, bool nt, int wgs, KArgs a, int tiles, int n0, int n1,
         const char* e = std::getenv("STRIPE_SOBEL_RP");
         return !(e && std::atoi(e) == 0);
       }();
-      // STRIPE_SOBEL_PB=8|12: bands of that height with every input row
-      // requested up front (A/B)
-      static const int pb = [] {
+      // 8-row bands request all ten input rows up front (the autotuner's
+      // band-8 candidate; full 8192^2 frame 2-3.5 % faster than the best
+      // streamed band, profiles/r5/cfg3/README.md); STRIPE_SOBEL_PB=8|12
+      // forces bands of that height with up-front loads (A/B)
+      static const int pb_env = [] {
         const char* e = std::getenv("STRIPE_SOBEL_PB");
-        const int v = e ? std::atoi(e) : 0;
-        return v == 8 || v == 12 ? v : 0;
+        const int v = e ? std::atoi(e) : -1;
+        return v == 0 || v == 8 || v == 12 ? v : -1;
       }();
       if (rp && !skip) {
+        const int pb = pb_env >= 0 ? pb_env : (band == 8 ? 8 : 0);
         K fn = nt ? k_sobel_rp<kNtAux> : k_sobel_rp<0>;
         if (pb == 8) fn = nt ? k_sobel_rp<kNtAux, 8> : k_sobel_rp<0, 8>;
         if (pb == 12) fn = nt ? k_sobel_rp<kNtAux, 12> : k_sobel_rp<0, 12>;

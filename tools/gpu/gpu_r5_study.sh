@@ -170,8 +170,9 @@ exitprobe)
   ;;
 sobelpb)
   STRIPE_SOBEL_PB=8 gpu_tests "tests -k sobel" || exit 2
+  gpu_tests "tests -k sobel" || exit 2
   for r in 1 2; do
-    for pb in 0 8 12; do
+    for pb in ${PBS:-0 8 12}; do
       B=-1; [ $pb != 0 ] && B=$pb
       STRIPE_SOBEL_PB=$pb timeout -k 10 200 $KB --shape 8192x2048x1 --chains sobel --bands=$B --iters 200 >> $O/share_pb$pb.txt 2>&1 || exit 3
       STRIPE_SOBEL_PB=$pb timeout -k 10 200 $KB --shape 8192x8192x1 --chains sobel --bands=$B --iters 200 >> $O/full_pb$pb.txt 2>&1 || exit 3
