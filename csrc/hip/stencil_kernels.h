@@ -353,12 +353,12 @@ __device__ __forceinline__ void apply_skip(const KArgs& a, int gy, int R, const 
 // C: stencil channels (the wave tiling covers W * C bytes); CO: output bytes
 // per pixel (3 for a fused expand of a 1-channel stencil, else C).
 template <int C, int CO = C>
-__device__ __forceinline__ void band_margins(const KArgs& a, const WaveTask& t) {
+__device__ __forceinline__ void band_margins(const KArgs& a, const WaveTask& t, int tile_bytes = kOutChunks * 16) {
   const int px = a.out_px;
   if (px == 0) return;
   const int E = a.W * C;
   const bool left = t.xt == 0;
-  const bool right = (t.xt + 1) * kOutChunks * 16 >= E;
+  const bool right = (t.xt + 1) * tile_bytes >= E;
   if (!left && !right) return;
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this band's stores are done
   const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
@@ -883,8 +883,12 @@ __device__ __forceinline__ uint32_t rows_pair(const u32x4& ra, const u32x4& rb, 
 // Two output rows (y, y + 1) from rows y - 1 .. y + 2: r0 = row y, r1 = y + 1,
 // r2 = y + 2; A[j] holds (r(y - 1), r(y)) on entry and (r(y + 1), r(y + 2))
 // on return; o0 / o1 are the lane's 16 output bytes of rows y / y + 1.
+// se / de: the vertical sum / difference pair of the pixel beyond the wave's
+// edge (lane 0: the left neighbour, lane 63: the right one; 0 when the wave's
+// outer lanes are halo lanes).
 __device__ __forceinline__ void sobel_rp_step(const u32x4& r0, const u32x4& r1, const u32x4& r2, uint32_t (&A)[16],
-                                              uint32_t (&o0)[4], uint32_t (&o1)[4]) {
+                                              uint32_t (&o0)[4], uint32_t (&o1)[4], uint32_t se = 0,
+                                              uint32_t de = 0) {
   uint32_t S[18], D[18];
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
@@ -895,11 +899,12 @@ __device__ __forceinline__ void sobel_rp_step(const u32x4& r0, const u32x4& r1, 
     D[j + 1] = as_u32(as_i16x2(b) - as_i16x2(A[j]));  // [-1 0 1]
     A[j] = b;
   }
-  // neighbours across the lane edges: lane l - 1's last pixel, lane l + 1's first
-  S[0] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)S[16], 0x138, 0xf, 0xf, false);
-  D[0] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)D[16], 0x138, 0xf, 0xf, false);
-  S[17] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)S[1], 0x130, 0xf, 0xf, false);
-  D[17] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)D[1], 0x130, 0xf, 0xf, false);
+  // neighbours across the lane edges: lane l - 1's last pixel, lane l + 1's
+  // first (wave shifts; lanes 0 / 63 keep se / de)
+  S[0] = (uint32_t)__builtin_amdgcn_update_dpp((int)se, (int)S[16], 0x138, 0xf, 0xf, false);
+  D[0] = (uint32_t)__builtin_amdgcn_update_dpp((int)de, (int)D[16], 0x138, 0xf, 0xf, false);
+  S[17] = (uint32_t)__builtin_amdgcn_update_dpp((int)se, (int)S[1], 0x130, 0xf, 0xf, false);
+  D[17] = (uint32_t)__builtin_amdgcn_update_dpp((int)de, (int)D[1], 0x130, 0xf, 0xf, false);
   // horizontal [1 2 1] of D as two pair sums shared by neighbouring pixels
   i16x2 T[17];
 #pragma unroll
@@ -925,20 +930,55 @@ __device__ __forceinline__ void sobel_rp_step(const u32x4& r0, const u32x4& r1, 
 // is PB rows and all PB + 2 input rows are requested up front, so a wave
 // waits for one memory round trip, not one per step (a short-lived wave's
 // life is mostly those waits: profiles/r5/cfg3/README.md).
-template <int SAUX, int PB = 0>
+// WIDE: 1 KiB tiles, every lane an output lane; the two pixels beyond the
+// tile come from one extra dword load per row (lanes 0-31 the left
+// neighbour's dword, 32-63 the right one's) and enter the wave shifts as their
+// `old` value.  8192-wide gray rows are then 8 tiles instead of 9 (the ninth
+// 26 % used): 4096 waves at 4-row bands, 4 per SIMD instead of 4-5.
+template <int SAUX, int PB = 0, bool WIDE = false>
 __global__ __launch_bounds__(kNT, 4) void k_sobel_rp(KArgs a) {
   const WaveTask t = wave_task(a);
   if (!t.valid) return;
   const int lane = t.lane;
   const int ys = t.ys, ye = t.ye;
-  const int cb = t.xt * (kOutChunks * 16) - 16 + lane * 16;
+  constexpr int kTile = WIDE ? kW * 16 : kOutChunks * 16;  // output bytes per wave row
+  const int cb0 = t.xt * kTile - (WIDE ? 0 : 16);
+  const int cb = cb0 + lane * 16;
   const uint32_t lane_in = cb < a.E + 16 ? (uint32_t)cb : kOOB;
-  const OutLanes lout = out_lanes<false>(a, lane, cb - 16 * lane);
+  OutLanes lout;
+  if constexpr (WIDE) {
+    lout.off[0] = cb < a.E ? (uint32_t)cb : kOOB;
+    lout.off[1] = lout.off[2] = kOOB;
+  } else {
+    lout = out_lanes<false>(a, lane, cb0);
+  }
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);
   const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
   // rows past the band's lower halo row (ye) re-read it: they feed unstored outputs
   auto load = [&](int y) __attribute__((always_inline)) {
     return __builtin_amdgcn_raw_buffer_load_b128(rin, in_row_off(a, min(y, ye)) + lane_in, 0, kLoadAux);
+  };
+  // the edge pixels' dwords (WIDE): byte 3 of the dword before the tile for
+  // lanes < 32, byte 0 of the one after it for lanes >= 32 (x-margins hold the
+  // border pixels; past the row's right margin nothing is needed)
+  const int eo = lane < 32 ? cb0 - 4 : cb0 + kTile;
+  const uint32_t e_in = eo < a.E + 16 ? (uint32_t)eo : kOOB;
+  const uint32_t ek = lane < 32 ? 3u : 0u;
+  const uint32_t esel = ek | 0x0C00u | ((4u + ek) << 16) | 0x0C000000u;  // (byte of row a, byte of row b) as u16s
+  auto load_e = [&](int y) __attribute__((always_inline)) {
+    return WIDE ? __builtin_amdgcn_raw_buffer_load_b32(rin, in_row_off(a, min(y, ye)) + e_in, 0, kLoadAux) : 0u;
+  };
+  uint32_t Ae = 0;  // edge pair (r(y - 1), r(y))
+  auto edge = [&](uint32_t e0, uint32_t e1, uint32_t e2, uint32_t& se, uint32_t& de) __attribute__((always_inline)) {
+    if constexpr (WIDE) {
+      const uint32_t me = __builtin_amdgcn_perm(e1, e0, esel);
+      const uint32_t be = __builtin_amdgcn_perm(e2, e1, esel);
+      se = Ae + be + (me << 1);
+      de = as_u32(as_i16x2(be) - as_i16x2(Ae));
+      Ae = be;
+    } else {
+      se = de = 0;
+    }
   };
   auto store2 = [&](int y, const uint32_t (&o0)[4], const uint32_t (&o1)[4]) __attribute__((always_inline)) {
     store_out<false, SAUX>(o0, rout, y < ye, a.out_org + (uint32_t)((int64_t)y * a.out_pitch), lout, nullptr, lane);
@@ -948,46 +988,66 @@ __global__ __launch_bounds__(kNT, 4) void k_sobel_rp(KArgs a) {
   // A[j] = (r(y - 1), r(y)) of the current step y (the previous step's B)
   uint32_t A[16];
   if constexpr (PB > 0) {
-    u32x4 R[PB + 2];  // rows ys - 1 .. ys + PB
+    u32x4 R[PB + 2];     // rows ys - 1 .. ys + PB
+    uint32_t Ee[PB + 2];  // their edge dwords
 #pragma unroll
-    for (int k = 0; k < PB + 2; ++k) R[k] = load(ys - 1 + k);
+    for (int k = 0; k < PB + 2; ++k) {
+      R[k] = load(ys - 1 + k);
+      Ee[k] = load_e(ys - 1 + k);
+    }
 #pragma unroll
     for (int j = 0; j < 16; ++j) A[j] = rows_pair(R[0], R[1], j);
+    if constexpr (WIDE) Ae = __builtin_amdgcn_perm(Ee[1], Ee[0], esel);
 #pragma unroll
     for (int st = 0; st < PB / 2; ++st) {
-      uint32_t o0[4], o1[4];
-      sobel_rp_step(R[2 * st + 1], R[2 * st + 2], R[2 * st + 3], A, o0, o1);
+      uint32_t o0[4], o1[4], se, de;
+      edge(Ee[2 * st + 1], Ee[2 * st + 2], Ee[2 * st + 3], se, de);
+      sobel_rp_step(R[2 * st + 1], R[2 * st + 2], R[2 * st + 3], A, o0, o1, se, de);
       store2(ys + 2 * st, o0, o1);
     }
   } else {
     u32x4 r0;  // row y
+    uint32_t e0;
     {
       const u32x4 rm = load(ys - 1);
       r0 = load(ys);
+      const uint32_t em = load_e(ys - 1);
+      e0 = load_e(ys);
 #pragma unroll
       for (int j = 0; j < 16; ++j) A[j] = rows_pair(rm, r0, j);
+      if constexpr (WIDE) Ae = __builtin_amdgcn_perm(e0, em, esel);
     }
     // rows y + 1, y + 2 of this step and of the next one in flight
     u32x4 nx[2][2];
+    uint32_t ne[2][2];
     nx[0][0] = load(ys + 1);
     nx[0][1] = load(ys + 2);
     nx[1][0] = load(ys + 3);
     nx[1][1] = load(ys + 4);
-    auto step = [&](int y, u32x4 (&cur)[2]) __attribute__((always_inline)) {
+    ne[0][0] = load_e(ys + 1);
+    ne[0][1] = load_e(ys + 2);
+    ne[1][0] = load_e(ys + 3);
+    ne[1][1] = load_e(ys + 4);
+    auto step = [&](int y, u32x4 (&cur)[2], uint32_t (&ce)[2]) __attribute__((always_inline)) {
       const u32x4 r1 = cur[0], r2 = cur[1];
+      const uint32_t e1 = ce[0], e2 = ce[1];
       cur[0] = load(y + 5);  // the step after next
       cur[1] = load(y + 6);
-      uint32_t o0[4], o1[4];
-      sobel_rp_step(r0, r1, r2, A, o0, o1);
+      ce[0] = load_e(y + 5);
+      ce[1] = load_e(y + 6);
+      uint32_t o0[4], o1[4], se, de;
+      edge(e0, e1, e2, se, de);
+      sobel_rp_step(r0, r1, r2, A, o0, o1, se, de);
       store2(y, o0, o1);
       r0 = r2;
+      e0 = e2;
     };
     for (int y = ys; y < ye; y += 4) {
-      step(y, nx[0]);
-      step(y + 2, nx[1]);
+      step(y, nx[0], ne[0]);
+      step(y + 2, nx[1], ne[1]);
     }
   }
-  band_margins<1, 1>(a, t);
+  band_margins<1, 1>(a, t, kTile);
 }
 
 // ------------------------------------------------------------------------------
@@ -1275,12 +1335,22 @@ void launch_one(bool skip, bool nt, int wgs, KArgs a, int tiles, int n0, int n1,
         const int v = e ? std::atoi(e) : -1;
         return v == 0 || v == 8 || v == 12 ? v : -1;
       }();
+      // 1 KiB tiles with edge loads (STRIPE_SOBEL_WIDE=0: 62-lane tiles, A/B)
+      static const bool wide = [] {
+        const char* e = std::getenv("STRIPE_SOBEL_WIDE");
+        return !(e && std::atoi(e) == 0);
+      }();
       if (rp && !skip) {
         const int pb = pb_env >= 0 ? pb_env : (band == 8 ? 8 : 0);
-        K fn = nt ? k_sobel_rp<kNtAux> : k_sobel_rp<0>;
-        if (pb == 8) fn = nt ? k_sobel_rp<kNtAux, 8> : k_sobel_rp<0, 8>;
-        if (pb == 12) fn = nt ? k_sobel_rp<kNtAux, 12> : k_sobel_rp<0, 12>;
+        const K fns[2][3][2] = {{{k_sobel_rp<0>, k_sobel_rp<kNtAux>},
+                                 {k_sobel_rp<0, 8>, k_sobel_rp<kNtAux, 8>},
+                                 {k_sobel_rp<0, 12>, k_sobel_rp<kNtAux, 12>}},
+                                {{k_sobel_rp<0, 0, true>, k_sobel_rp<kNtAux, 0, true>},
+                                 {k_sobel_rp<0, 8, true>, k_sobel_rp<kNtAux, 8, true>},
+                                 {k_sobel_rp<0, 12, true>, k_sobel_rp<kNtAux, 12, true>}}};
+        const K fn = fns[wide][pb == 8 ? 1 : pb == 12 ? 2 : 0][nt];
         if (pb) band = pb;
+        if (wide) tiles = (int)div_up((int64_t)a.E, kW * 16);
         plan_bands(a, grid, tiles, n0, n1, band, F::R, 0);
         fn<<<grid, kNT, nt_lds_reserve((const void*)fn, stencil_cap(nt, wgs, kNtWgsSep)), s>>>(a);
         return;

@@ -24,7 +24,8 @@ def _run(m, img, chain, border="reflect101"):
     return y.cpu().numpy()
 
 
-SHAPES = [(1, 1), (3, 2), (17, 15), (64, 65), (37, 1365), (130, 4100), (9, 5000)]
+# (5, 2048): gray rows of exactly two 1 KiB sobel tiles (the right edge pixel is the margin)
+SHAPES = [(1, 1), (3, 2), (17, 15), (64, 65), (37, 1365), (130, 4100), (9, 5000), (5, 2048)]
 STENCILS = ["gaussian3", "gaussian5", "gaussian7", "box3", "box5", "emboss3", "emboss5", "sharpen", "laplace",
             "sobel", "sobel_l2"]
 

@@ -26,6 +26,7 @@
 #   benchprof the driver's bench command under a kernel trace         -> r5/bench
 #   exitprobe process exit under rocprofv3 with an RCCL communicator -> r5/bench
 #   sobelpb  gray sobel with every band row requested up front (A/B)  -> r5/cfg3
+#   sobelwide gray sobel on 1 KiB tiles with edge loads vs 62-lane tiles -> r5/cfg3
 #   idct     JPEG IDCT: row-per-lane vs per-block kernel        -> r5/jpeg
 #   e2e      e2e pipeline chunk count                           -> r5/e2e
 # Every GPU step runs under its own timeout; a failing step ends the script.
@@ -37,6 +38,7 @@ mkdir -p $O
 export TMPDIR=/tmp
 C31="$(python3 -c "print('conv:31:' + ';'.join(str(((i*7)%13-4)/400.0) for i in range(961)))")"
 KB="python tools/kbench.py"
+CLI=bin/stripe
 gpu_tests() {  # $1: pytest selection
   timeout -k 10 600 python -u -m pytest $1 -m gpu -q --timeout 200 --timeout-method thread > $O/tests_$S.txt 2>&1
 }
@@ -176,6 +178,17 @@ sobelpb)
       B=-1; [ $pb != 0 ] && B=$pb
       STRIPE_SOBEL_PB=$pb timeout -k 10 200 $KB --shape 8192x2048x1 --chains sobel --bands=$B --iters 200 >> $O/share_pb$pb.txt 2>&1 || exit 3
       STRIPE_SOBEL_PB=$pb timeout -k 10 200 $KB --shape 8192x8192x1 --chains sobel --bands=$B --iters 200 >> $O/full_pb$pb.txt 2>&1 || exit 3
+    done
+  done
+  ;;
+sobelwide)
+  gpu_tests "tests -k sobel" || exit 2
+  STRIPE_SOBEL_PB=8 gpu_tests "tests -k sobel" || exit 2
+  for r in 1 2; do
+    for w in 1 0; do
+      STRIPE_SOBEL_WIDE=$w timeout -k 10 200 $KB --shape 8192x2048x1 --chains sobel --bands=-1 --iters 200 >> $O/share_w$w.txt 2>&1 || exit 3
+      STRIPE_SOBEL_WIDE=$w timeout -k 10 200 $KB --shape 8192x8192x1 --chains sobel --bands=-1 --iters 200 >> $O/full_w$w.txt 2>&1 || exit 3
+      STRIPE_SOBEL_WIDE=$w timeout -k 10 200 $CLI bench --synthetic 8192x8192x1 --chain sobel --ranks 4 --iters 50 --warmup 10 --scope resident --backend local >> $O/local4_w$w.txt 2>&1 || exit 3
     done
   done
   ;;
