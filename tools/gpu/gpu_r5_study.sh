@@ -27,6 +27,7 @@
 #   exitprobe process exit under rocprofv3 with an RCCL communicator -> r5/bench
 #   sobelpb  gray sobel with every band row requested up front (A/B)  -> r5/cfg3
 #   sobelwide gray sobel on 1 KiB tiles with edge loads vs 62-lane tiles -> r5/cfg3
+#   hband    headline bench at fixed band heights (probe picks streams) -> r5/bench
 #   idct     JPEG IDCT: row-per-lane vs per-block kernel        -> r5/jpeg
 #   e2e      e2e pipeline chunk count                           -> r5/e2e
 # Every GPU step runs under its own timeout; a failing step ends the script.
@@ -189,6 +190,14 @@ sobelwide)
       STRIPE_SOBEL_WIDE=$w timeout -k 10 200 $KB --shape 8192x2048x1 --chains sobel --bands=-1 --iters 200 >> $O/share_w$w.txt 2>&1 || exit 3
       STRIPE_SOBEL_WIDE=$w timeout -k 10 200 $KB --shape 8192x8192x1 --chains sobel --bands=-1 --iters 200 >> $O/full_w$w.txt 2>&1 || exit 3
       STRIPE_SOBEL_WIDE=$w timeout -k 10 200 $CLI bench --synthetic 8192x8192x1 --chain sobel --ranks 4 --iters 50 --warmup 10 --scope resident --backend local >> $O/local4_w$w.txt 2>&1 || exit 3
+    done
+  done
+  ;;
+hband)
+  for r in 1 2; do
+    for b in 0 8 12 16 24; do
+      A=""; [ $b != 0 ] && A="--band $b"
+      timeout -k 10 300 python bench.py --steps 100 --warmup 10 --dist-steps 0 --ref-steps 0 --e2e-steps 0 --deep-steps 0 $A > $O/hband_${b}_$r.json 2> $O/hband_${b}_$r.err || exit 2
     done
   done
   ;;
