@@ -205,12 +205,15 @@ hipStream_t Engine::dedicated_stream(int device, int index) {
   int prev = 0;
   HIP_CHECK(hipGetDevice(&prev));
   HIP_CHECK(hipSetDevice(device));
+  struct Restore {
+    int dev;
+    ~Restore() { (void)hipSetDevice(dev); }  // also when a call below throws
+  } restore{prev};
   int cus = 0;
   HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
   std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0xFFFFFFFFu);
   hipStream_t s = nullptr;
   HIP_CHECK(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
-  HIP_CHECK(hipSetDevice(prev));
   pool[{device, index}] = s;
   static const bool registered = [] {
     std::atexit([] {
