@@ -28,6 +28,7 @@
 #   sobelpb  gray sobel with every band row requested up front (A/B)  -> r5/cfg3
 #   sobelwide gray sobel on 1 KiB tiles with edge loads vs 62-lane tiles -> r5/cfg3
 #   hband    headline bench at fixed band heights (probe picks streams) -> r5/bench
+#   placement frame-stream 1 vs 2 streams over several buffer layouts -> r5/streams
 #   idct     JPEG IDCT: row-per-lane vs per-block kernel        -> r5/jpeg
 #   e2e      e2e pipeline chunk count                           -> r5/e2e
 # Every GPU step runs under its own timeout; a failing step ends the script.
@@ -199,6 +200,11 @@ hband)
       A=""; [ $b != 0 ] && A="--band $b"
       timeout -k 10 300 python bench.py --steps 100 --warmup 10 --dist-steps 0 --ref-steps 0 --e2e-steps 0 --deep-steps 0 $A > $O/hband_${b}_$r.json 2> $O/hband_${b}_$r.err || exit 2
     done
+  done
+  ;;
+placement)
+  for r in 1 2; do
+    timeout -k 10 300 python tools/placement_probe.py > $O/placement_$r.jsonl 2> $O/placement_$r.err || exit 2
   done
   ;;
 idct)
