@@ -18,6 +18,7 @@ case "$OUT" in /*) ;; *) OUT="$ROOT/$OUT" ;; esac
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 KB=(python3 "$ROOT/tools/kbench.py" --chains "$CHAIN" --shape "$SHAPE")
+[ -n "$BANDS" ] && KB+=(--bands "$BANDS")  # e.g. BANDS=8: a fixed band height (the tuner's pick)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run -- "${KB[@]}" --iters 20 > "$OUT/trace.log" 2>&1 || { tail -20 "$OUT/trace.log"; exit 1; }
 i=0
 for set in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \

@@ -29,6 +29,7 @@
 #   sobelwide gray sobel on 1 KiB tiles with edge loads vs 62-lane tiles -> r5/cfg3
 #   hband    headline bench at fixed band heights (probe picks streams) -> r5/bench
 #   placement frame-stream 1 vs 2 streams over several buffer layouts -> r5/streams
+#   sobelprof counters of the sobel share: 1 KiB vs 62-lane tiles      -> r5/cfg3
 #   idct     JPEG IDCT: row-per-lane vs per-block kernel        -> r5/jpeg
 #   e2e      e2e pipeline chunk count                           -> r5/e2e
 # Every GPU step runs under its own timeout; a failing step ends the script.
@@ -206,6 +207,10 @@ placement)
   for r in 1 2; do
     timeout -k 10 300 python tools/placement_probe.py > $O/placement_$r.jsonl 2> $O/placement_$r.err || exit 2
   done
+  ;;
+sobelprof)
+  BANDS=8 STRIPE_SOBEL_WIDE=1 timeout -k 10 900 bash scripts/profile.sh "sobel|" 8192x2048x1 $O/wide > $O/wide.txt 2>&1 || exit 2
+  BANDS=4 STRIPE_SOBEL_WIDE=0 timeout -k 10 900 bash scripts/profile.sh "sobel|" 8192x2048x1 $O/narrow > $O/narrow.txt 2>&1 || exit 2
   ;;
 idct)
   gpu_tests tests/test_jpeg.py || exit 2
