@@ -328,17 +328,33 @@ class FrameStream:
             # cross-stream event schedules slower on some boxes
             # (profiles/r5/streams/).  pick_schedule measures both;
             # STRIPE_FRAME_QUEUES=pool|dedicated pins one.
-            self._sets["dedicated"] = [torch.cuda.ExternalStream(C.dedicated_stream(ctx.gpu, k), device=ctx.gpu)
-                                       for k in range(nmax)]
-            self._sets["pool"] = [torch.cuda.Stream() for _ in range(nmax)]
+            # Processes that share one GPU (gloo-gpu with more local ranks than
+            # GPUs) get no dedicated queues: each one's extra HSA queues
+            # oversubscribe the GPU's hardware queue slots, and the time-sliced
+            # queues made a 4-process 16384^2 step 3x slower
+            # (profiles/r5/shared/)
             pin = os.environ.get("STRIPE_FRAME_QUEUES", "")
-            self.queue_options = [pin] if pin in self._sets else (["dedicated", "pool"] if nmax > 1 else ["dedicated"])
+            if pin == "dedicated" or not self.shares_gpu(ctx):
+                self._sets["dedicated"] = [torch.cuda.ExternalStream(C.dedicated_stream(ctx.gpu, k), device=ctx.gpu)
+                                           for k in range(nmax)]
+            self._sets["pool"] = [torch.cuda.Stream() for _ in range(nmax)]
+            kinds = [k for k in ("dedicated", "pool") if k in self._sets]
+            self.queue_options = [pin] if pin in self._sets else (kinds if nmax > 1 else kinds[:1])
             self.queues = self.queue_options[0]
             self.streams = self._sets[self.queues]
             for f in self.frames:
                 f.engine.stage_timing = stage_timing
         self.set_streams(nmax)
         self._i = 0
+
+    @staticmethod
+    def shares_gpu(ctx: DistContext) -> bool:
+        """More processes of this node than GPUs (gloo-gpu places rank r on
+        GPU r mod count; RCCL runs one rank per GPU)."""
+        if ctx.transport != "gloo-gpu":
+            return False
+        local = int(os.environ.get("LOCAL_WORLD_SIZE", str(ctx.world)))
+        return local > max(1, torch.cuda.device_count())
 
     @classmethod
     def plan(cls, ws_max: int, iterable: bool, device: bool, frames: int = 0):

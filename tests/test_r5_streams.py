@@ -83,3 +83,18 @@ def test_dedicated_streams_are_reused_gpu():
     assert int(y[-1]) == 3 * ((1 << 20) - 1)
     with pytest.raises(Exception):
         C.dedicated_stream(0, 8)
+
+
+def test_shared_gpu_processes_get_no_dedicated_queues(monkeypatch):
+    # gloo-gpu with more local ranks than GPUs: the ranks share a GPU, and each
+    # one's extra HSA queues would oversubscribe its hardware queue slots
+    from types import SimpleNamespace
+
+    ctx = SimpleNamespace(transport="gloo-gpu", world=4)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")
+    assert parallel.FrameStream.shares_gpu(ctx)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
+    assert not parallel.FrameStream.shares_gpu(ctx)
+    # RCCL runs one rank per GPU
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    assert not parallel.FrameStream.shares_gpu(SimpleNamespace(transport="rccl", world=8))

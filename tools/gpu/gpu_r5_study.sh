@@ -30,6 +30,7 @@
 #   hband    headline bench at fixed band heights (probe picks streams) -> r5/bench
 #   placement frame-stream 1 vs 2 streams over several buffer layouts -> r5/streams
 #   sobelprof counters of the sobel share: 1 KiB vs 62-lane tiles      -> r5/cfg3
+#   shared   bench.py at N=4 / 8 as processes sharing the GPU (gloo-gpu) -> r5/shared
 #   idct     JPEG IDCT: row-per-lane vs per-block kernel        -> r5/jpeg
 #   e2e      e2e pipeline chunk count                           -> r5/e2e
 # Every GPU step runs under its own timeout; a failing step ends the script.
@@ -211,6 +212,11 @@ placement)
 sobelprof)
   BANDS=8 STRIPE_SOBEL_WIDE=1 timeout -k 10 900 bash scripts/profile.sh "sobel|" 8192x2048x1 $O/wide > $O/wide.txt 2>&1 || exit 2
   BANDS=4 STRIPE_SOBEL_WIDE=0 timeout -k 10 900 bash scripts/profile.sh "sobel|" 8192x2048x1 $O/narrow > $O/narrow.txt 2>&1 || exit 2
+  ;;
+shared)
+  for n in 4 8; do
+    timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29500 + n)) bench.py --gpus $n --backend gloo-gpu --steps 20 --warmup 5 > $O/bench_16k_n$n.json 2> $O/bench_16k_n$n.err || exit 2
+  done
   ;;
 idct)
   gpu_tests tests/test_jpeg.py || exit 2
