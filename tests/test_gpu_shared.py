@@ -50,13 +50,21 @@ def test_bench_gloo_gpu_processes(tmp_path, n):
     # the three halo schedules differ on device engines: each was timed on the
     # real transport and the verified headline ran the fastest
     # (frames rotate here, so one stream and two alternating ones are both
-    # tried, the two from either stream set: dedicated hardware queues or
-    # torch's pool)
+    # tried; processes sharing one GPU take torch's pool streams only --
+    # dedicated hardware queues in every process oversubscribe the GPU's queue
+    # slots, profiles/r5/shared/ -- otherwise both stream sets are tried)
+    import torch
+
     hs = rec["halo_schedule"]
     scheds = ("serial", "overlap", "pipeline")
-    assert set(hs["ms"]) == ({f"{s}@1" for s in scheds} |
-                             {f"{s}@2/{q}" for s in scheds for q in ("dedicated", "pool")})
-    key = f"{hs['chosen']}@{hs['streams']}" + (f"/{hs['queues']}" if hs["streams"] > 1 else "")
+    if n > torch.cuda.device_count():
+        assert hs["queues"] == "pool"
+        assert set(hs["ms"]) == {f"{s}@{k}" for s in scheds for k in (1, 2)}
+    else:
+        assert set(hs["ms"]) == ({f"{s}@1" for s in scheds} |
+                                 {f"{s}@2/{q}" for s in scheds for q in ("dedicated", "pool")})
+    multi = any("/" in k for k in hs["ms"])
+    key = f"{hs['chosen']}@{hs['streams']}" + (f"/{hs['queues']}" if hs["streams"] > 1 and multi else "")
     assert key == min(hs["ms"], key=hs["ms"].get) and rec["streams"] == hs["streams"]
     for name, sc in rec["scopes"].items():
         assert "error" not in sc, (name, sc)
