@@ -278,6 +278,20 @@ class DistributedPipeline:
 MALL_BYTES = 256 << 20  # MI355X Infinity Cache
 
 
+class _PlainStreams:
+    """Plain (non-blocking) HIP streams owned by a frame stream's frames."""
+
+    def __init__(self, gpu: int, n: int):
+        self.handles = [C.stream_create(gpu, False) for _ in range(n)]
+
+    def __del__(self):
+        for h in self.handles:
+            try:
+                C.stream_destroy(h)
+            except Exception:  # noqa: BLE001 - teardown of a failed device: nothing left to free
+                pass
+
+
 class FrameStream:
     """A stream of independent frames through one distributed pipeline: the
     video-rate workload (each frame filtered, halo exchanged every step).
@@ -320,14 +334,14 @@ class FrameStream:
         self.queues = "none"
         self._sets = {}
         if ctx.device:
-            # two stream sets: torch's pool streams, which share GPU_MAX_HW_QUEUES
-            # hardware queues round-robin (once another library has created
-            # streams, two of them can land on one queue: cold N=8 share 41.4
-            # us a step), and streams with hardware queues of their own
+            # two stream sets: plain streams, which share GPU_MAX_HW_QUEUES
+            # hardware queues round-robin (two of torch's pool streams landed
+            # on one queue after the RCCL check: cold N=8 share 41.4 us a
+            # step), and streams with hardware queues of their own
             # (process-wide, C.dedicated_stream: 35.6 us), which in turn made
             # cross-stream event schedules slower on some boxes
             # (profiles/r5/streams/).  pick_schedule measures both;
-            # STRIPE_FRAME_QUEUES=pool|dedicated pins one.
+            # STRIPE_FRAME_QUEUES=plain|dedicated pins one.
             # Processes that share one GPU (gloo-gpu with more local ranks than
             # GPUs) get no dedicated queues: each one's extra HSA queues
             # oversubscribe the GPU's hardware queue slots, and the time-sliced
@@ -337,8 +351,18 @@ class FrameStream:
             if pin == "dedicated" or not self.shares_gpu(ctx):
                 self._sets["dedicated"] = [torch.cuda.ExternalStream(C.dedicated_stream(ctx.gpu, k), device=ctx.gpu)
                                            for k in range(nmax)]
-            self._sets["pool"] = [torch.cuda.Stream() for _ in range(nmax)]
-            kinds = [k for k in ("dedicated", "pool") if k in self._sets]
+            # plain HIP streams created back to back here, so they take
+            # consecutive hardware queues of the round-robin: two of torch's
+            # pool streams could share one after other code took pool streams
+            # (4 processes on one GPU: 0.52 -> 0.39 ms a step,
+            # profiles/r5/shared/); freed with the last frame that uses them
+            holder = _PlainStreams(ctx.gpu, nmax)
+            self._sets["plain"] = [torch.cuda.ExternalStream(h, device=ctx.gpu) for h in holder.handles]
+            for f in self.frames:
+                f._plain_streams = holder
+            if pin == "pool":  # the set's earlier name
+                pin = "plain"
+            kinds = [k for k in ("dedicated", "plain") if k in self._sets]
             self.queue_options = [pin] if pin in self._sets else (kinds if nmax > 1 else kinds[:1])
             self.queues = self.queue_options[0]
             self.streams = self._sets[self.queues]
@@ -387,7 +411,7 @@ class FrameStream:
         return frames, streaming, cold, cache
 
     def set_queues(self, kind: str):
-        """Use the "dedicated" or the "pool" stream set (same stream count)."""
+        """Use the "dedicated" or the "plain" stream set (same stream count)."""
         if not getattr(self, "_sets", {}):
             return
         self.queues = kind
@@ -439,7 +463,7 @@ class FrameStream:
         three-stream pipeline, the plain serial one),
         with the frames on one stream or alternating over two, on the real
         transport, and keep the fastest; two streams come from either stream
-        set (dedicated hardware queues or torch's pool, set_queues); returns
+        set (dedicated hardware queues or plain streams, set_queues); returns
         {"chosen", "streams", "queues", "ms"} ("ms" keys: schedule, or
         schedule@streams[/queues] when several are tried).
         Which one wins depends on the link and RCCL's per-exchange cost, which

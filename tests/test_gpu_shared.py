@@ -50,7 +50,7 @@ def test_bench_gloo_gpu_processes(tmp_path, n):
     # the three halo schedules differ on device engines: each was timed on the
     # real transport and the verified headline ran the fastest
     # (frames rotate here, so one stream and two alternating ones are both
-    # tried; processes sharing one GPU take torch's pool streams only --
+    # tried; processes sharing one GPU take plain streams only --
     # dedicated hardware queues in every process oversubscribe the GPU's queue
     # slots, profiles/r5/shared/ -- otherwise both stream sets are tried)
     import torch
@@ -58,11 +58,11 @@ def test_bench_gloo_gpu_processes(tmp_path, n):
     hs = rec["halo_schedule"]
     scheds = ("serial", "overlap", "pipeline")
     if n > torch.cuda.device_count():
-        assert hs["queues"] == "pool"
+        assert hs["queues"] == "plain"
         assert set(hs["ms"]) == {f"{s}@{k}" for s in scheds for k in (1, 2)}
     else:
         assert set(hs["ms"]) == ({f"{s}@1" for s in scheds} |
-                                 {f"{s}@2/{q}" for s in scheds for q in ("dedicated", "pool")})
+                                 {f"{s}@2/{q}" for s in scheds for q in ("dedicated", "plain")})
     multi = any("/" in k for k in hs["ms"])
     key = f"{hs['chosen']}@{hs['streams']}" + (f"/{hs['queues']}" if hs["streams"] > 1 and multi else "")
     assert key == min(hs["ms"], key=hs["ms"].get) and rec["streams"] == hs["streams"]
@@ -127,7 +127,10 @@ for sched in ("serial", "overlap", "pipeline"):
         for f in range(2):
             if not (fs.frames[f].result_stripe() == refs[f]).all():
                 bad.append([sched, ns, f])
-print("RESULT", ctx.rank, json.dumps(bad), flush=True)
+# one file per rank: the ranks share torchrun's stdout, where their writes can
+# interleave character by character
+with open(f"result_{ctx.rank}.json", "w") as fh:
+    json.dump(bad, fh)
 '''
 
 
@@ -142,11 +145,7 @@ def test_frame_stream_every_schedule_exact_gloo_gpu(tmp_path):
     env = dict(os.environ, STRIPE_ROOT=ROOT, OMP_NUM_THREADS="2")
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
     assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
-    # the two ranks share torchrun's stdout: their lines can interleave
-    # mid-line ("RESULT 0 []RESULT\n 1 []"), so match the records, not lines
-    import re
-
-    res = re.findall(r"RESULT\s+(\d+)\s+(\[[^\]]*\])", r.stdout)
-    assert sorted(int(k) for k, _ in res) == [0, 1], r.stdout[-2000:]
-    for _, bad in res:
-        assert json.loads(bad) == [], bad
+    for rank in (0, 1):
+        f = tmp_path / f"result_{rank}.json"
+        assert f.exists(), (rank, r.stdout[-2000:])
+        assert json.loads(f.read_text()) == [], rank

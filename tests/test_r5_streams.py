@@ -1,4 +1,4 @@
-"""FrameStream stream sets: torch's pool streams (shared hardware queues) or
+"""FrameStream stream sets: plain streams (shared hardware queues) or
 streams with hardware queues of their own (C.dedicated_stream); the schedule
 probe measures both with two streams and keeps the fastest
 (profiles/r5/streams/README.md)."""
@@ -16,8 +16,8 @@ def _stand_in(cost):
     frames = [SimpleNamespace(engine=SimpleNamespace(halo_schedule="serial")) for _ in range(4)]
     fs = parallel.FrameStream.__new__(parallel.FrameStream)
     fs.frames = frames
-    fs._sets = {"dedicated": ["d0", "d1"], "pool": ["p0", "p1"]}
-    fs.queue_options = ["dedicated", "pool"]
+    fs._sets = {"dedicated": ["d0", "d1"], "plain": ["p0", "p1"]}
+    fs.queue_options = ["dedicated", "plain"]
     fs.queues = "dedicated"
     fs.streams = fs._sets["dedicated"]
     fs.stream_options = [1, 2]
@@ -38,15 +38,15 @@ def test_probe_picks_stream_set():
     # two streams on the pool set are fastest here: the probe must land there
     def cost(sched, n, q):
         base = {"pipeline": 0.004, "overlap": 0.003, "serial": 0.002}[sched]
-        return base / 2 if (n == 2 and q == "pool") else base
+        return base / 2 if (n == 2 and q == "plain") else base
 
     fs, frames = _stand_in(cost)
     got = fs.pick_schedule(steps=2, rounds=1)
-    assert got["chosen"] == "serial" and got["streams"] == 2 and got["queues"] == "pool"
+    assert got["chosen"] == "serial" and got["streams"] == 2 and got["queues"] == "plain"
     assert fs.streams == ["p0", "p1"] and fs.nstreams == 2
     # one stream is timed once (the queue kind makes no difference there)
     assert set(got["ms"]) == {f"{s}@1" for s in fs.SCHEDULES} | {f"{s}@2/{q}" for s in fs.SCHEDULES
-                                                                  for q in ("dedicated", "pool")}
+                                                                  for q in ("dedicated", "plain")}
 
 
 def test_probe_keeps_dedicated_when_faster():
@@ -61,7 +61,7 @@ def test_probe_keeps_dedicated_when_faster():
 
 def test_pinned_queue_kind(monkeypatch):
     # host engines have no stream sets: the pin is ignored, nothing breaks
-    monkeypatch.setenv("STRIPE_FRAME_QUEUES", "pool")
+    monkeypatch.setenv("STRIPE_FRAME_QUEUES", "plain")
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
         monkeypatch.delenv(k, raising=False)
     ctx = parallel.init("gloo")

@@ -214,7 +214,7 @@ sobelprof)
   BANDS=4 STRIPE_SOBEL_WIDE=0 timeout -k 10 900 bash scripts/profile.sh "sobel|" 8192x2048x1 $O/narrow > $O/narrow.txt 2>&1 || exit 2
   ;;
 shared)
-  for n in 4 8; do
+  for n in ${NS:-4 8}; do
     timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29500 + n)) bench.py --gpus $n --backend gloo-gpu --steps 20 --warmup 5 > $O/bench_16k_n$n.json 2> $O/bench_16k_n$n.err || exit 2
   done
   ;;
