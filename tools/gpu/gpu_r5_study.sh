@@ -31,6 +31,7 @@
 #   placement frame-stream 1 vs 2 streams over several buffer layouts -> r5/streams
 #   sobelprof counters of the sobel share: 1 KiB vs 62-lane tiles      -> r5/cfg3
 #   shared   bench.py at N=4 / 8 as processes sharing the GPU (gloo-gpu) -> r5/shared
+#   share    the N=8 share through bench.py (--height 2048), twice      -> r5/streams
 #   idct     JPEG IDCT: row-per-lane vs per-block kernel        -> r5/jpeg
 #   e2e      e2e pipeline chunk count                           -> r5/e2e
 # Every GPU step runs under its own timeout; a failing step ends the script.
@@ -216,6 +217,11 @@ sobelprof)
 shared)
   for n in ${NS:-4 8}; do
     timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29500 + n)) bench.py --gpus $n --backend gloo-gpu --steps 20 --warmup 5 > $O/bench_16k_n$n.json 2> $O/bench_16k_n$n.err || exit 2
+  done
+  ;;
+share)
+  for r in 1 2; do
+    timeout -k 10 300 python bench.py --steps 200 --warmup 20 --height 2048 > $O/bench_stripe_$r.json 2> $O/bench_stripe_$r.err || exit 2
   done
   ;;
 idct)
