@@ -32,6 +32,7 @@
 #   sobelprof counters of the sobel share: 1 KiB vs 62-lane tiles      -> r5/cfg3
 #   shared   bench.py at N=4 / 8 as processes sharing the GPU (gloo-gpu) -> r5/shared
 #   share    the N=8 share through bench.py (--height 2048), twice      -> r5/streams
+#   prio     headline with the first frame stream at high priority (A/B) -> r5/streams
 #   idct     JPEG IDCT: row-per-lane vs per-block kernel        -> r5/jpeg
 #   e2e      e2e pipeline chunk count                           -> r5/e2e
 # Every GPU step runs under its own timeout; a failing step ends the script.
@@ -222,6 +223,14 @@ shared)
 share)
   for r in 1 2; do
     timeout -k 10 300 python bench.py --steps 200 --warmup 20 --height 2048 > $O/bench_stripe_$r.json 2> $O/bench_stripe_$r.err || exit 2
+  done
+  ;;
+prio)
+  export STRIPE_FRAME_QUEUES=plain
+  for r in 1 2 3; do
+    for p in 1 0; do
+      STRIPE_FRAME_PRIO=$p timeout -k 10 300 python bench.py --steps 100 --warmup 10 --dist-steps 0 --ref-steps 0 --e2e-steps 0 --deep-steps 0 > $O/prio${p}_$r.json 2> $O/prio${p}_$r.err || exit 2
+    done
   done
   ;;
 idct)
