@@ -32,7 +32,7 @@
 #   sobelprof counters of the sobel share: 1 KiB vs 62-lane tiles      -> r5/cfg3
 #   shared   bench.py at N=4 / 8 as processes sharing the GPU (gloo-gpu) -> r5/shared
 #   share    the N=8 share through bench.py (--height 2048), twice      -> r5/streams
-#   prio     headline with the first frame stream at high priority (A/B) -> r5/streams
+#   prio     headline with the first frame stream at high priority (A/B; the STRIPE_FRAME_PRIO switch was removed after it) -> r5/streams
 #   idct     JPEG IDCT: row-per-lane vs per-block kernel        -> r5/jpeg
 #   e2e      e2e pipeline chunk count                           -> r5/e2e
 # Every GPU step runs under its own timeout; a failing step ends the script.
