@@ -108,6 +108,10 @@ def parse():
     ap.add_argument("--e2e-steps", type=int, default=3, help="steps of the e2e-scope measurement (0: skip)")
     ap.add_argument("--ref-shm", action="store_true",
                     help="ref-window host frame in POSIX shared memory even on one rank (tests the multi-rank path)")
+    ap.add_argument("--self-halo", action="store_true",
+                    help="N=1 only: the rank exchanges its boundary rows with itself through the one-rank RCCL "
+                         "communicator (loopback) every step, the transfers an interior rank of an N>1 run makes; "
+                         "the frame is then vertically periodic (verified against a periodic golden frame)")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-autotune", action="store_true", help="skip the per-shape band / occupancy autotune")
     ap.add_argument("--budget-s", type=float, default=420.0,
@@ -144,6 +148,31 @@ def build_info(root):
     except Exception as e:  # noqa: BLE001
         info["error"] = str(e)
     return info
+
+
+def comm_counters(ctx) -> dict:
+    """The communicator's host-side group counters (RCCL: groups, summed
+    microseconds per grouped call); {} for transports without them."""
+    if ctx.comm is None:
+        return {}
+    try:
+        return {k: float(v) for k, v in ctx.comm.identity().items() if k.startswith("group")}
+    except Exception:  # noqa: BLE001 - a transport without an identity
+        return {}
+
+
+def exchange_cost(before: dict, after: dict, steps: int) -> dict | None:
+    """Host microseconds per grouped exchange over a timed region (the
+    enqueue, ncclGroupEnd and the non-blocking progress poll), from two
+    comm_counters snapshots."""
+    n = after.get("groups", 0) - before.get("groups", 0)
+    if n <= 0:
+        return None
+    us = after["group_us"] - before["group_us"]
+    end = after.get("group_end_us", 0) - before.get("group_end_us", 0)
+    return {"exchanges": int(n), "per_step": round(n / max(1, steps), 3), "host_us_per_exchange": round(us / n, 2),
+            "group_end_us_per_exchange": round(end / n, 2), "host_us_per_step": round(us / max(1, steps), 2),
+            "in_progress_ends": int(after.get("groups_in_progress", 0) - before.get("groups_in_progress", 0))}
 
 
 def elapsed_s() -> float:
@@ -264,7 +293,12 @@ def main():
     # ---- headline: a FrameStream (halo exchanged every step; when a stripe
     # fits the Infinity Cache, round-robin over enough frames that every step
     # reads HBM-cold data; consecutive frames on alternating streams) ----
-    pipe1 = Pipeline(a.chain, overlap=not a.no_overlap, halo_depth=1)
+    if a.self_halo and (world != 1 or a.backend != "rccl"):
+        raise SystemExit("--self-halo needs one rank on the rccl backend (the communicator sends to itself)")
+    if a.self_halo:
+        # the ref-window and e2e scopes verify a non-periodic frame: not run here
+        a.ref_steps = a.e2e_steps = 0
+    pipe1 = Pipeline(a.chain, overlap=not a.no_overlap, halo_depth=1, self_halo=a.self_halo)
     fs = parallel.FrameStream(ctx, pipe1, W, H, Cc, frames=a.frames, streams=a.streams, autotune=not a.no_autotune)
     ws_max, fits_mall, cold = fs.ws_max, fs.fits_mall, fs.cold
     nframes, nstreams = len(fs), fs.nstreams
@@ -283,12 +317,12 @@ def main():
     if a.no_overlap and world > 1:
         fs.set_schedule("serial")
         sched = {"chosen": fs.schedule, "ms": {}, "requested": "serial"}
-    elif a.halo_schedule != "auto" and world > 1:
+    elif a.halo_schedule != "auto" and (world > 1 or a.self_halo):
         fs.set_schedule(a.halo_schedule)
         sched = {"chosen": fs.schedule, "ms": {}, "requested": a.halo_schedule}
     else:
         sched = dict(fs.pick_schedule(max_over_ranks, barrier), requested="auto")
-        if world == 1:
+        if world == 1 and not a.self_halo:
             sched["chosen"] = "none (one rank: no exchange)"
     nstreams = fs.nstreams  # the probe may have settled on one stream (and picked the stream set)
     streams = fs.streams
@@ -304,6 +338,7 @@ def main():
     sync()
     barrier()
     sync()
+    comm_before = comm_counters(ctx)
     t0 = time.perf_counter()
     for i in range(a.steps):
         step(i)
@@ -311,6 +346,7 @@ def main():
     sync()
     barrier()
     t1 = time.perf_counter()
+    comm_after = comm_counters(ctx)
     ms = max_over_ranks((t1 - t0) * 1e3)
     ms_per_step = ms / a.steps
     mpx = W * H / (ms_per_step * 1e-3) / 1e6
@@ -360,8 +396,30 @@ def main():
     # ---- correctness of the timed engine (untimed, after the timed region):
     # n_it iterated steps through the same schedule vs the golden path on edge
     # crops and on this stripe's upper seam ----
+    def torus_rows(lo, n):
+        """frame rows lo .. lo + n - 1 modulo H (the self-halo frame is vertically periodic)"""
+        parts, y = [], lo
+        while y < lo + n:
+            r = y % H
+            k = min(H - r, lo + n - y)
+            parts.append(C.synth_rows(a.seed, W, Cc, r, k))
+            y += k
+        return np.concatenate(parts, axis=0)
+
     verify = None
-    if not a.no_verify:
+    if not a.no_verify and a.self_halo:
+        n_it = 2 if iterable else 1
+        dp.load_synthetic(a.seed)
+        dp.run(n_it)
+        out = dp.result_stripe()
+        reach = n_it * R
+        crop = max(48, 4 * reach)
+        ok = True
+        for lo in (0, H - crop):  # both frame edges read the other edge's rows through the exchange
+            ref = gold(torus_rows(lo - reach, crop + 2 * reach), n_it)[reach:reach + crop]
+            ok &= same(out[lo:lo + crop], ref)
+        verify = all_ok(ok)
+    elif not a.no_verify:
         n_it = 2 if iterable else 1
         dp.load_synthetic(a.seed)
         dp.run(n_it)
@@ -418,7 +476,10 @@ def main():
             "global_batch": 1,
             "seq_len": H,
             "parallelism": f"rowpart{world}+halo",
-            "scope": ("resident: halo exchange every step + full-frame filter per step"
+            "scope": (("resident: halo exchange every step + full-frame filter per step" if world > 1 else
+                       "resident: self-halo -- the rank exchanges its boundary rows with itself through the one-rank "
+                       "RCCL communicator every step (vertically periodic frame) + full-frame filter per step"
+                       if a.self_halo else "resident: full-frame filter per step (one rank: no halo exchange)")
                       + (f", round-robin over {nframes} frames so every step reads HBM-cold data" if cold else
                          (f", round-robin over {nframes} independent frames" if nframes > 1 else ""))
                       + (f", consecutive frames on {nstreams} alternating streams" if nstreams > 1 else "")),
@@ -446,6 +507,8 @@ def main():
         "cache": fs.cache,
         "halo_depth": 1,
         "halo_schedule": sched,
+        "self_halo": bool(a.self_halo),
+        "exchange_cost": exchange_cost(comm_before, comm_after, a.steps),
         "transport_check": transport,
         "stripe_rows": [r for _, r in part],
         "stage_ms_rank0": stages,

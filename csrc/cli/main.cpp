@@ -441,6 +441,21 @@ int cmd_bench(const Args& a) {
           if (!g.devices.empty()) c.device = g.devices[r];
           if (nframes > 1) {
             c.cold = true;
+            // the frames' two streams (declared before the engines, which use
+            // them until they are destroyed): plain streams created back to
+            // back when STRIPE_FRAME_QUEUES=plain, else two streams with
+            // hardware queues of their own (Engine::dedicated_stream) --
+            // two per device, like parallel.FrameStream (more dedicated
+            // queues oversubscribe the GPU's queue slots, profiles/r5/shared/)
+            struct PlainStreams {
+              hipStream_t s[2] = {nullptr, nullptr};
+              ~PlainStreams() {
+                for (auto x : s)
+                  if (x) (void)hipStreamDestroy(x);
+              }
+            } plain_streams;
+            const char* fq = std::getenv("STRIPE_FRAME_QUEUES");
+            const bool plain_q = fq && (std::strcmp(fq, "plain") == 0 || std::strcmp(fq, "pool") == 0);
             std::vector<std::unique_ptr<Engine>> fr;
             for (int f = 0; f < nframes; ++f) {
               EngineConfig cf = c;
@@ -451,10 +466,16 @@ int cmd_bench(const Args& a) {
             }
             // one GPU per rank (not `local` ranks sharing one): each frame on a
             // stream with a hardware queue of its own (Engine::dedicated_stream)
-            if ((backend != "local" || N == 1) && cfg.backend == BackendKind::Device)
+            if ((backend != "local" || N == 1) && cfg.backend == BackendKind::Device) {
+              const int dev = std::max(0, fr[0]->config().device);
+              if (plain_q) {
+                HIP_CHECK(hipSetDevice(dev));
+                for (auto& x : plain_streams.s) HIP_CHECK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+              }
               for (int f = 0; f < nframes; ++f)
-                fr[(size_t)f]->use_external_stream(
-                    Engine::dedicated_stream(std::max(0, fr[(size_t)f]->config().device), f % 8));
+                fr[(size_t)f]->use_external_stream(plain_q ? plain_streams.s[f % 2]
+                                                           : Engine::dedicated_stream(dev, f % 2));
+            }
             fr[0]->tune();
             for (int f = 1; f < nframes; ++f) fr[f]->set_tuning(fr[0]->bands(), fr[0]->caps(), fr[0]->policies(), fr[0]->orders());
             const bool it_ok = fr[0]->plan().cin == fr[0]->plan().cout;

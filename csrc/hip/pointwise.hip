@@ -260,7 +260,7 @@ void launch_pattern_check(const void* p, int64_t bytes, uint32_t tag, unsigned l
 }
 
 CopyRoofline copy_roofline(int device, int64_t bytes, int frames, int reps) {
-  STRIPE_CHECK(bytes > 0 && bytes < (int64_t)dev::kOOB, "copy roofline: 0 < bytes < 2 GiB");
+  STRIPE_CHECK(bytes > 0, "copy roofline: bytes must be positive");
   frames = std::max(1, frames);
   reps = std::max(3, reps);
   HIP_CHECK(hipSetDevice(device));
@@ -285,14 +285,22 @@ CopyRoofline copy_roofline(int device, int64_t bytes, int frames, int reps) {
     HIP_CHECK(hipDeviceSynchronize());
     HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
-    const unsigned blocks = (unsigned)div_up(n, 16 * dev::kNT);
+    // one buffer descriptor addresses < 2 GiB: larger copies (e.g. a 32768^2
+    // RGB frame, 3 GiB) run as back-to-back launches of at most 1 GiB each
+    constexpr int64_t kChunk = int64_t(1) << 30;
     r.bytes = n;
     r.frames = frames;
     for (int policy : {0, 16}) {  // default stores; sc1 (write-through) stores
       auto launch = [&](int i) {
         const int f = i % frames;
-        if (policy == 0) dev::k_copy_linear<0><<<blocks, dev::kNT, 0, s>>>(buf[2 * f], buf[2 * f + 1], (uint32_t)n);
-        else dev::k_copy_linear<16><<<blocks, dev::kNT, 0, s>>>(buf[2 * f], buf[2 * f + 1], (uint32_t)n);
+        for (int64_t o = 0; o < n; o += kChunk) {
+          const int64_t len = std::min(kChunk, n - o);
+          const unsigned blocks = (unsigned)div_up(len, 16 * dev::kNT);
+          if (policy == 0)
+            dev::k_copy_linear<0><<<blocks, dev::kNT, 0, s>>>(buf[2 * f] + o, buf[2 * f + 1] + o, (uint32_t)len);
+          else
+            dev::k_copy_linear<16><<<blocks, dev::kNT, 0, s>>>(buf[2 * f] + o, buf[2 * f + 1] + o, (uint32_t)len);
+        }
       };
       for (int i = 0; i < 2 * frames + 2; ++i) launch(i);
       HIP_CHECK(hipGetLastError());

@@ -207,6 +207,29 @@ void launch_stencil(const Pass& p, const PassConsts& pc, const PassLaunch& L, hi
   HIP_CHECK(hipGetLastError());
 }
 
+namespace {
+template <class F>
+constexpr bool runs_capable() {
+  if constexpr (F::SEP) return dev::SepTraits<F>::SYM;
+  else return false;
+}
+}  // namespace
+
+bool sep_order_supported(const Pass& p) {
+  // launch_one takes PassLaunch::order only on the plain path: no gray / LUT
+  // prologue, no expand epilogue, a separable filter with symmetric vertical
+  // taps (kRuns bands run bottom-up too)
+  if (p.kind != PassKind::Separable || p.pro.gray || p.pro.has_post || p.epi_expand) return false;
+  using namespace sdef;
+  switch (p.sid) {
+#define STRIPE_RUNS_CASE(F) \
+  case StencilId::F: return runs_capable<F>();
+    STRIPE_STENCIL_FILTERS(STRIPE_RUNS_CASE)
+#undef STRIPE_RUNS_CASE
+    default: return false;
+  }
+}
+
 bool conv_small_supported(const Pass& p) {
   // 7x7 RGB needs more than 256 VGPRs (f32 sums of 7 rows x 16 bytes): MFMA path
   return p.kind == PassKind::Conv && (p.K == 3 || p.K == 5 || (p.K == 7 && p.cmid == 1)) &&

@@ -59,6 +59,13 @@ struct EngineConfig {
                                 // whatever their size, and the autotuner times every candidate
                                 // on cold data (a rotation of scratch stripes larger than the
                                 // 256 MiB Infinity Cache) and tunes the policy too
+  bool self_halo = false;       // one rank on a one-rank device communicator (RCCL loopback)
+                                // plays an interior rank of a ring whose neighbours are both
+                                // itself: every pass exchanges its R boundary rows through the
+                                // communicator (its last rows become the halo above its first
+                                // row and vice versa, a vertically periodic frame) -- the
+                                // per-step transfers of an N > 1 rank, measurable on one GPU.
+                                // Deep halo stays off; every halo schedule applies.
   bool graphs = false;          // replay iterated chains from a captured hipGraph when a run()
                                 // involves no collective (single rank, or no halo exchange).
                                 // Off by default: measured on MI355X/ROCm 7, graph replay of
@@ -168,6 +175,8 @@ class Engine {
   int graph_launches() const { return graph_launches_; }
   // Iterations per chain-level halo exchange (0: one exchange per pass and iteration).
   int halo_depth() const { return depth_; }
+  // EngineConfig::self_halo in effect (the stripe exchanges halo rows with itself)
+  bool self_halo() const { return self_halo_; }
   // Tuned band heights, occupancy caps and memory policies per pass (after
   // autotune), for reporting.
   std::vector<int> bands() const;
@@ -262,6 +271,11 @@ class Engine {
   uint8_t* origin(const Buffer& b, int C) const;
   uint8_t* root_origin(const Buffer& b, int C) const;
   void exchange_halo(uint8_t* org, int C, int R, hipStream_t s);
+  // this rank exchanges halo rows (another active rank, or the self-halo ring)
+  bool neighbours() const { return part_.active > 1 || self_halo_; }
+  bool has_up() const { return rank_ > 0 || self_halo_; }
+  bool has_down() const { return rank_ + 1 < part_.active || self_halo_; }
+  bool self_halo_ = false;  // EngineConfig::self_halo, validated
   bool time_halo_ = true;  // record the halo stage events (last iteration of a run only)
   bool stage_timing_ = true;  // set_stage_timing
   void run_pass(const Pass& p, const uint8_t* in, uint8_t* out);

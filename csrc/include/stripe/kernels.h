@@ -115,6 +115,10 @@ void prepare_conv_consts(const Pass& p, PassConsts* pc, hipStream_t s);
 
 // Small general conv (K <= 7) on the VALU (csrc/hip/stencil.hip k_conv_small).
 bool conv_small_supported(const Pass& p);
+// The stencil launch honours PassLaunch::order (separable task order) for
+// this pass: plain separable passes with symmetric vertical taps (no gray /
+// LUT prologue, no expand epilogue).  The autotuner probes the order only here.
+bool sep_order_supported(const Pass& p);
 void launch_conv_small(const Pass& p, const PassLaunch& L, hipStream_t s);
 
 // Separable (rank-one) conv on MFMA (csrc/hip/blur_sep.hip).

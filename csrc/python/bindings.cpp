@@ -8,6 +8,7 @@
 #include <pybind11/functional.h>
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
+#include <thread>
 #include <pybind11/stl.h>
 
 #include <memory>
@@ -271,6 +272,43 @@ PYBIND11_MODULE(_C, m) {
         return d;
       });
   m.def("preconnect_peers", &preconnect_peers, py::arg("rank"), py::arg("world"));
+  // Test hook (tests/test_r6_advice.py): two host `local` ranks, rank 1 posts
+  // a receive of the wrong size.  Returns the errors of that group, of rank
+  // 0's send, and of a second group on rank 1 afterwards (the aborted hub's
+  // message, not a stale pending receive or an open group).
+  m.def("local_comm_failure_probe", []() {
+    py::gil_scoped_release nogil;
+    auto hub = make_local_hub(2, false, 30.0);
+    auto c0 = make_local_comm(hub, 0);
+    auto c1 = make_local_comm(hub, 1);
+    std::vector<uint8_t> a(16), b(32);
+    std::string e_recv, e_send, e_next;
+    std::thread t0([&] {
+      try {
+        c0->group_start();
+        c0->send(a.data(), a.size(), 1, nullptr);
+        c0->group_end();
+      } catch (const std::exception& e) {
+        e_send = e.what();
+      }
+    });
+    try {
+      c1->group_start();
+      c1->recv(b.data(), b.size(), 0, nullptr);
+      c1->group_end();
+    } catch (const std::exception& e) {
+      e_recv = e.what();
+    }
+    t0.join();
+    try {
+      c1->group_start();
+      c1->recv(b.data(), 16, 0, nullptr);
+      c1->group_end();
+    } catch (const std::exception& e) {
+      e_next = e.what();
+    }
+    return std::make_tuple(e_recv, e_send, e_next);
+  });
   // the bounded progress loop of the non-blocking communicators, driven by a
   // Python probe (0 done, 1 pending, 2 failed): unit tests of the state machine
   m.def("await_progress", [](const std::string& what, double limit_s, py::function probe, py::object aborted) {
@@ -485,6 +523,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("root_buffers", &EngineConfig::root_buffers)
       .def_readwrite("autotune", &EngineConfig::autotune)
       .def_readwrite("graphs", &EngineConfig::graphs)
+      .def_readwrite("self_halo", &EngineConfig::self_halo)
       .def_readwrite("cold", &EngineConfig::cold)
       .def_readwrite("pipeline", &EngineConfig::pipeline)
       .def_readwrite("halo_depth", &EngineConfig::halo_depth)
@@ -529,6 +568,7 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("world", &Engine::world)
       .def_property_readonly("out_channels", &Engine::out_channels)
       .def_property_readonly("halo_depth", &Engine::halo_depth)
+      .def_property_readonly("self_halo", &Engine::self_halo)
       .def_property_readonly("plan", [](const Engine& e) { return e.plan().describe(); })
       .def_property_readonly("partition", [](const Engine& e) { return e.partition().describe(); })
       .def_property_readonly("stripe", [](const Engine& e) {

@@ -69,6 +69,10 @@ class LocalHub {
     m->consumed = true;
     changed();
   }
+  bool is_consumed(const std::shared_ptr<Msg>& m) {
+    std::lock_guard<std::mutex> lk(mu_);
+    return m->consumed;
+  }
   void wait_consumed(const std::shared_ptr<Msg>& m, int dst) {
     std::unique_lock<std::mutex> lk(mu_);
     wait(lk, [&] { return m->consumed; }, "send to rank " + std::to_string(dst) + " to be received");
@@ -256,8 +260,29 @@ class LocalComm final : public Comm {
       group_events_.clear();
     } catch (const std::exception& e) {
       hub_->abort(std::string("rank ") + std::to_string(rank_) + ": " + e.what());
+      drop_group();
       throw;
     }
+  }
+  // A failed group: its events are destroyed rather than pooled (a peer's
+  // stream may still hold a wait on them, and the aborted hub runs no later
+  // group), a receiver-created `done` of a consumed message with it (the
+  // receiver set it before marking the message consumed, under the hub's
+  // lock), and the pending lists are cleared so no later call sees them.
+  void drop_group() {
+    if (hub_->device()) {
+      for (auto& sd : sends_)
+        if (hub_->is_consumed(sd.m) && sd.m->own_done && sd.m->done) {
+          (void)hipEventDestroy(sd.m->done);
+          sd.m->done = nullptr;
+        }
+      for (hipEvent_t ev : group_events_) (void)hipEventDestroy(ev);
+      (void)hipGetLastError();
+    }
+    group_events_.clear();
+    sends_.clear();
+    recvs_.clear();
+    in_group_ = false;
   }
 
   std::shared_ptr<LocalHub> hub_;

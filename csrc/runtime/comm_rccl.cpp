@@ -10,6 +10,7 @@
 // returns and the others wait in MPI forever).
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdlib>
@@ -76,9 +77,23 @@ bool blocking_requested() {
   return e && std::atoi(e) != 0;
 }
 
+// STRIPE_RCCL_MAX_CTAS=n caps the workgroups (channels) RCCL's kernels use on
+// this framework's communicators (ncclConfig_t::maxCTAs; 0 / unset: RCCL's
+// choice).  The per-step halo messages are ~100 KiB: a few channels move them
+// as fast as many, and every extra workgroup of rcclGenericKernel is a CU slot
+// taken from the stencil running beside it.
+int max_ctas_requested() {
+  const char* e = std::getenv("STRIPE_RCCL_MAX_CTAS");
+  return e ? std::max(0, std::atoi(e)) : 0;
+}
+
 ncclConfig_t nonblocking_config() {
   ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
   cfg.blocking = blocking_requested() ? 1 : 0;
+  if (const int n = max_ctas_requested(); n > 0) {
+    cfg.minCTAs = 1;
+    cfg.maxCTAs = n;
+  }
   return cfg;
 }
 
@@ -114,6 +129,7 @@ class RcclComm final : public Comm {
   // poll round (run_group aborts every rank from the failing rank's thread).
   void group_start() override {
     enter();
+    g0_ = std::chrono::steady_clock::now();
     NCCL_CHECK(ncclGroupStart());
     in_group_ = true;
   }
@@ -131,10 +147,23 @@ class RcclComm final : public Comm {
     // an abort raised between group_start and here still closes the group
     // (the RCCL group state is per thread), then takes effect
     in_group_ = false;
+    const auto t1 = std::chrono::steady_clock::now();
     const ncclResult_t r = ncclGroupEnd();
     enter();
-    if (r == ncclInProgress) await("group end (p2p connection setup / enqueue)");
-    else if (r != ncclSuccess) NCCL_CHECK(r);
+    if (r == ncclInProgress) {
+      await("group end (p2p connection setup / enqueue)");
+      ++groups_pending_;
+    } else if (r != ncclSuccess) {
+      NCCL_CHECK(r);
+    }
+    // host cost of the group: enqueue (group start .. group end) and the end
+    // itself (ncclGroupEnd plus the progress poll of a non-blocking comm)
+    const auto t2 = std::chrono::steady_clock::now();
+    const double all = std::chrono::duration<double, std::micro>(t2 - g0_).count();
+    group_us_ += all;
+    group_end_us_ += std::chrono::duration<double, std::micro>(t2 - t1).count();
+    group_max_us_ = std::max(group_max_us_, all);
+    ++groups_;
   }
   void barrier() override {
     enter();
@@ -198,7 +227,15 @@ class RcclComm final : public Comm {
             {"nccl_count", (double)count},    {"nccl_device", (double)cudev},
             {"nccl_user_rank", (double)urank}, {"device", (double)dev_},
             {"init_ms", init_ms_},            {"connect_ms", connect_ms_},
-            {"nonblocking", blocking_requested() ? 0.0 : 1.0}};
+            {"nonblocking", blocking_requested() ? 0.0 : 1.0},
+            {"max_ctas", (double)max_ctas_requested()},
+            // host-side cost of every grouped call so far (callers diff two
+            // snapshots): count, summed and worst microseconds from group
+            // start to the end's return, the part spent in ncclGroupEnd and
+            // its progress poll, and how many ends returned in progress
+            {"groups", (double)groups_},               {"group_us", group_us_},
+            {"group_end_us", group_end_us_},           {"group_max_us", group_max_us_},
+            {"groups_in_progress", (double)groups_pending_}};
   }
 
   // Connect this rank's p2p peers (preconnect_peers) with a 4-byte exchange,
@@ -281,6 +318,9 @@ class RcclComm final : public Comm {
   std::string why_;
   hipStream_t bar_stream_ = nullptr;
   int* bar_buf_ = nullptr;
+  std::chrono::steady_clock::time_point g0_{};
+  int64_t groups_ = 0, groups_pending_ = 0;
+  double group_us_ = 0, group_end_us_ = 0, group_max_us_ = 0;
 };
 
 }  // namespace

@@ -108,6 +108,12 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
     STRIPE_CHECK(!cfg_.legacy_partition, "row_weights and the legacy split are exclusive");
     part_ = plan_rows_weighted(cfg_.H, cfg_.row_weights, std::max(1, plan_.max_radius));
   }
+  if (cfg_.self_halo) {
+    STRIPE_CHECK(device() && comm_ && world_ == 1 && std::strcmp(comm_->backend(), "rccl") == 0 && cfg_.halo &&
+                     !cfg_.legacy_partition,
+                 "self_halo needs a device engine on a one-rank RCCL communicator (loopback) with halo exchange on");
+    self_halo_ = true;
+  }
   halo_ = plan_.max_radius;
   depth_ = choose_depth();
   if (depth_ >= 1) halo_ = std::max(halo_, depth_ * chain_reach());
@@ -267,6 +273,11 @@ const uint8_t* Engine::output_origin() const {
 
 RowGeom Engine::geom() const {
   const Stripe& st = stripe();
+  // self-halo: the stripe sits inside a taller virtual frame, so every row
+  // within reach of its edges is read from the halo rows the exchange filled
+  // (never border-resolved); the offset keeps the MFMA passes' 32-row group
+  // grid where row 0 puts it
+  if (self_halo_) return RowGeom{kSelfHaloRow0, st.rows + 2 * kSelfHaloRow0};
   // a legacy split (Q7) processes only the covered rows H/N*N: with halo
   // exchange those rows form the frame, so the last rank's bottom rows take the
   // border rather than halo rows no neighbour fills
@@ -483,7 +494,7 @@ void Engine::scatter() {
 
 void Engine::exchange_halo(uint8_t* org, int C, int R, hipStream_t s) {
   const Stripe& st = stripe();
-  if (st.rows == 0 || part_.active <= 1) return;
+  if (st.rows == 0 || !neighbours()) return;
   const int64_t P = pitch(C);
   const size_t bytes = (size_t)(R * P);
   uint8_t* base = org - kMarginBytes;
@@ -491,9 +502,20 @@ void Engine::exchange_halo(uint8_t* org, int C, int R, hipStream_t s) {
   const int down = rank_ + 1 < part_.active ? rank_ + 1 : -1;
   TraceRange tr("stripe.halo");
   fault_point("halo", rank_);
+  STRIPE_CHECK(!self_halo_ || R <= st.rows, "self-halo of " << R << " rows needs a stripe of at least that many rows");
   if (time_halo_) stage_begin(Stage::Halo, s);
   comm_->group_start();
-  if (up >= 0) {
+  if (self_halo_) {
+    // the rank is its own upper and lower neighbour: the same two sends and
+    // two receives an interior rank posts, all to itself.  Sends and receives
+    // between one pair of ranks match in issue order, so the bottom rows
+    // (what the upper neighbour sends down) land in the halo above row 0 and
+    // the top rows in the halo below the last row.
+    comm_->send(base + (int64_t)(st.rows - R) * P, bytes, rank_, s);
+    comm_->recv(base - (int64_t)R * P, bytes, rank_, s);
+    comm_->send(base, bytes, rank_, s);
+    comm_->recv(base + (int64_t)st.rows * P, bytes, rank_, s);
+  } else if (up >= 0) {
     comm_->send(base, bytes, up, s);
     comm_->recv(base - (int64_t)R * P, bytes, up, s);
   }
@@ -551,7 +573,7 @@ void Engine::run_pass(const Pass& p, const uint8_t* in, uint8_t* out) {
   if (rows == 0) return;
   const RowGeom g = geom();
   const int R = p.R;
-  const bool xchg = (cfg_.halo && R > 0 && part_.active > 1) || (device() && schedule_emu() == 1 && R > 0);
+  const bool xchg = (cfg_.halo && R > 0 && neighbours()) || (device() && schedule_emu() == 1 && R > 0);
   if (device() && schedule_emu() == 3 && R > 0 && rows > 2 * R) {  // two launches, one stream, no events
     const size_t pi3 = (size_t)(&p - plan_.passes.data());
     PassLaunch L3 = make_launch(p, in, out, (int)pi3);
@@ -621,7 +643,7 @@ void Engine::run_pass(const Pass& p, const uint8_t* in, uint8_t* out) {
 // chain without halo exchange.  (RCCL calls are kept out of captured graphs.)
 bool Engine::graph_ok() const {
   if (!device() || !cfg_.graphs) return false;
-  const bool comm = cfg_.halo && plan_.max_radius > 0 && part_.active > 1;
+  const bool comm = cfg_.halo && plan_.max_radius > 0 && neighbours();
   return !comm && stripe().rows > 0;
 }
 

@@ -25,6 +25,11 @@ inline int schedule_emu() {
   return v;
 }
 
+// Global row of a self-halo stripe's first row inside its virtual frame
+// (Engine::geom): beyond any stencil reach, a multiple of the MFMA passes'
+// 32-row group grid.
+constexpr int kSelfHaloRow0 = 4096;
+
 // host wall clock in milliseconds
 inline double host_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();

@@ -38,7 +38,7 @@ bool Engine::pipelined_ok() const {
   if (device() && schedule_emu() == 2 && plan_.passes.size() == 1 && plan_.cin == plan_.cout &&
       stripe().rows > 4 * plan_.passes[0].R && plan_.passes[0].R > 0)
     return true;
-  if (!device() || !cfg_.halo || !cfg_.overlap || part_.active <= 1) return false;
+  if (!device() || !cfg_.halo || !cfg_.overlap || !neighbours()) return false;
   if (plan_.passes.size() != 1 || plan_.cin != plan_.cout) return false;
   const int R = plan_.passes[0].R;
   // large windows (MFMA blur) pay a whole 32-row group per thin rim range:
@@ -56,7 +56,7 @@ void Engine::set_halo_schedule(int s) {
 
 int Engine::halo_schedule() const {
   // mirrors run(1)'s dispatch and run_pass's split for a single-pass chain
-  if (!device() || !cfg_.halo || part_.active <= 1) return 0;
+  if (!device() || !cfg_.halo || !neighbours()) return 0;
   if (cfg_.pipeline && cfg_.overlap && pipelined_ok()) return 2;
   const int R = plan_.passes.empty() ? 0 : plan_.passes[0].R;
   return cfg_.overlap && stripe().rows > 2 * R ? 1 : 0;

@@ -140,9 +140,9 @@ void Engine::run_e2e(int chunks) {
   }
   const Pass& p = plan_.passes[0];
   const int R = p.R;
-  const bool xchg = cfg_.halo && R > 0 && part_.active > 1;
-  const bool up = xchg && rank_ > 0;
-  const bool down = xchg && rank_ + 1 < part_.active;
+  const bool xchg = cfg_.halo && R > 0 && neighbours();
+  const bool up = xchg && has_up();
+  const bool down = xchg && has_down();
   uint8_t* out_org = origin(buf_[1], cout);
   PassLaunch L = make_launch(p, in_org, out_org, 0);
   if (xchg) {  // halo rows come from the first and last chunks
@@ -477,7 +477,7 @@ void Engine::run_to_host(void* dst, int chunks) {
     copy2d(host, Eout, origin(buf_[ob], cout), pitch(cout), Eout, rows, s_d2h_, 0);
   } else {
     stage_begin(Stage::Compute, s_compute_);
-    const bool xchg = cfg_.halo && p0.R > 0 && part_.active > 1;
+    const bool xchg = cfg_.halo && p0.R > 0 && neighbours();
     uint8_t* in = origin(buf_[in_buf], p0.cin);
     uint8_t* out = origin(buf_[in_buf ^ 1], cout);
     if (xchg) exchange_halo(in, p0.cin, p0.R, s_compute_);

@@ -231,7 +231,7 @@ void Engine::autotune_bands() {
     // (16K RGB: 270-272 us at 12 rows vs 277 us one-task at 16, cold N=8
     // share: no gain, profiles/r5/cold/README.md)
     int best_order = 0;
-    if (p.kind == PassKind::Separable) {
+    if (sep_order_supported(p)) {
       if (env_sep_order() >= 0) {
         best_order = env_sep_order() == 1 ? 1 : 0;
       } else {

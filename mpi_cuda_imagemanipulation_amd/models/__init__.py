@@ -63,7 +63,7 @@ class Pipeline:
 
     def __init__(self, chain: str = "gaussian5", border: str = "reflect101", halo: bool = True,
                  legacy_partition: bool = False, fuse: bool = True, overlap: bool = True, halo_depth: int = 0,
-                 dist_chunks: int = 0):
+                 dist_chunks: int = 0, self_halo: bool = False):
         self.spec = PipelineSpec(chain, border, halo, legacy_partition)
         self.fuse = fuse
         self.overlap = overlap
@@ -72,6 +72,10 @@ class Pipeline:
         # > 1: a one-iteration distributed run ships, filters and gathers single-pass
         # chains in this many overlapped row chunks (Engine::run_dist)
         self.dist_chunks = int(dist_chunks)
+        # one rank on a one-rank RCCL communicator exchanges its boundary rows
+        # with itself every pass (an interior rank's transfers, on one GPU;
+        # the frame is then vertically periodic -- EngineConfig::self_halo)
+        self.self_halo = bool(self_halo)
         C.parse_chain(chain)  # validate early
 
     @classmethod
@@ -108,6 +112,7 @@ class Pipeline:
         cfg.autotune = bool(autotune)
         cfg.halo_depth = self.halo_depth
         cfg.dist_chunks = self.dist_chunks
+        cfg.self_halo = self.self_halo
         if row_weights is not None:
             cfg.row_weights = [float(w) for w in row_weights]
         sched = os.environ.get("STRIPE_HALO_SCHEDULE")  # tuning: overlap | pipeline | serial
