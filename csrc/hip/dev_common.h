@@ -48,37 +48,7 @@ struct KArgs {
   uint8_t* out_base;
   uint32_t in_bytes, in_org, in_zero;
   uint32_t out_bytes, out_org;
-  // Diagnostic per-wave timeline (nullptr in every engine launch): when set,
-  // each stencil wave writes {start, end, HW_ID, XCC_ID} (4 dwords; times in
-  // 100 MHz ticks of the constant real-time counter) at stamps[4 * wave] --
-  // the ramp, the per-wave lifetime and the tail of one dispatch
-  // (tools/sepx.hip, profiles/r5/cold/).
-  uint32_t* stamps;
-  // Persistent launches (k_sep<..., PERSIST>): the grid holds the resident
-  // workgroups only and every wave claims tasks from a device work queue
-  // (queue[0]: next task, queue[1]: retired waves; the last wave to retire
-  // resets both to zero for the next launch on the same queue) until all
-  // persist_tasks tasks are claimed.  Range 0 ends in tail_band-row bands from
-  // row tail_y on (nbig bands of `band` rows before it): the last tasks
-  // claimed are short, so the launch's tail is one short task long.
-  uint32_t* queue;
-  int persist_tasks;
-  int tail_y, tail_band, nbig;
 };
-
-__device__ __forceinline__ uint32_t stamp_now() { return (uint32_t)__builtin_amdgcn_s_memrealtime(); }
-
-// Closes a wave's stamp: waits for its own memory operations (the stores count
-// as done only once they have left the wave), then lanes 0-3 write the record.
-__device__ __forceinline__ void stamp_wave(uint32_t* stamps, int wave_id, uint32_t t0) {
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-  const uint32_t t1 = stamp_now();
-  const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID: wave, SIMD, CU, SE
-  const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
-  const int lane = threadIdx.x & 63;
-  const uint32_t v = lane == 0 ? t0 : lane == 1 ? t1 : lane == 2 ? hw : xcc;
-  if (lane < 4) stamps[4 * (int64_t)wave_id + lane] = v;
-}
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);

@@ -40,41 +40,14 @@ __device__ __forceinline__ uint8_t jpeg_u8(float v) {
   return (uint8_t)fminf(255.f, fmaxf(0.f, r));
 }
 
-// One wave per 8x8 block (lane = row * 8 + column), four blocks per workgroup:
-// row pass tmp[v][x] = sum_u B[x][u] F[v][u], column pass out[y][x] =
-// sum_v B[y][v] tmp[v][x], both through LDS.
-__global__ __launch_bounds__(256) void k_jpeg_idct(const int16_t* __restrict__ coef, int64_t nblocks, int bw,
-                                                   uint8_t* __restrict__ plane, int64_t ps) {
-  __shared__ float f[4][64];
-  __shared__ float t[4][64];
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const int64_t b = (int64_t)blockIdx.x * 4 + w;
-  const bool ok = b < nblocks;
-  f[w][l] = ok ? (float)coef[b * 64 + l] : 0.f;
-  __syncthreads();
-  const int r = l >> 3, c = l & 7;
-  float s = 0.f;
-#pragma unroll
-  for (int u = 0; u < 8; ++u) s += kJpegBasis[c * 8 + u] * f[w][r * 8 + u];
-  t[w][l] = s;
-  __syncthreads();
-  float o = 0.f;
-#pragma unroll
-  for (int v = 0; v < 8; ++v) o += kJpegBasis[r * 8 + v] * t[w][v * 8 + c];
-  if (ok) {
-    const int64_t by = b / bw, bx = b % bw;
-    plane[(by * 8 + r) * ps + bx * 8 + c] = jpeg_u8(o + 128.f);
-  }
-}
-
 // IDCT with a lane per block row: a wave owns 8 blocks (lane = 8 b + r).  A
 // lane loads its row's 8 coefficients with one 16-byte load (a block's 128
 // bytes by 8 lanes), runs the row pass in registers, trades rows for columns
 // through LDS for the column pass, and rows back for the store: one 8-byte
 // store of a block row per lane, 8 blocks of a block row side by side (64
-// contiguous bytes per image row) instead of a byte store per thread.  The
-// sums run in the same order with the same operations as k_jpeg_idct (fp
-// contraction is off in this file): bit-identical.
+// contiguous bytes per image row) instead of a byte store per thread.  Row
+// pass tmp[v][x] = sum_u B[x][u] F[v][u], column pass out[y][x] = sum_v
+// B[y][v] tmp[v][x], in a fixed order (fp contraction is off in this file).
 __global__ __launch_bounds__(256) void k_jpeg_idct8(const int16_t* __restrict__ coef, int64_t nblocks, int bw,
                                                     uint8_t* __restrict__ plane, int64_t ps) {
   __shared__ float tt[4][8][65];   // [wave][block][row * 8 + col], padded against bank conflicts
@@ -281,61 +254,6 @@ __global__ __launch_bounds__(256) void k_jpeg_color16(JpegPlaneRef c0, JpegPlane
   }
 }
 
-// one thread per output pixel: upsample every component, convert, store
-// interleaved RGB (or gray) rows of `pitch` bytes (STRIPE_JPEG_COLOR=1: the
-// round-4 form, kept for A/B runs)
-__global__ __launch_bounds__(256) void k_jpeg_color(JpegPlaneRef c0, JpegPlaneRef c1, JpegPlaneRef c2, int nc,
-                                                    bool rgb, int W, int H, uint8_t* __restrict__ dst, int64_t pitch) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (int64_t)W * H) return;
-  const int y = (int)(i / W), x = (int)(i % W);
-  uint8_t* o = dst + (int64_t)y * pitch + (int64_t)x * nc;
-  const int Y = jpeg_sample(c0, x, y);
-  if (nc == 1) {
-    o[0] = (uint8_t)Y;
-    return;
-  }
-  const int U = jpeg_sample(c1, x, y), V = jpeg_sample(c2, x, y);
-  if (rgb) {
-    o[0] = (uint8_t)Y;
-    o[1] = (uint8_t)U;
-    o[2] = (uint8_t)V;
-    return;
-  }
-  const float yy = (float)Y, cb = (float)U - 128.f, cr = (float)V - 128.f;
-  o[0] = jpeg_u8(yy + 1.402f * cr);
-  o[1] = jpeg_u8(yy - 0.344136f * cb - 0.714136f * cr);
-  o[2] = jpeg_u8(yy + 1.772f * cb);
-}
-
-// encode: level-shifted luma (or gray) / centred, box-averaged chroma planes
-// of MCU-padded size from an interleaved source (edge pixels replicated)
-__global__ __launch_bounds__(256) void k_jpeg_planes(const uint8_t* __restrict__ src, int64_t pitch, int W, int H,
-                                                     int nc, int comp, int f, int ps, int rows,
-                                                     float* __restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (int64_t)ps * rows) return;
-  const int y = (int)(i / ps), x = (int)(i % ps);
-  auto px = [&](int xx, int yy, int c) -> float {
-    xx = min(W - 1, xx);
-    yy = min(H - 1, yy);
-    return (float)src[(int64_t)yy * pitch + (int64_t)xx * nc + c];
-  };
-  if (comp == 0) {
-    const float v = nc == 1 ? px(x, y, 0) : 0.299f * px(x, y, 0) + 0.587f * px(x, y, 1) + 0.114f * px(x, y, 2);
-    out[i] = v - 128.f;
-    return;
-  }
-  float acc = 0.f;
-  for (int dy = 0; dy < f; ++dy)
-    for (int dx = 0; dx < f; ++dx) {
-      const int sx = x * f + dx, sy = y * f + dy;
-      const float r = px(sx, sy, 0), g = px(sx, sy, 1), b = px(sx, sy, 2);
-      acc += comp == 1 ? -0.168736f * r - 0.331264f * g + 0.5f * b : 0.5f * r - 0.418688f * g - 0.081312f * b;
-    }
-  out[i] = acc / (float)(f * f);
-}
-
 // 16 plane samples x0 .. x0 + 15 of row y from an in-frame source block of
 // 16 FS pixels x FS rows (NC channels): words of 16-byte row loads, bytes
 // picked at compile-time indices (no scratch), the per-element expressions.
@@ -389,7 +307,8 @@ __device__ __forceinline__ void planes_group(const uint8_t* __restrict__ src, in
 // (no edge replication) reads them as 16-byte row loads (ALIGNED: source rows
 // 16-byte aligned) and stores 16 floats as four 16-byte stores; edge groups
 // replicate edge pixels element by element.  Each sample is the per-element
-// form's expression in the same order (k_jpeg_planes).
+// reference expression (luma 0.299 / 0.587 / 0.114 level-shifted; chroma
+// box-averaged over f x f) in a fixed order.
 template <bool ALIGNED>
 __global__ __launch_bounds__(256) void k_jpeg_planes16(const uint8_t* __restrict__ src, int64_t pitch, int W, int H,
                                                        int nc, int comp, int f, int ps,
@@ -496,23 +415,6 @@ bool pin_uploads() {
   }();
   return on;
 }
-// STRIPE_JPEG_COLOR=1: the per-pixel colour / planes kernels (A/B switch)
-// STRIPE_JPEG_IDCT=1: the block-per-wave IDCT (k_jpeg_idct) for A/B runs
-bool legacy_idct() {
-  static const bool on = [] {
-    const char* e = std::getenv("STRIPE_JPEG_IDCT");
-    return e && std::atoi(e) == 1;
-  }();
-  return on;
-}
-
-bool legacy_color() {
-  static const bool on = [] {
-    const char* e = std::getenv("STRIPE_JPEG_COLOR");
-    return e && std::atoi(e) == 1;
-  }();
-  return on;
-}
 }  // namespace
 
 namespace {
@@ -584,8 +486,7 @@ void jpeg_pixels_device(const JpegCoefs& jc, uint8_t* dst, int64_t pitch, hipStr
       else (void)hipGetLastError();  // not registrable: the pageable copy below still works
     }
     HIP_CHECK(hipMemcpyAsync(dcoef, c.coef.data(), cbytes, hipMemcpyHostToDevice, s));
-    if (legacy_idct()) dev::k_jpeg_idct<<<blocks_for(nb, 4), 256, 0, s>>>(dcoef, nb, c.bw, planes[(size_t)ci], ps);
-    else dev::k_jpeg_idct8<<<blocks_for(nb, 32), 256, 0, s>>>(dcoef, nb, c.bw, planes[(size_t)ci], ps);
+    dev::k_jpeg_idct8<<<blocks_for(nb, 32), 256, 0, s>>>(dcoef, nb, c.bw, planes[(size_t)ci], ps);
     HIP_CHECK(hipGetLastError());
     st.free_async(dcoef);
     ref[ci] = {planes[(size_t)ci], ps, (jc.W * c.h + jc.hmax - 1) / jc.hmax, (jc.H * c.v + jc.vmax - 1) / jc.vmax,
@@ -593,10 +494,7 @@ void jpeg_pixels_device(const JpegCoefs& jc, uint8_t* dst, int64_t pitch, hipStr
   }
   const dev::JpegPlaneRef& r1 = ref[nc == 3 ? 1 : 0];
   const dev::JpegPlaneRef& r2 = ref[nc == 3 ? 2 : 0];
-  if (legacy_color()) {
-    const int64_t npx = (int64_t)jc.W * jc.H;
-    dev::k_jpeg_color<<<blocks_for(npx, 256), 256, 0, s>>>(ref[0], r1, r2, nc, jc.rgb, jc.W, jc.H, dst, pitch);
-  } else {
+  {
     const dim3 grid(blocks_for(blocks_for(jc.W, 16), 256), (unsigned)jc.H);
     if ((uintptr_t)dst % 16 == 0 && pitch % 16 == 0)
       dev::k_jpeg_color16<true><<<grid, 256, 0, s>>>(ref[0], r1, r2, nc, jc.rgb, jc.W, dst, pitch);
@@ -635,10 +533,7 @@ JpegQuant jpeg_quantise_device(const uint8_t* src, int64_t pitch, int W, int H, 
     HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&plane), (size_t)ps * rows * sizeof(float), s));
     HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&dcoef), (size_t)nb * 64 * sizeof(int16_t), s));
     const int f = ci == 0 ? 1 : jq.hs;
-    if (legacy_color()) {
-      dev::k_jpeg_planes<<<blocks_for((int64_t)ps * rows, 256), 256, 0, s>>>(src, pitch, W, H, C, ci, f, ps, rows,
-                                                                               plane);
-    } else {
+    {
       const dim3 grid(blocks_for(blocks_for(ps, 16), 256), (unsigned)rows);
       if ((uintptr_t)src % 16 == 0 && pitch % 16 == 0)
         dev::k_jpeg_planes16<true><<<grid, 256, 0, s>>>(src, pitch, W, H, C, ci, f, ps, plane);

@@ -59,26 +59,10 @@ struct WaveTask {
   int xt;     // tile column
   int ys, ye; // rows
   bool valid;
-  int dir = 1;  // 1: rows ys .. ye - 1 top-down; -1: bottom-up (kQuad launches)
+  int dir = 1;  // 1: rows ys .. ye - 1 top-down; -1: bottom-up (kRuns launches)
 };
 
-// Row range of band `by` of a persistent launch: range 0 in `band`-row bands
-// down to tail_y, then tail_band-row bands (KArgs::tail_y); range 1 as usual.
-__device__ __forceinline__ void band_range_tail(const KArgs& a, int by, int& ys, int& ye) {
-  if (by < a.nbig) {
-    ys = a.ry0 + by * a.band;
-    ye = min(ys + a.band, a.tail_y);
-  } else if (by < a.nb0) {
-    ys = a.tail_y + (by - a.nbig) * a.tail_band;
-    ye = min(ys + a.tail_band, a.ry1);
-  } else {
-    ys = a.ry2 + (by - a.nb0) * a.band;
-    ye = min(ys + a.band, a.ry3);
-  }
-}
-
 // Task w of a pass: tile column w mod ntx of band w / ntx (band-major).
-template <bool TAIL = false>
 __device__ __forceinline__ WaveTask task_at(const KArgs& a, int w) {
   WaveTask t;
   t.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -88,33 +72,9 @@ __device__ __forceinline__ WaveTask task_at(const KArgs& a, int w) {
   t.valid = bt < a.nbands;
   t.ys = t.ye = 0;
   if (t.valid) {
-    if constexpr (TAIL) band_range_tail(a, bt, t.ys, t.ye);
-    else band_range(a, bt, t.ys, t.ye);
-    t.valid = t.ys < t.ye;
-  }
-  return t;
-}
-
-// kQuad task: a workgroup owns 4 vertically consecutive bands of one tile
-// column (wave v: band 4 q + v) and even bands run bottom-up, odd bands
-// top-down, so the two readers of every boundary's halo rows inside the
-// workgroup read them at the same moment (both first or both last) on one CU:
-// the second read is an L2 (or L1) hit instead of another fabric read.  The
-// boundary to the next quad is read last by both of its readers.
-__device__ __forceinline__ WaveTask quad_task(const KArgs& a) {
-  WaveTask t;
-  t.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  t.lane = threadIdx.x & 63;
-  const int g = xcd_remap((int)blockIdx.x, (int)gridDim.x, a.nxcd);
-  t.xt = g % a.ntx;
-  const int bt = 4 * (g / a.ntx) + t.wave;
-  t.valid = bt < a.nbands;
-  t.ys = t.ye = 0;
-  if (t.valid) {
     band_range(a, bt, t.ys, t.ye);
     t.valid = t.ys < t.ye;
   }
-  t.dir = (bt & 1) ? 1 : -1;
   return t;
 }
 
@@ -159,43 +119,6 @@ template <int NW = kWaves>
 __device__ __forceinline__ WaveTask wave_task(const KArgs& a) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   return task_at(a, xcd_remap((int)blockIdx.x, (int)gridDim.x, a.nxcd) * NW + wave);
-}
-
-// Work queue of persistent launches (KArgs::queue, kQueueWords dwords).
-//   * round 0 is static: wave w of the grid takes task w (no claim);
-//   * the remaining tasks form kQueueShards classes (task - nwaves mod 8), each
-//     with its own head counter on its own 128-byte line, drained by the
-//     workgroups with blockIdx % 8 == class (on MI355X those share an XCD).
-//     One counter serves ~88 claims / us (MI355X_MICROARCH.md, row dequeue):
-//     a single head for all 2048 waves made a 40 us pass take 150 us;
-//   * a wave claims its next task (one lane, a device-scope atomic with
-//     return) before streaming the current one, so the claim's latency hides
-//     under the task and the index is read only at the end;
-//   * the workgroups of a class arrive on the class's counter after their last
-//     (failed) claim; the last to arrive resets the class's head and counter
-//     for the next launch on this queue (stream order publishes the reset).
-// Correct for any workgroup placement and residency: every class has >= 1
-// workgroup (grid >= kQueueShards, launch side) and each one drains its class.
-constexpr int kQueueShards = 8;
-constexpr int kQueueLine = 32;                          // dwords per 128-byte line
-constexpr int kQueueWords = 2 * kQueueShards * kQueueLine;  // heads, then arrival counters
-
-__device__ __forceinline__ uint32_t queue_claim_async(uint32_t* head) {
-  uint32_t v = 0;
-  if ((threadIdx.x & 63) == 0) v = atomicAdd(head, 1u);
-  return v;  // lane 0's VGPR; read with readfirstlane once needed
-}
-
-__device__ __forceinline__ void queue_retire(uint32_t* q, int shard) {
-  __syncthreads();  // every wave of the workgroup has made its last claim
-  if (threadIdx.x == 0) {
-    const uint32_t members = (gridDim.x - (uint32_t)shard + kQueueShards - 1) / kQueueShards;
-    uint32_t* arrived = q + (kQueueShards + shard) * kQueueLine;
-    if (atomicAdd(arrived, 1u) == members - 1u) {
-      atomicExch(q + shard * kQueueLine, 0u);
-      atomicExch(arrived, 0u);
-    }
-  }
 }
 
 enum { PRO_NONE = 0, PRO_LUT = 1, PRO_GRAY = 2, PRO_GRAYLUT = 3 };
@@ -612,7 +535,7 @@ __device__ __forceinline__ void sep_task(const KArgs& a, const WaveTask& t, cons
   // (t.dir < 0) maps logical row y to physical row ys + ye - 1 - y.  The
   // vertical taps are symmetric (sobel's difference taps flip sign under a
   // magnitude), so the outputs are the same bits in either direction.
-  constexpr bool kRev = SepTraits<F>::SYM;  // kQuad instances only (static_assert there)
+  constexpr bool kRev = SepTraits<F>::SYM;  // kRuns instances only (static_assert there)
   const int pbase = kRev && t.dir < 0 ? ys + ye - 1 : 0;
   const int psign = kRev && t.dir < 0 ? -1 : 1;
   auto phys = [&](int y) __attribute__((always_inline)) { return pbase + psign * y; };
@@ -803,65 +726,31 @@ __device__ __forceinline__ void sep_task(const KArgs& a, const WaveTask& t, cons
   band_margins<C, EXP ? 3 : C>(a, t);
 }
 
-// Separable filter kernel.  MODE (KMode) picks how waves get their tasks:
-//   kOneTask   one band of one tile column per wave (the hardware dispatcher
-//              refills the CUs as workgroups retire);
-//   kTailBands the same, but range 0 ends in short bands (KArgs::tail_y):
-//              the workgroups dispatched last carry the short tasks, so the
-//              launch's tail is one short task long;
-//   kQueue     a grid of the resident workgroups claiming tasks from the work
-//              queue (KArgs::queue) until none is left;
-//   kQuad      one task per wave, a workgroup = 4 stacked bands of one tile
-//              column in alternating directions (quad_task);
-//   kRuns      one task per wave, XCD-local runs of bands in alternating
-//              directions (runs_task).
-// STAMP: the per-wave timeline of KArgs::stamps (diagnostic instances,
-// tools/sepx.hip).  Both are compile-time, so the one-task instances carry
-// neither the loop nor the stamp code.  NW: waves per workgroup (one-task
-// mode; the engine launches kWaves: one- and two-wave workgroups at the same
-// waves per CU were 4-7 % slower on the cold share and the 16K frame,
-// tools/sepx.hip `wg` sweep, profiles/r5/cold/sepx_wg_*.txt).
+// Separable filter kernel.  MODE picks how waves get their tasks:
+//   kOneTask  one band of one tile column per wave (the hardware dispatcher
+//             refills the CUs as workgroups retire);
+//   kRuns     one task per wave, XCD-local runs of bands in alternating
+//             directions (runs_task; PassLaunch::order = 1).
+// Round 5's other task modes (tail bands, a persistent work queue, stacked
+// bands per workgroup) and the per-wave timeline were measured slower and
+// live in tools/sepx_modes.h with the study that measured them.  4-wave
+// workgroups: one- and two-wave workgroups at the same waves per CU were
+// 4-7 % slower (profiles/r5/cold/sepx_wg_*.txt).
 // (skip border + expand epilogue, a rare combination: 2 VGPRs over the 128 of
 // 4 waves/SIMD with the gray prologue -> 3 waves rather than a scratch spill)
-enum KMode { kOneTask = 0, kTailBands = 1, kQueue = 2, kQuad = 3, kRuns = 4 };
-template <int C, class F, int PRO, bool SKIP, int SAUX, bool EXP = false, int MODE = kOneTask, bool STAMP = false,
-          int NW = kWaves>
-__global__ __launch_bounds__(NW * kW, (F::K >= 7 ? 2 : (SKIP && EXP ? 3 : 4))) void k_sep(KArgs a) {
-  constexpr bool PERSIST = MODE == kQueue;
-  static_assert(NW == kWaves || MODE == kOneTask, "task modes assume kWaves-wave workgroups");
-  static_assert(MODE != kQuad || kWaves == 4, "kQuad: one band per wave of a 4-wave workgroup");
-  static_assert((MODE != kQuad && MODE != kRuns) || SepTraits<F>::SYM, "a bottom-up band needs symmetric vertical taps");
-  const uint32_t t_start = STAMP ? stamp_now() : 0u;
-  __shared__ __attribute__((aligned(16))) uint4 xbuf[EXP ? NW : 1][EXP ? 3 * kW : 1];
+enum KMode { kOneTask = 0, kRuns = 4 };
+template <int C, class F, int PRO, bool SKIP, int SAUX, bool EXP = false, int MODE = kOneTask>
+__global__ __launch_bounds__(kNT, (F::K >= 7 ? 2 : (SKIP && EXP ? 3 : 4))) void k_sep(KArgs a) {
+  static_assert(MODE == kOneTask || MODE == kRuns, "k_sep task modes: kOneTask, kRuns");
+  static_assert(MODE != kRuns || SepTraits<F>::SYM, "a bottom-up band needs symmetric vertical taps");
+  __shared__ __attribute__((aligned(16))) uint4 xbuf[EXP ? kWaves : 1][EXP ? 3 * kW : 1];
   __shared__ uint8_t luts[768];
   if (PRO != PRO_NONE || a.has_epi) {
     load_luts<PRO>(a, luts);
     __syncthreads();
   }
-  if constexpr (PERSIST) {
-    const int nw = (int)gridDim.x * kWaves;
-    const int shard = (int)(blockIdx.x % kQueueShards);
-    uint32_t* head = a.queue + shard * kQueueLine;
-    int task = (int)blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // static round 0
-    while (task < a.persist_tasks) {
-      const uint32_t next = queue_claim_async(head);  // in flight while this task streams
-      const WaveTask t = task_at<true>(a, task);
-      if (t.valid) sep_task<C, F, PRO, SKIP, SAUX, EXP>(a, t, luts, xbuf[EXP ? t.wave : 0]);
-      task = nw + kQueueShards * (int)__builtin_amdgcn_readfirstlane(next) + shard;
-    }
-    queue_retire(a.queue, shard);
-  } else if constexpr (MODE == kQuad || MODE == kRuns) {
-    const WaveTask t = MODE == kQuad ? quad_task(a) : runs_task(a);
-    if (t.valid) sep_task<C, F, PRO, SKIP, SAUX, EXP>(a, t, luts, xbuf[EXP ? t.wave : 0]);
-  } else if constexpr (MODE == kTailBands) {
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const WaveTask t = task_at<true>(a, xcd_remap((int)blockIdx.x, (int)gridDim.x, a.nxcd) * kWaves + wave);
-    if (t.valid) sep_task<C, F, PRO, SKIP, SAUX, EXP>(a, t, luts, xbuf[EXP ? t.wave : 0]);
-  } else {
-    const WaveTask t = wave_task<NW>(a);
-    if (t.valid) sep_task<C, F, PRO, SKIP, SAUX, EXP>(a, t, luts, xbuf[EXP ? t.wave : 0]);
-  }
-  if constexpr (STAMP) stamp_wave(a.stamps, (int)blockIdx.x * NW + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), t_start);
+  const WaveTask t = MODE == kRuns ? runs_task(a) : wave_task(a);
+  if (t.valid) sep_task<C, F, PRO, SKIP, SAUX, EXP>(a, t, luts, xbuf[EXP ? t.wave : 0]);
 }
 
 // ------------------------------------------------------------------------------
@@ -1206,53 +1095,6 @@ inline void plan_bands(KArgs& a, dim3& grid, int tiles, int n0, int n1, int band
   a.nbands = a.nb0 + (int)div_up(n1, band);
   a.ntx = tiles;
   grid = dim3((unsigned)div_up((int64_t)tiles * a.nbands, kWaves));
-}
-
-// Persistent launch geometry (after plan_bands): a grid of the resident
-// workgroups of `fn` at dynamic LDS `dyn` (the occupancy cap), and range 0's
-// last rows re-cut into tail_band-row bands, one tail task per resident wave,
-// so the tasks claimed last are short (tail_band <= 0 or >= band: no tail).
-inline int resident_wgs(const void* fn, size_t dyn) {
-  int per_cu = 0, cus = 0, dev = 0;
-  HIP_CHECK(hipGetDevice(&dev));
-  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kNT, dyn));
-  HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  return std::max(1, per_cu) * std::max(1, cus);
-}
-
-// Re-cut range 0's last rows into tail_band-row bands, one tail task per
-// resident wave (`waves`), and recount the bands (KArgs::tail_y; kTailBands /
-// kQueue kernels).  tail_band <= 0 or >= band: no tail.
-inline void set_tail_bands(KArgs& a, int tail_band, int waves) {
-  const int n0 = a.ry1 - a.ry0;
-  const int n1 = a.ry3 - a.ry2;
-  int tail_rows = 0;
-  if (tail_band > 0 && tail_band < a.band) {
-    tail_rows = (int)std::min<int64_t>(div_up((int64_t)waves, a.ntx) * tail_band, n0 / 2);
-    tail_rows -= tail_rows % tail_band;
-  }
-  a.tail_band = tail_rows > 0 ? tail_band : a.band;
-  a.tail_y = a.ry1 - tail_rows;
-  a.nbig = (int)div_up(a.tail_y - a.ry0, a.band);
-  a.nb0 = a.nbig + (int)div_up(tail_rows, a.tail_band);
-  a.nbands = a.nb0 + (int)div_up(n1, a.band);
-}
-
-// One-task launch with tail bands (kTailBands): the grid covers every task.
-inline void plan_tail(KArgs& a, dim3& grid, const void* fn, size_t dyn, int tail_band) {
-  set_tail_bands(a, tail_band, resident_wgs(fn, dyn) * kWaves);
-  grid = dim3((unsigned)div_up((int64_t)a.ntx * a.nbands, kWaves));
-}
-
-inline void plan_persistent(KArgs& a, dim3& grid, const void* fn, size_t dyn, int tail_band) {
-  const int wgs = resident_wgs(fn, dyn);
-  set_tail_bands(a, tail_band, wgs * kWaves);
-  a.persist_tasks = a.ntx * a.nbands;
-  a.nxcd = 0;
-  int64_t g = std::max<int64_t>(1, std::min<int64_t>(wgs, div_up(a.persist_tasks, kWaves)));
-  // tasks past round 0 are claimed per queue class: every class needs a workgroup
-  if (a.persist_tasks > g * kWaves) g = std::max<int64_t>(g, kQueueShards);
-  grid = dim3((unsigned)g);
 }
 
 // Occupancy cap of the HBM-streaming (nt-store) stencil launches: fewer

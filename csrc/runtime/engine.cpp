@@ -504,6 +504,19 @@ void Engine::exchange_halo(uint8_t* org, int C, int R, hipStream_t s) {
   fault_point("halo", rank_);
   STRIPE_CHECK(!self_halo_ || R <= st.rows, "self-halo of " << R << " rows needs a stripe of at least that many rows");
   if (time_halo_) stage_begin(Stage::Halo, s);
+  // STRIPE_SELF_HALO_COPY=1 (A/B): the self-halo rows move by two device copy
+  // launches instead of RCCL, separating RCCL's own cost from the exchange's
+  // place in the schedule
+  static const bool self_copy = [] {
+    const char* e = std::getenv("STRIPE_SELF_HALO_COPY");
+    return e && std::atoi(e) != 0;
+  }();
+  if (self_halo_ && self_copy) {
+    launch_copy_rows(base - (int64_t)R * P, P, base + (int64_t)(st.rows - R) * P, P, P, R, s);
+    launch_copy_rows(base + (int64_t)st.rows * P, P, base, P, P, R, s);
+    if (time_halo_) stage_end(Stage::Halo, s);
+    return;
+  }
   comm_->group_start();
   if (self_halo_) {
     // the rank is its own upper and lower neighbour: the same two sends and

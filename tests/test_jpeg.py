@@ -7,6 +7,7 @@ IDCT, float YCbCr) stays within 3 levels of libjpeg-turbo's integer path, with
 a mean difference well under 0.1 level.
 """
 import io
+import json
 import os
 import subprocess
 import sys
@@ -414,7 +415,10 @@ def test_long_scan_speculative_decode_is_exact(C, shape, subsampling):
     assert part.shape == ours.shape and np.array_equal(part[:rows], ours[:rows])
 
 
-# ---- round 5: vectorised colour / planes kernels are bit-identical to the per-pixel forms ----
+# ---- the device pixel stages (k_jpeg_idct8, k_jpeg_color16, k_jpeg_planes16)
+# against the host codec, over 4:4:4 / 4:2:2 / 4:2:0 / gray, widths that are and
+# are not multiples of 16, a 1x1 frame (the per-pixel / per-block kernels they
+# replaced in round 5 were removed in round 6) ----
 _COLOR_WORKER = r'''
 import io, os, sys, json
 import numpy as np
@@ -424,7 +428,6 @@ import mpi_cuda_imagemanipulation_amd as m
 from mpi_cuda_imagemanipulation_amd._native import C
 from PIL import Image
 out = os.environ["OUT"]
-res = {}
 def smooth(h, w, c, seed):
     rng = np.random.default_rng(seed)
     y, x = np.mgrid[0:h, 0:w]
@@ -432,6 +435,7 @@ def smooth(h, w, c, seed):
     img = np.clip(base + rng.normal(0, 6.0, base.shape), 0, 255).astype(np.uint8)
     return img[..., 0] if c == 1 else img
 k = 0
+worst = {"decode": 0, "encode": 0}
 for (h, w, c) in [(211, 157, 3), (96, 512, 3), (61, 1000, 3), (64, 99, 1), (48, 256, 1), (1, 1, 3), (17, 33, 3)]:
     for sub in ([0, 1, 2] if c == 3 else [None]):
         img = smooth(h, w, c, k)
@@ -439,46 +443,30 @@ for (h, w, c) in [(211, 157, 3), (96, 512, 3), (61, 1000, 3), (64, 99, 1), (48, 
         Image.fromarray(img).save(b, "JPEG", quality=90, **({"subsampling": sub} if sub is not None else {}))
         p = os.path.join(out, f"in{k}.jpg")
         open(p, "wb").write(b.getvalue())
-        dec = m.utils.read_image_device(p).cpu().numpy()
-        np.save(os.path.join(out, f"dec{k}_{os.environ['TAG']}.npy"), dec)
-        q = os.path.join(out, f"enc{k}_{os.environ['TAG']}.jpg")
+        dev = m.utils.read_image_device(p).cpu().numpy()
+        host = C.decode_jpeg(b.getvalue())
+        assert dev.shape == host.shape, (k, dev.shape, host.shape)
+        worst["decode"] = max(worst["decode"], int(np.abs(dev.astype(int) - host.astype(int)).max()))
+        q = os.path.join(out, f"enc{k}.jpg")
         m.utils.write_image_device(q, torch.from_numpy(img).cuda(), quality=90)
+        back = C.decode_jpeg(open(q, "rb").read())
+        ref = C.decode_jpeg(C.encode_jpeg(img, 90, True, -1))
+        assert back.shape == ref.shape, k
+        worst["encode"] = max(worst["encode"], int(np.abs(back.astype(int) - ref.astype(int)).max()))
         k += 1
-print("DONE", k)
+print("RESULT", json.dumps(dict(worst, n=k)))
 '''
 
 
 @pytest.mark.gpu
-def test_vectorised_color_and_planes_match_per_pixel_kernels(tmp_path):
-    # k_jpeg_color16 / k_jpeg_planes16 (16 samples per lane, wide loads and
-    # stores) against the per-pixel kernels they replace (STRIPE_JPEG_COLOR=1):
-    # decoded pixels and encoded files byte for byte, over 4:4:4 / 4:2:2 /
-    # 4:2:0 / gray, widths that are and are not multiples of 16, a 1x1 frame
+def test_device_pixel_stages_match_host_codec(tmp_path):
+    # device decode within one level of the host decode (float IDCT / colour
+    # rounding of ties), device encode decoding within a few levels of the host
+    # encoder's file
     script = tmp_path / "w.py"
     script.write_text(_COLOR_WORKER)
-    for tag, legacy in (("new", "0"), ("old", "1")):
-        env = dict(os.environ, STRIPE_ROOT=ROOT, OUT=str(tmp_path), TAG=tag, STRIPE_JPEG_COLOR=legacy)
-        r = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=300)
-        assert r.returncode == 0 and "DONE" in r.stdout, (r.stdout + r.stderr)[-3000:]
-    n = int([ln for ln in r.stdout.splitlines() if ln.startswith("DONE")][0].split()[1])
-    for k in range(n):
-        a, b = np.load(tmp_path / f"dec{k}_new.npy"), np.load(tmp_path / f"dec{k}_old.npy")
-        assert a.shape == b.shape and np.array_equal(a, b), k
-        assert (tmp_path / f"enc{k}_new.jpg").read_bytes() == (tmp_path / f"enc{k}_old.jpg").read_bytes(), k
-
-
-@pytest.mark.gpu
-def test_row_idct_matches_per_block_kernel(tmp_path):
-    # k_jpeg_idct8 (a lane per block row, 8-byte row stores) against the
-    # per-block IDCT it replaces (STRIPE_JPEG_IDCT=1): same sums in the same
-    # order, so decoded pixels must be bit-identical over every sampling mode
-    script = tmp_path / "w.py"
-    script.write_text(_COLOR_WORKER)
-    for tag, legacy in (("new", "0"), ("old", "1")):
-        env = dict(os.environ, STRIPE_ROOT=ROOT, OUT=str(tmp_path), TAG=tag, STRIPE_JPEG_IDCT=legacy)
-        r = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=300)
-        assert r.returncode == 0 and "DONE" in r.stdout, (r.stdout + r.stderr)[-3000:]
-    n = int([ln for ln in r.stdout.splitlines() if ln.startswith("DONE")][0].split()[1])
-    for k in range(n):
-        a, b = np.load(tmp_path / f"dec{k}_new.npy"), np.load(tmp_path / f"dec{k}_old.npy")
-        assert a.shape == b.shape and np.array_equal(a, b), k
+    env = dict(os.environ, STRIPE_ROOT=ROOT, OUT=str(tmp_path))
+    r = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "RESULT" in r.stdout, (r.stdout + r.stderr)[-3000:]
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("RESULT")][0][len("RESULT "):])
+    assert res["n"] == 17 and res["decode"] <= 1 and res["encode"] <= 3, res

@@ -3,7 +3,7 @@
 // time go, and which launch shape / store policy gets closest to a plain copy
 // of the same bytes?  (profiles/r5/cold/README.md)
 //
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Icsrc/include -Icsrc/hip \
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Icsrc/include -Icsrc/hip -Itools \
 //         -o bin/sepx tools/sepx.hip
 //   bin/sepx [rows] [frames] [stamp_csv_prefix] [sweep: tail | policy | sobel | wg | quad | sobelquad | runs | fetch |
 //             pattern | pitch (SEPX_PAD=bytes added to the row pitch)]
@@ -15,12 +15,13 @@
 // and frames alternating over two streams): what the headline's host clock
 // sees.  Kernel-only times come from rocprofv3 over the same binary.
 //
-// Variants (k_sep<3, Gaussian5, ...> of csrc/hip/stencil_kernels.h): store
+// Variants (k_sepx<3, Gaussian5, ...> of tools/sepx_modes.h, the production
+// k_sep's per-wave body under every task mode): store
 // policy aux 0 (default), 2 (nt), 16 (sc1 write-through), 18 (sc1 nt); band
 // height x occupancy cap x workgroup order (XCD remap); the task mode
 // (kOneTask, kTailBands, kQueue); waves per workgroup (`wg`: 1, 2 or 4 with
 // the occupancy cap held in waves per CU); a linear copy of the same bytes as
-// the floor.  Then per-wave stamps (KArgs::stamps) of one cold dispatch of chosen
+// the floor.  Then per-wave stamps (SepxArgs::stamps) of one cold dispatch of chosen
 // variants: start / end spread and wave lifetime, written as CSV.
 #include <algorithm>
 #include <cstdio>
@@ -29,7 +30,7 @@
 #include <string>
 #include <vector>
 
-#include "stencil_kernels.h"
+#include "sepx_modes.h"
 
 using namespace stripe;
 using namespace stripe::dev;
@@ -58,7 +59,7 @@ __global__ __launch_bounds__(256) void k_copy_lin(const uint8_t* in, uint8_t* ou
 // mapping, same store policy: the difference to k_sep is the compute, the
 // difference to the linear copy is the pattern.
 template <int R>
-__global__ __launch_bounds__(256) void k_band_copy(KArgs a) {
+__global__ __launch_bounds__(256) void k_band_copy(SepxArgs a) {
   const WaveTask t = wave_task(a);
   if (!t.valid) return;
   const int lane = t.lane;
@@ -144,11 +145,11 @@ static int g_W = 16384, g_C = 3, g_rows = 2048, g_out_px = 0;
 static int64_t g_pitch = 0, g_bytes = 0, g_org = 0;
 static std::vector<Frame> g_frames;
 
-using SepFn = void (*)(KArgs);
+using SepFn = void (*)(SepxArgs);
 static bool g_sobel = false;  // the filter: gaussian5 on RGB (default) or sobel on gray
 template <int C, class Flt, int SAUX, int MODE>
 static SepFn sep_fn_mode(bool stamp) {
-  return stamp ? k_sep<C, Flt, PRO_NONE, false, SAUX, false, MODE, true> : k_sep<C, Flt, PRO_NONE, false, SAUX, false, MODE>;
+  return stamp ? k_sepx<C, Flt, PRO_NONE, false, SAUX, false, MODE, true> : k_sepx<C, Flt, PRO_NONE, false, SAUX, false, MODE>;
 }
 template <int C, class Flt, int SAUX>
 static SepFn sep_fn_aux(int mode, bool stamp) {
@@ -170,8 +171,8 @@ static SepFn sep_fn_flt(int saux, int mode, bool stamp) {
 // gaussian5, nt stores, one task per wave, NW waves per workgroup
 template <int NW>
 static SepFn sep_fn_nw(bool stamp) {
-  return stamp ? k_sep<3, sdef::Gaussian5, PRO_NONE, false, 2, false, kOneTask, true, NW>
-               : k_sep<3, sdef::Gaussian5, PRO_NONE, false, 2, false, kOneTask, false, NW>;
+  return stamp ? k_sepx<3, sdef::Gaussian5, PRO_NONE, false, 2, false, kOneTask, true, NW>
+               : k_sepx<3, sdef::Gaussian5, PRO_NONE, false, 2, false, kOneTask, false, NW>;
 }
 static SepFn sep_fn(int saux, int mode, bool stamp, int nw) {
   if (nw == 1) return sep_fn_nw<1>(stamp);
@@ -193,7 +194,7 @@ struct SepCfg {
 
 static void launch_sep(const SepCfg& c, const Frame& f, hipStream_t s, uint32_t* stamps = nullptr,
                        int* grid_out = nullptr) {
-  KArgs a{};
+  SepxArgs a{};
   a.in = f.in + g_org;
   a.out = f.out + g_org;
   a.in_pitch = a.out_pitch = g_pitch;
