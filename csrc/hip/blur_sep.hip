@@ -162,13 +162,21 @@ struct PlGeom {
 // within 1 LSB of the f64 result (the host bounds the error per weight set and
 // keeps the exact kernel when it cannot promise that).
 // (launch bounds: OCC waves per SIMD = OCC * 256 / THREADS workgroups per CU)
-template <int C, bool EDGE, int NX_, int PFD, int OCC, bool LSB = false, int NW = 1, bool EARLY = true>
+// SCHED (A/B, STRIPE_BLUR_SCHED): bit 0 -- the younger half of an 8-wave
+// workgroup (waves 4-7) runs at priority 1 for the whole kernel (it otherwise
+// loses every issue arbitration to the older half on its SIMD); bit 1 -- every
+// wave raises its priority over its step's tile loop (the MFMAs) and drops it
+// for the staging / barrier part.
+template <int C, bool EDGE, int NX_, int PFD, int OCC, bool LSB = false, int NW = 1, bool EARLY = true, int SCHED = 0>
 __global__ __launch_bounds__(blur_threads(NW), OCC * 256 / blur_threads(NW)) void k_blur_pl(SepArgs sa) {
   using G = PlGeom<C, NX_, NW>;
   constexpr int NX = G::NX;
   const KArgs& a = sa.a;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if constexpr ((SCHED & 1) && NW == 8) {
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);  // wave-uniform (readfirstlane): a scalar branch
+  }
   const int sl = NW == 1 ? lane : (int)threadIdx.x;  // staging lane
   int strip, by, sgx;  // strip of this wave, band, first strip of the staged window
   if constexpr (NW == 1) {
@@ -456,6 +464,7 @@ __global__ __launch_bounds__(blur_threads(NW), OCC * 256 / blur_threads(NW)) voi
     };
     half8 F[2][2][2];
     f4 X[2][2];
+    if constexpr (SCHED & 2) __builtin_amdgcn_s_setprio(2);
     hread(0, F[0]);
     if (T > 1) hread(1, F[1]);
     hmfma(F[0], X[0]);
@@ -468,6 +477,10 @@ __global__ __launch_bounds__(blur_threads(NW), OCC * 256 / blur_threads(NW)) voi
         if (t == (T > 1 ? 1 : 0) && k + 1 <= ngroups)
           stage(std::integral_constant<int, 1 - decltype(buf_c)::value>{}, wl + ((k + 1) & 1) * G::TILE);
       }
+    }
+    if constexpr (SCHED & 2) {
+      if ((SCHED & 1) && NW == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
     }
     if constexpr (NW == 1) sep_lds_sync();  // fragment reads done before the next pair overwrites the planes
   };
@@ -678,22 +691,29 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
   // A/B variants of the RGB non-edge kernel (STRIPE_BLUR_VARIANT=n): 1 = two
   // independent 4-wave workgroups per CU (NW 4, two pairs in flight), 2 = the
   // same with one pair in flight, 3 = the 8-wave windows staging each pair
-  // between the barrier and the MFMAs (round 4's default, EARLY = false).
+  // between the barrier and the MFMAs (round 4's default, EARLY = false),
+  // 4 / 5 / 6 = the default with wave priorities (k_blur_pl SCHED 1 / 2 / 3).
   // (Three pairs in flight, lsb, 254 registers: 0.376 vs 0.354 ms on 16K,
   // 0.047 vs 0.042 on the stripe, profiles/r5/blur/pfd3_*.txt: removed.)
 #define STRIPE_BLUR_LATE(LSB)                                                                        \
   Cfg { 2, 2, 8, dev::k_blur_pl<3, false, 2, 2, 2, LSB, 8, false>, (size_t)dev::PlGeom<3, 2, 8>::LDS }
-  static const Cfg variants[2][4] = {
+  // 4-6: the default shape with wave priorities (k_blur_pl SCHED 1-3)
+#define STRIPE_BLUR_PRIO(LSB, SC)                                                                    \
+  Cfg { 2, 2, 8, dev::k_blur_pl<3, false, 2, 2, 2, LSB, 8, true, SC>, (size_t)dev::PlGeom<3, 2, 8>::LDS }
+  static const Cfg variants[2][7] = {
       {STRIPE_BLUR_CFGW(3, false, 2, 2, 2, false, 8), STRIPE_BLUR_CFGW(3, false, 2, 2, 2, false, 4),
-       STRIPE_BLUR_CFGW(3, false, 2, 1, 2, false, 4), STRIPE_BLUR_LATE(false)},
+       STRIPE_BLUR_CFGW(3, false, 2, 1, 2, false, 4), STRIPE_BLUR_LATE(false), STRIPE_BLUR_PRIO(false, 1),
+       STRIPE_BLUR_PRIO(false, 2), STRIPE_BLUR_PRIO(false, 3)},
       {STRIPE_BLUR_CFGW(3, false, 2, 2, 2, true, 8), STRIPE_BLUR_CFGW(3, false, 2, 2, 2, true, 4),
-       STRIPE_BLUR_CFGW(3, false, 2, 1, 2, true, 4), STRIPE_BLUR_LATE(true)}};
+       STRIPE_BLUR_CFGW(3, false, 2, 1, 2, true, 4), STRIPE_BLUR_LATE(true), STRIPE_BLUR_PRIO(true, 1),
+       STRIPE_BLUR_PRIO(true, 2), STRIPE_BLUR_PRIO(true, 3)}};
 #undef STRIPE_BLUR_LATE
+#undef STRIPE_BLUR_PRIO
   static const int env_variant = [] {
     const char* e = std::getenv("STRIPE_BLUR_VARIANT");
     return e ? std::atoi(e) : 0;
   }();
-  const Cfg& cf = (p.cmid == 3 && !edge && env_variant > 0 && env_variant < 4) ? variants[lsb][env_variant]
+  const Cfg& cf = (p.cmid == 3 && !edge && env_variant > 0 && env_variant < 7) ? variants[lsb][env_variant]
                                                                                : cfgs[lsb][p.cmid == 3][edge];
 #undef STRIPE_BLUR_CFG
 #undef STRIPE_BLUR_CFGW

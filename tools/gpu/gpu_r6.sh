@@ -7,6 +7,11 @@
 #             without and with the self-halo exchange (RCCL loopback every
 #             step), non-blocking vs blocking communicators, RCCL's workgroups
 #             capped; a kernel trace of the self-halo share       -> r6/selfhalo
+#   batch1    GPU tests of round 6's changes; the self-halo share under RCCL
+#             protocol / channel settings and with the exchange as plain
+#             device copies (STRIPE_SELF_HALO_COPY); blur:31 wave-priority
+#             variants and conv:31 k-loop scheduling variants (A/B,
+#             alternating), each variant's numerics checked first   -> r6/batch1
 # Every GPU step runs under its own timeout; a failing step ends the script.
 set -o pipefail
 S=${1:?study}
@@ -29,6 +34,27 @@ selfhalo)
   cd /tmp
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_self -o run -- python3 $R/bench.py $SHARE --steps 50 --self-halo > $O/prof_self.json 2> $O/prof_self.err || exit 4
   python3 $R/tools/prof_summary.py $O/prof_self/run_results.db > $O/rocprof_self.txt 2>&1 || true
+  ;;
+batch1)
+  timeout -k 10 900 python -u -m pytest tests/test_r6_selfhalo.py tests/test_r6_advice.py tests/test_r5_order.py tests/test_oracle_conv.py tests/test_jpeg.py tests/test_gpu_kernels.py -m gpu -q -x --timeout 200 --timeout-method thread > $O/tests.txt 2>&1 || exit 2
+  STRIPE_CONV_SCHED=3 STRIPE_BLUR_VARIANT=6 timeout -k 10 600 python -u -m pytest tests/test_oracle_conv.py -m gpu -q -x -k "gpu_conv or gpu_blur" --timeout 200 --timeout-method thread > $O/tests_sched3.txt 2>&1 || exit 2
+  STRIPE_CONV_SCHED=1 STRIPE_BLUR_VARIANT=4 timeout -k 10 600 python -u -m pytest tests/test_oracle_conv.py -m gpu -q -x -k "gpu_conv or gpu_blur" --timeout 200 --timeout-method thread > $O/tests_sched1.txt 2>&1 || exit 2
+  timeout -k 10 300 python bench.py $SHARE > $O/share_plain.json 2> $O/share_plain.err || exit 3
+  for v in default ll copy ch1 ch4 default; do
+    case $v in default) E="" ;; ll) E="NCCL_P2P_LL_THRESHOLD=1048576" ;; copy) E="STRIPE_SELF_HALO_COPY=1" ;;
+      ch1) E="NCCL_NCHANNELS_PER_PEER=1" ;; ch4) E="NCCL_NCHANNELS_PER_PEER=4" ;; esac
+    env $E timeout -k 10 300 python bench.py $SHARE --self-halo >> $O/share_self_$v.json 2>> $O/share_self_$v.err || exit 3
+  done
+  C31="$(python3 -c "print('conv:31:' + ';'.join(str(((i*7)%13-4)/400.0) for i in range(961)))")"
+  for r in 1 2; do
+    for v in 0 4 5 6; do
+      STRIPE_BLUR_VARIANT=$v timeout -k 10 120 python tools/kbench.py --chains "blur:31|blur:31:lsb" --shape 16384x16384x3 --iters 30 >> $O/blur_v${v}_16k.txt 2>&1 || exit 4
+      STRIPE_BLUR_VARIANT=$v timeout -k 10 120 python tools/kbench.py --chains "blur:31|blur:31:lsb" --shape 16384x2048x3 --iters 60 >> $O/blur_v${v}_stripe.txt 2>&1 || exit 4
+    done
+    for v in 0 1 2 3; do
+      STRIPE_CONV_SCHED=$v timeout -k 10 200 python tools/kbench.py --chains "$C31|$C31:lsb" --shape 16384x16384x3 --iters 30 >> $O/conv_s${v}_16k.txt 2>&1 || exit 5
+    done
+  done
   ;;
 *)
   echo "unknown study $S" >&2
