@@ -338,6 +338,38 @@ CopyRoofline copy_roofline(int device, int64_t bytes, int frames, int reps) {
   return r;
 }
 
+namespace dev {
+struct CopyMultiArgs {
+  CopyDesc d[kCopyMultiMax];
+};
+// blockIdx.y: the copy; 16-byte chunks when both ends are 16-byte aligned
+__global__ __launch_bounds__(kNT) void k_copy_multi(CopyMultiArgs a) {
+  const CopyDesc c = a.d[blockIdx.y];
+  const bool al = ((uintptr_t)c.src % 16 == 0) && ((uintptr_t)c.dst % 16 == 0);
+  const int64_t n16 = al ? c.bytes / 16 : 0;
+  for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n16; i += (int64_t)gridDim.x * kNT)
+    reinterpret_cast<uint4*>(c.dst)[i] = reinterpret_cast<const uint4*>(c.src)[i];
+  for (int64_t b = 16 * n16 + (int64_t)blockIdx.x * kNT + threadIdx.x; b < c.bytes; b += (int64_t)gridDim.x * kNT)
+    c.dst[b] = c.src[b];
+}
+}  // namespace dev
+
+void launch_copy_multi(const CopyDesc* d, int n, hipStream_t s) {
+  for (int k = 0; k < n; k += kCopyMultiMax) {
+    dev::CopyMultiArgs a{};
+    const int m = std::min(kCopyMultiMax, n - k);
+    int64_t big = 0;
+    for (int i = 0; i < m; ++i) {
+      a.d[i] = d[k + i];
+      big = std::max(big, d[k + i].bytes);
+    }
+    if (big <= 0) continue;
+    const unsigned gx = (unsigned)std::min<int64_t>(div_up(big, 16 * dev::kNT), 64);
+    dev::k_copy_multi<<<dim3(gx, (unsigned)m), dev::kNT, 0, s>>>(a);
+    HIP_CHECK(hipGetLastError());
+  }
+}
+
 void launch_copy_rows(uint8_t* dst, int64_t dpitch, const uint8_t* src, int64_t spitch, int64_t E, int rows,
                       hipStream_t s) {
   if (rows <= 0 || E <= 0) return;

@@ -52,6 +52,17 @@ class Comm {
   virtual std::vector<std::pair<std::string, double>> identity() const {
     return {{"rank", (double)rank()}, {"size", (double)size()}};
   }
+  // One halo exchange of an active rank with its neighbours, all `participants`
+  // active ranks (0 .. participants - 1) calling it for the same exchange:
+  // send_up -> rank - 1's recv_down, send_down -> rank + 1's recv_up, `bytes`
+  // each way, ordered on stream `s` (nullptr pointers: no neighbour on that
+  // side).  Returns false when the backend has no collective form; the caller
+  // then posts the grouped sends and receives.
+  virtual bool exchange_rows(int participants, const void* send_up, void* recv_up, const void* send_down,
+                             void* recv_down, size_t bytes, hipStream_t s) {
+    (void)participants, (void)send_up, (void)recv_up, (void)send_down, (void)recv_down, (void)bytes, (void)s;
+    return false;
+  }
 };
 
 // ---- RCCL ----

@@ -88,6 +88,16 @@ void launch_fill_margins(uint8_t* origin, int64_t pitch, int W, int C, int y0, i
 void launch_copy_rows(uint8_t* dst, int64_t dpitch, const uint8_t* src, int64_t spitch, int64_t E, int rows,
                       hipStream_t s);
 
+// Up to kCopyMultiMax independent device copies in one launch (the `local`
+// hub's halo rounds: every rank's halo rows of one exchange).
+constexpr int kCopyMultiMax = 16;
+struct CopyDesc {
+  const uint8_t* src = nullptr;
+  uint8_t* dst = nullptr;
+  int64_t bytes = 0;
+};
+void launch_copy_multi(const CopyDesc* d, int n, hipStream_t s);
+
 // Same-box streaming floor: a hand-written linear device copy of `bytes`
 // (csrc/hip/pointwise.hip k_copy_linear) rotating over `frames` buffer pairs
 // (frames x 2 x bytes > 2 x 256 MiB: every copy reads cache-cold data), the

@@ -8,6 +8,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -95,6 +96,119 @@ class LocalHub {
     changed();
   }
 
+  // ---- halo rounds (device hubs, Comm::exchange_rows) ----
+  // Every active rank posts its exchange (its halo row pointers and a `ready`
+  // event recorded on its stream); the last to arrive issues the whole
+  // exchange on its own stream -- a wait on every rank's `ready`, every
+  // rank's halo rows in one multi-copy launch, one `done` event -- and every
+  // rank's stream waits on `done`.  3 N + 2 HIP calls per exchange instead of
+  // ~9 N from N threads contending for the runtime (profiles/r6/local/).
+  struct RoundPost {
+    int rank = 0;
+    const void* su = nullptr;
+    void* ru = nullptr;
+    const void* sd = nullptr;
+    void* rd = nullptr;
+    size_t bytes = 0;
+    hipEvent_t ready = nullptr;
+    int dev = 0;
+  };
+  void halo_round(const RoundPost& p, int n, hipStream_t s) {
+    std::unique_lock<std::mutex> lk(mu_);
+    if (aborted_) fail("communicator aborted (" + abort_msg_ + ") before a halo exchange");
+    const long id = open_round_;
+    Round& r = rounds_[id];
+    r.posts.push_back(p);
+    if ((int)r.posts.size() == n) {
+      ++open_round_;  // later arrivals start the next round
+      const std::vector<RoundPost> posts = r.posts;
+      hipEvent_t done = nullptr;
+      auto& pool = done_pool_[p.dev];
+      if (!pool.empty()) {
+        done = pool.back();
+        pool.pop_back();
+      }
+      lk.unlock();
+      std::string err;
+      try {
+        if (!done) HIP_CHECK(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+        issue_round(posts, p.rank, p.dev, done, s);
+      } catch (const std::exception& e) {
+        err = e.what();
+      }
+      lk.lock();
+      r.done = done;
+      r.dev = p.dev;
+      r.issued = true;
+      if (!err.empty()) {
+        if (!aborted_) abort_msg_ = "halo round: " + err;
+        aborted_ = true;
+      }
+      changed();
+      if (!err.empty()) fail("local comm " + abort_msg_);
+    } else {
+      wait(lk, [&] { return r.issued; }, "halo exchange of " + std::to_string(n) + " ranks");
+      if (aborted_) fail("communicator aborted (" + abort_msg_ + ") during a halo exchange");
+    }
+    hipEvent_t done = r.done;
+    lk.unlock();
+    const hipError_t we = hipStreamWaitEvent(s, done, 0);  // `done` may live on another device
+    lk.lock();
+    if (++r.waited == n) {  // every wait on `done` is enqueued: it may be recorded again
+      done_pool_[r.dev].push_back(r.done);
+      rounds_.erase(id);
+    }
+    lk.unlock();
+    HIP_CHECK(we);
+  }
+  ~LocalHub() {
+    for (auto& kv : done_pool_)
+      for (hipEvent_t e : kv.second) (void)hipEventDestroy(e);
+  }
+
+ private:
+  struct Round {
+    std::vector<RoundPost> posts;
+    hipEvent_t done = nullptr;
+    int dev = 0;
+    bool issued = false;
+    int waited = 0;
+  };
+  static void issue_round(const std::vector<RoundPost>& posts, int me, int dev, hipEvent_t done, hipStream_t s) {
+    std::map<int, const RoundPost*> by;
+    bool same = true;
+    for (const auto& q : posts) {
+      by[q.rank] = &q;
+      same &= q.dev == dev;
+    }
+    for (const auto& q : posts)
+      if (q.rank != me) HIP_CHECK(hipStreamWaitEvent(s, q.ready, 0));
+    std::vector<CopyDesc> cps;
+    std::vector<std::pair<int, int>> devs;  // (dst device, src device) per copy
+    auto add = [&](const RoundPost& q, void* dst, int src_rank, bool from_sd) {
+      auto it = by.find(src_rank);
+      STRIPE_CHECK(it != by.end(), "halo round: rank " << q.rank << " expects rows from rank " << src_rank
+                                                        << ", which is not in the exchange");
+      const RoundPost& o = *it->second;
+      const void* src = from_sd ? o.sd : o.su;
+      STRIPE_CHECK(src != nullptr && o.bytes == q.bytes,
+                   "halo round: rank " << src_rank << " sends no matching rows to rank " << q.rank);
+      cps.push_back(CopyDesc{static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), (int64_t)q.bytes});
+      devs.emplace_back(q.dev, o.dev);
+    };
+    for (const auto& q : posts) {
+      if (q.ru) add(q, q.ru, q.rank - 1, true);
+      if (q.rd) add(q, q.rd, q.rank + 1, false);
+    }
+    if (same) {
+      launch_copy_multi(cps.data(), (int)cps.size(), s);
+    } else {
+      for (size_t i = 0; i < cps.size(); ++i)
+        HIP_CHECK(hipMemcpyPeerAsync(cps[i].dst, devs[i].first, cps[i].src, devs[i].second, (size_t)cps[i].bytes, s));
+    }
+    HIP_CHECK(hipEventRecord(done, s));
+  }
+
  private:
   void changed() {  // under mu_
     ver_.fetch_add(1, std::memory_order_release);
@@ -134,6 +248,9 @@ class LocalHub {
   std::map<std::pair<int, int>, std::deque<std::shared_ptr<Msg>>> box_;
   int bar_count_ = 0;
   long bar_gen_ = 0;
+  std::map<long, Round> rounds_;
+  long open_round_ = 0;
+  std::map<int, std::vector<hipEvent_t>> done_pool_;  // recycled `done` events per device
   bool aborted_ = false;
   std::string abort_msg_;
 };
@@ -186,6 +303,36 @@ class LocalComm final : public Comm {
   }
   void barrier() override { hub_->barrier(); }
   void abort(const std::string& why) override { hub_->abort(why); }
+  bool exchange_rows(int participants, const void* send_up, void* recv_up, const void* send_down, void* recv_down,
+                     size_t bytes, hipStream_t s) override {
+    // STRIPE_LOCAL_ROUNDS=0: grouped sends / receives instead (A/B)
+    static const bool rounds = [] {
+      const char* e = std::getenv("STRIPE_LOCAL_ROUNDS");
+      return !(e && std::atoi(e) == 0);
+    }();
+    if (!rounds || !hub_->device() || participants <= 1) return false;
+    STRIPE_CHECK(!in_group_, "exchange_rows inside an open group");
+    LocalHub::RoundPost p;
+    p.rank = rank_;
+    p.su = send_up;
+    p.ru = recv_up;
+    p.sd = send_down;
+    p.rd = recv_down;
+    p.bytes = bytes;
+    p.ready = take_event();
+    try {
+      HIP_CHECK(hipGetDevice(&p.dev));
+      HIP_CHECK(hipEventRecord(p.ready, s));
+      hub_->halo_round(p, participants, s);
+    } catch (const std::exception& e) {
+      hub_->abort(std::string("rank ") + std::to_string(rank_) + ": " + e.what());
+      (void)hipEventDestroy(p.ready);
+      (void)hipGetLastError();
+      throw;
+    }
+    free_events_.push_back(p.ready);  // the issuer's wait on it is enqueued
+    return true;
+  }
   ~LocalComm() override {
     for (hipEvent_t e : free_events_) (void)hipEventDestroy(e);
   }

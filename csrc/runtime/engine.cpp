@@ -517,6 +517,15 @@ void Engine::exchange_halo(uint8_t* org, int C, int R, hipStream_t s) {
     if (time_halo_) stage_end(Stage::Halo, s);
     return;
   }
+  // a transport with a collective halo form (the in-process `local` hub: one
+  // thread issues every rank's copies)
+  if (!self_halo_ &&
+      comm_->exchange_rows(part_.active, up >= 0 ? base : nullptr, up >= 0 ? base - (int64_t)R * P : nullptr,
+                           down >= 0 ? base + (int64_t)(st.rows - R) * P : nullptr,
+                           down >= 0 ? base + (int64_t)st.rows * P : nullptr, bytes, s)) {
+    if (time_halo_) stage_end(Stage::Halo, s);
+    return;
+  }
   comm_->group_start();
   if (self_halo_) {
     // the rank is its own upper and lower neighbour: the same two sends and

@@ -12,6 +12,10 @@
 #             device copies (STRIPE_SELF_HALO_COPY); blur:31 wave-priority
 #             variants and conv:31 k-loop scheduling variants (A/B,
 #             alternating), each variant's numerics checked first   -> r6/batch1
+#   local     the `local` hub's halo rounds: GPU tests of every local-rank
+#             path, then 4 local ranks on 8192^2 gray sobel at halo depth 1
+#             (rounds vs grouped send / receive, each halo schedule) and at
+#             the automatic depth                                     -> r6/local
 # Every GPU step runs under its own timeout; a failing step ends the script.
 set -o pipefail
 S=${1:?study}
@@ -53,6 +57,20 @@ batch1)
     done
     for v in 0 1 2 3; do
       STRIPE_CONV_SCHED=$v timeout -k 10 200 python tools/kbench.py --chains "$C31|$C31:lsb" --shape 16384x16384x3 --iters 30 >> $O/conv_s${v}_16k.txt 2>&1 || exit 5
+    done
+  done
+  ;;
+local)
+  timeout -k 10 900 python -u -m pytest tests/test_r6_local.py tests/test_gpu_engine.py tests/test_dist_pipelined.py tests/test_deep_halo.py tests/test_advice_r2.py tests/test_weighted_split.py tests/test_n8.py tests/test_multi_gpu.py -m gpu -q -x --timeout 200 --timeout-method thread > $O/tests.txt 2>&1 || exit 2
+  CFG3="bin/stripe bench --synthetic 8192x8192x1 --chain sobel --ranks 4 --iters 64 --warmup 8 --scope resident --backend local"
+  for r in 1 2; do
+    for rounds in 1 0; do
+      for sc in pipeline overlap serial; do
+        echo "rounds $rounds schedule $sc depth 1" >> $O/cfg3_depth1.txt
+        STRIPE_LOCAL_ROUNDS=$rounds STRIPE_HALO_SCHEDULE=$sc timeout -k 10 120 $CFG3 --halo-depth 1 2>&1 | grep -v amdgpu.ids >> $O/cfg3_depth1.txt || exit 3
+      done
+      echo "rounds $rounds depth auto" >> $O/cfg3_auto.txt
+      STRIPE_LOCAL_ROUNDS=$rounds timeout -k 10 120 $CFG3 2>&1 | grep -v amdgpu.ids >> $O/cfg3_auto.txt || exit 3
     done
   done
   ;;
