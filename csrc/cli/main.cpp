@@ -155,6 +155,14 @@ struct Group {
   std::vector<int> devices;
 };
 
+// N > 1 `local` ranks all on one GPU (their halo schedule: shared_gpu_schedule)
+bool shares_one_gpu(const std::string& backend, const Group& g) {
+  if (backend != "local" || g.devices.size() < 2) return false;
+  for (int d : g.devices)
+    if (d != g.devices[0]) return false;
+  return true;
+}
+
 Group make_group(const std::string& backend, int N, const std::vector<int>& devlist) {
   Group g;
   const int ndev = device_count();
@@ -309,8 +317,9 @@ int cmd_run(const Args& a) {
   JpegOut jo;
   jo.quality = a.geti("quality", 95);
   JpegOut* jp = is_jpeg_path(a.get("output")) ? &jo : nullptr;
-  Image out = in.coefs ? run_group(cfg, g.comms, g.devices, in.jpeg, iters, &t, jp)
-                       : run_group(cfg, g.comms, g.devices, in.img, iters, &t, jp);
+  const EngineConfig gcfg = shares_one_gpu(backend, g) ? shared_gpu_schedule(cfg) : cfg;
+  Image out = in.coefs ? run_group(gcfg, g.comms, g.devices, in.jpeg, iters, &t, jp)
+                       : run_group(gcfg, g.comms, g.devices, in.img, iters, &t, jp);
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   const auto tw = std::chrono::steady_clock::now();
   if (jp) write_file_atomic(a.get("output"), jo.bytes);
@@ -436,7 +445,7 @@ int cmd_bench(const Args& a) {
       int chosen = -1;
       auto body = [&](int r) {
         try {
-          EngineConfig c = cfg;
+          EngineConfig c = shares_one_gpu(backend, g) ? shared_gpu_schedule(cfg) : cfg;
           c.root_buffers = scope == "dist";
           if (!g.devices.empty()) c.device = g.devices[r];
           if (nframes > 1) {

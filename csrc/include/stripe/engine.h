@@ -374,6 +374,14 @@ struct RingCheck {
 };
 RingCheck comm_ring_check(Comm* comm, int device, size_t bytes, int frames, int streams, int iters);
 
+// Halo schedule for N in-process `local` ranks sharing ONE GPU: the serial
+// schedule (exchange, then the whole stripe on one stream), unless
+// STRIPE_HALO_SCHEDULE pins one.  4 local ranks on 8192^2 gray sobel at halo
+// depth 1: serial 0.068-0.069 ms a step, overlap 0.113-0.135, the pipelined
+// default 0.148-0.163 -- the cross-stream events of N rank threads cost more
+// than they hide (profiles/r6/local/).  Ranks on distinct GPUs keep `cfg`.
+EngineConfig shared_gpu_schedule(EngineConfig cfg);
+
 // Convenience driver: run the whole distributed pipeline on `world` in-process
 // ranks (local device backend or host backend), root -> scatter -> run -> gather.
 Image run_local_group(const EngineConfig& cfg, int world, const Image& input, int iterations,

@@ -101,8 +101,9 @@ class LocalHub {
   // event recorded on its stream); the last to arrive issues the whole
   // exchange on its own stream -- a wait on every rank's `ready`, every
   // rank's halo rows in one multi-copy launch, one `done` event -- and every
-  // rank's stream waits on `done`.  3 N + 2 HIP calls per exchange instead of
-  // ~9 N from N threads contending for the runtime (profiles/r6/local/).
+  // rank's stream waits on `done`: 3 N + 2 HIP calls per exchange instead of
+  // ~9 N from N threads contending for the runtime, but every rank thread
+  // waits for the last one (measured slower; opt-in, profiles/r6/local/).
   struct RoundPost {
     int rank = 0;
     const void* su = nullptr;
@@ -305,10 +306,13 @@ class LocalComm final : public Comm {
   void abort(const std::string& why) override { hub_->abort(why); }
   bool exchange_rows(int participants, const void* send_up, void* recv_up, const void* send_down, void* recv_down,
                      size_t bytes, hipStream_t s) override {
-    // STRIPE_LOCAL_ROUNDS=0: grouped sends / receives instead (A/B)
+    // STRIPE_LOCAL_ROUNDS=1 (A/B, off by default): slower than the grouped
+    // sends / receives it replaces -- every exchange becomes a host barrier
+    // of all rank threads (4 ranks, 8192^2 sobel, serial schedule at depth 1:
+    // 0.088-0.090 vs 0.068-0.069 ms a step, profiles/r6/local/)
     static const bool rounds = [] {
       const char* e = std::getenv("STRIPE_LOCAL_ROUNDS");
-      return !(e && std::atoi(e) == 0);
+      return e && std::atoi(e) == 1;
     }();
     if (!rounds || !hub_->device() || participants <= 1) return false;
     STRIPE_CHECK(!in_group_, "exchange_rows inside an open group");

@@ -313,7 +313,17 @@ Image run_group(const EngineConfig& cfg, const std::vector<Comm*>& comms, const 
   return run_group_impl(cfg, comms, devices, input, iterations, times, jpeg_out);
 }
 
-Image run_local_group(const EngineConfig& cfg, int world, const Image& input, int iterations, PhaseTimes* times) {
+EngineConfig shared_gpu_schedule(EngineConfig cfg) {
+  if (cfg.backend == BackendKind::Device && !std::getenv("STRIPE_HALO_SCHEDULE")) {
+    cfg.overlap = false;
+    cfg.pipeline = false;
+  }
+  return cfg;
+}
+
+Image run_local_group(const EngineConfig& cfg_in, int world, const Image& input, int iterations, PhaseTimes* times) {
+  // every in-process rank runs on cfg.device: one shared GPU
+  const EngineConfig cfg = world > 1 ? shared_gpu_schedule(cfg_in) : cfg_in;
   auto hub = make_local_hub(world, cfg.backend == BackendKind::Device);
   std::vector<std::unique_ptr<Comm>> owned;
   std::vector<Comm*> comms;
