@@ -74,6 +74,17 @@ local)
     done
   done
   ;;
+blurdiag)
+  # which memory stream sets blur:31's time: loads / stores masked out of range
+  # (STRIPE_BLUR_VARIANT 7 / 8 / 9, wrong output, timing only), alternating
+  # with the default
+  for r in 1 2; do
+    for v in 0 7 8 9; do
+      STRIPE_BLUR_VARIANT=$v timeout -k 10 120 python tools/kbench.py --chains "blur:31|blur:31:lsb" --shape 16384x16384x3 --iters 30 >> $O/blur_v${v}_16k.txt 2>&1 || exit 4
+      STRIPE_BLUR_VARIANT=$v timeout -k 10 120 python tools/kbench.py --chains "blur:31|blur:31:lsb" --shape 16384x2048x3 --iters 60 >> $O/blur_v${v}_stripe.txt 2>&1 || exit 4
+    done
+  done
+  ;;
 *)
   echo "unknown study $S" >&2
   exit 1
