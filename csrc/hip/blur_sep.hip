@@ -167,8 +167,7 @@ struct PlGeom {
 // loses every issue arbitration to the older half on its SIMD); bit 1 -- every
 // wave raises its priority over its step's tile loop (the MFMAs) and drops it
 // for the staging / barrier part.
-template <int C, bool EDGE, int NX_, int PFD, int OCC, bool LSB = false, int NW = 1, bool EARLY = true, int SCHED = 0,
-          int DIAG = 0>
+template <int C, bool EDGE, int NX_, int PFD, int OCC, bool LSB = false, int NW = 1, bool EARLY = true, int SCHED = 0>
 __global__ __launch_bounds__(blur_threads(NW), OCC * 256 / blur_threads(NW)) void k_blur_pl(SepArgs sa) {
   using G = PlGeom<C, NX_, NW>;
   constexpr int NX = G::NX;
@@ -264,7 +263,6 @@ __global__ __launch_bounds__(blur_threads(NW), OCC * 256 / blur_threads(NW)) voi
   for (int i = 0; i < P; ++i) loff[i] = (uint32_t)(srow[i] * a.in_pitch + (wx + scol[i]) * C);
   auto load = [&](int i, uint32_t off, auto buf_c) __attribute__((always_inline)) {
     constexpr int B = decltype(buf_c)::value;
-    if constexpr (DIAG & 1) off = kOOB;  // diagnostic: no read traffic
     if constexpr (C == 3) pf[B][i] = __builtin_amdgcn_raw_buffer_load_b96(rin, off, 0, 0);
     else pf[B][i] = __builtin_amdgcn_raw_buffer_load_b128(rin, off, 0, 0);
   };
@@ -449,7 +447,7 @@ __global__ __launch_bounds__(blur_threads(NW), OCC * 256 / blur_threads(NW)) voi
         // lane: pixels 4g .. 4g + 3 of x-tile i in output row yg + 16 q + m
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-          const uint32_t off = (DIAG & 2) ? kOOB : rowoff[q] + (uint32_t)((sx + 16 * i + 4 * g) * C);
+          const uint32_t off = rowoff[q] + (uint32_t)((sx + 16 * i + 4 * g) * C);
           if (!EDGE || npx[i] == 4 || npx[i] == 0 || rowoff[q] == kOOB) {
             if constexpr (C == 3)
               __builtin_amdgcn_raw_buffer_store_b96(u3{wo[q][0], wo[q][1], wo[q][2]}, rout, off | colok[i], 0, 0);
@@ -702,28 +700,20 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
   // 4-6: the default shape with wave priorities (k_blur_pl SCHED 1-3)
 #define STRIPE_BLUR_PRIO(LSB, SC)                                                                    \
   Cfg { 2, 2, 8, dev::k_blur_pl<3, false, 2, 2, 2, LSB, 8, true, SC>, (size_t)dev::PlGeom<3, 2, 8>::LDS }
-  // 7-9: diagnostics (wrong output): the default with its global loads (7),
-  // its stores (8) or both (9) masked out of range -- the instructions issue,
-  // no memory traffic moves
-#define STRIPE_BLUR_DIAG(LSB, DG)                                                                    \
-  Cfg { 2, 2, 8, dev::k_blur_pl<3, false, 2, 2, 2, LSB, 8, true, 0, DG>, (size_t)dev::PlGeom<3, 2, 8>::LDS }
-  static const Cfg variants[2][10] = {
+  static const Cfg variants[2][7] = {
       {STRIPE_BLUR_CFGW(3, false, 2, 2, 2, false, 8), STRIPE_BLUR_CFGW(3, false, 2, 2, 2, false, 4),
        STRIPE_BLUR_CFGW(3, false, 2, 1, 2, false, 4), STRIPE_BLUR_LATE(false), STRIPE_BLUR_PRIO(false, 1),
-       STRIPE_BLUR_PRIO(false, 2), STRIPE_BLUR_PRIO(false, 3), STRIPE_BLUR_DIAG(false, 1),
-       STRIPE_BLUR_DIAG(false, 2), STRIPE_BLUR_DIAG(false, 3)},
+       STRIPE_BLUR_PRIO(false, 2), STRIPE_BLUR_PRIO(false, 3)},
       {STRIPE_BLUR_CFGW(3, false, 2, 2, 2, true, 8), STRIPE_BLUR_CFGW(3, false, 2, 2, 2, true, 4),
        STRIPE_BLUR_CFGW(3, false, 2, 1, 2, true, 4), STRIPE_BLUR_LATE(true), STRIPE_BLUR_PRIO(true, 1),
-       STRIPE_BLUR_PRIO(true, 2), STRIPE_BLUR_PRIO(true, 3), STRIPE_BLUR_DIAG(true, 1),
-       STRIPE_BLUR_DIAG(true, 2), STRIPE_BLUR_DIAG(true, 3)}};
-#undef STRIPE_BLUR_DIAG
+       STRIPE_BLUR_PRIO(true, 2), STRIPE_BLUR_PRIO(true, 3)}};
 #undef STRIPE_BLUR_LATE
 #undef STRIPE_BLUR_PRIO
   static const int env_variant = [] {
     const char* e = std::getenv("STRIPE_BLUR_VARIANT");
     return e ? std::atoi(e) : 0;
   }();
-  const Cfg& cf = (p.cmid == 3 && !edge && env_variant > 0 && env_variant < 10) ? variants[lsb][env_variant]
+  const Cfg& cf = (p.cmid == 3 && !edge && env_variant > 0 && env_variant < 7) ? variants[lsb][env_variant]
                                                                                : cfgs[lsb][p.cmid == 3][edge];
 #undef STRIPE_BLUR_CFG
 #undef STRIPE_BLUR_CFGW
