@@ -77,7 +77,9 @@ local)
 blurdiag)
   # which memory stream sets blur:31's time: loads / stores masked out of range
   # (STRIPE_BLUR_VARIANT 7 / 8 / 9, wrong output, timing only), alternating
-  # with the default
+  # with the default.  The diagnostic instances were removed from the kernel
+  # after the run (git history: "blur:31 diagnostic variants"); today 7-9
+  # fall back to the default
   for r in 1 2; do
     for v in 0 7 8 9; do
       STRIPE_BLUR_VARIANT=$v timeout -k 10 120 python tools/kbench.py --chains "blur:31|blur:31:lsb" --shape 16384x16384x3 --iters 30 >> $O/blur_v${v}_16k.txt 2>&1 || exit 4
