@@ -87,6 +87,16 @@ blurdiag)
     done
   done
   ;;
+blurpst)
+  # paired row stores (STRIPE_BLUR_VARIANT=7): numerics first, then A/B with the default
+  STRIPE_BLUR_VARIANT=7 timeout -k 10 600 python -u -m pytest tests/test_oracle_conv.py tests/test_gpu_large.py -m gpu -q -x --timeout 200 --timeout-method thread > $O/tests_v7.txt 2>&1 || exit 2
+  for r in 1 2 3; do
+    for v in 0 7; do
+      STRIPE_BLUR_VARIANT=$v timeout -k 10 120 python tools/kbench.py --chains "blur:31|blur:31:lsb" --shape 16384x16384x3 --iters 30 >> $O/blur_v${v}_16k.txt 2>&1 || exit 4
+      STRIPE_BLUR_VARIANT=$v timeout -k 10 120 python tools/kbench.py --chains "blur:31|blur:31:lsb" --shape 16384x2048x3 --iters 60 >> $O/blur_v${v}_stripe.txt 2>&1 || exit 4
+    done
+  done
+  ;;
 *)
   echo "unknown study $S" >&2
   exit 1
