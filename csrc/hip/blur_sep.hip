@@ -162,23 +162,17 @@ struct PlGeom {
 // within 1 LSB of the f64 result (the host bounds the error per weight set and
 // keeps the exact kernel when it cannot promise that).
 // (launch bounds: OCC waves per SIMD = OCC * 256 / THREADS workgroups per CU)
-// SCHED (A/B, STRIPE_BLUR_VARIANT 4-7): bit 0 -- the younger half of an 8-wave
-// workgroup (waves 4-7) runs at priority 1 for the whole kernel (it otherwise
-// loses every issue arbitration to the older half on its SIMD); bit 1 -- every
-// wave raises its priority over its step's tile loop (the MFMAs) and drops it
-// for the staging / barrier part; bit 2 -- paired row stores (PST below).
-template <int C, bool EDGE, int NX_, int PFD, int OCC, bool LSB = false, int NW = 1, bool EARLY = true, int SCHED = 0>
+// (Round 6 measured wave priorities -- the static form for the younger half
+// of the 8-wave workgroup, priority over each step's MFMAs -- and stores of
+// whole 96-byte row pieces as A/B instances: null or slower, removed;
+// profiles/r6/sched/, profiles/r6/blurpst/.)
+template <int C, bool EDGE, int NX_, int PFD, int OCC, bool LSB = false, int NW = 1, bool EARLY = true>
 __global__ __launch_bounds__(blur_threads(NW), OCC * 256 / blur_threads(NW)) void k_blur_pl(SepArgs sa) {
   using G = PlGeom<C, NX_, NW>;
   constexpr int NX = G::NX;
-  // SCHED bit 2: paired row stores (RGB, 2-tile strips, whole 4-pixel groups)
-  constexpr bool PST = (SCHED & 4) && C == 3 && NX == 2 && !EDGE;
   const KArgs& a = sa.a;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if constexpr ((SCHED & 1) && NW == 8) {
-    if (wave >= 4) __builtin_amdgcn_s_setprio(1);  // wave-uniform (readfirstlane): a scalar branch
-  }
   const int sl = NW == 1 ? lane : (int)threadIdx.x;  // staging lane
   int strip, by, sgx;  // strip of this wave, band, first strip of the staged window
   if constexpr (NW == 1) {
@@ -358,18 +352,11 @@ __global__ __launch_bounds__(blur_threads(NW), OCC * 256 / blur_threads(NW)) voi
     if (START && k + PFD <= ngroups) prefetch(k + PFD, buf_c);
     const int yg = base + 32 * (k - 1);  // first row of the group being finished
     uint32_t rowoff[2];
-    // PST: row offsets of the paired stores (rows m & 7 and 8 + (m & 7) of each half)
-    uint32_t rowpa[2], rowpb[2];
     if constexpr (FIN) {
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int y = yg + 16 * q + m;
         rowoff[q] = (y >= ys && y < ye) ? a.out_org + (uint32_t)((int64_t)y * a.out_pitch) : kOOB;
-        if constexpr (PST) {
-          const int ya = yg + 16 * q + (m & 7), yb = ya + 8;
-          rowpa[q] = (ya >= ys && ya < ye) ? a.out_org + (uint32_t)((int64_t)ya * a.out_pitch) : kOOB;
-          rowpb[q] = (yb >= ys && yb < ye) ? a.out_org + (uint32_t)((int64_t)yb * a.out_pitch) : kOOB;
-        }
       }
     }
     // Tiles t = C i + c (x-tile i, channel c), software-pipelined: the LDS
@@ -400,7 +387,6 @@ __global__ __launch_bounds__(blur_threads(NW), OCC * 256 / blur_threads(NW)) voi
     // finished output bytes of the current x-tile, packed as the channels
     // complete: RGB interleave R0 G0 B0 R1 | G1 B1 R2 G2 | B2 R3 G3 B3 (byte e = 3 px + c)
     uint32_t wo[2][C];
-    uint32_t wo0[PST ? 2 : 1][C];  // PST: x-tile 0's bytes, stored with x-tile 1's
     auto vert = [&](int t, const f4 (&x)[2]) __attribute__((always_inline)) {
       const int i = t / C, c = t % C;
       // accumulator layout -> A operand of the vertical product (k = X row, permuted)
@@ -454,36 +440,6 @@ __global__ __launch_bounds__(blur_threads(NW), OCC * 256 / blur_threads(NW)) voi
       }
       if constexpr (FIN) {
         if (c != C - 1) return;
-        if constexpr (PST) {
-          // paired stores: x-tile 0's bytes wait for x-tile 1's; then the 16
-          // lanes of a DPP row trade halves (row_shr / row_shl 8) so one store
-          // writes rows m & 7 (A) or 8 + (m & 7) (B) with all 32 pixels of the
-          // strip: 8 rows x 96 contiguous bytes per instruction instead of
-          // 16 rows x 48
-          if (i == 0) {
-#pragma unroll
-            for (int q = 0; q < 2; ++q)
-#pragma unroll
-              for (int w = 0; w < C; ++w) wo0[q][w] = wo[q][w];
-            return;
-          }
-          const bool hi = m >= 8;  // lanes 8-15 of the DPP row: x-tile 1's pixels
-          const uint32_t xoff = (uint32_t)((sx + (hi ? 16 : 0) + 4 * g) * C) | colok[hi ? 1 : 0];
-#pragma unroll
-          for (int q = 0; q < 2; ++q) {
-            uint32_t va[C], vb[C];
-#pragma unroll
-            for (int w = 0; w < C; ++w) {
-              // A: lanes 0-7 keep x-tile 0 (row m), lanes 8-15 take x-tile 1 of row m - 8
-              va[w] = (uint32_t)__builtin_amdgcn_update_dpp((int)wo0[q][w], (int)wo[q][w], 0x118, 0xF, 0xC, false);
-              // B: lanes 8-15 keep x-tile 1 (row m), lanes 0-7 take x-tile 0 of row m + 8
-              vb[w] = (uint32_t)__builtin_amdgcn_update_dpp((int)wo[q][w], (int)wo0[q][w], 0x108, 0xF, 0x3, false);
-            }
-            __builtin_amdgcn_raw_buffer_store_b96(u3{va[0], va[1], va[2]}, rout, rowpa[q] + xoff, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b96(u3{vb[0], vb[1], vb[2]}, rout, rowpb[q] + xoff, 0, 0);
-          }
-          return;
-        }
         // lane: pixels 4g .. 4g + 3 of x-tile i in output row yg + 16 q + m
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
@@ -504,7 +460,6 @@ __global__ __launch_bounds__(blur_threads(NW), OCC * 256 / blur_threads(NW)) voi
     };
     half8 F[2][2][2];
     f4 X[2][2];
-    if constexpr (SCHED & 2) __builtin_amdgcn_s_setprio(2);
     hread(0, F[0]);
     if (T > 1) hread(1, F[1]);
     hmfma(F[0], X[0]);
@@ -517,10 +472,6 @@ __global__ __launch_bounds__(blur_threads(NW), OCC * 256 / blur_threads(NW)) voi
         if (t == (T > 1 ? 1 : 0) && k + 1 <= ngroups)
           stage(std::integral_constant<int, 1 - decltype(buf_c)::value>{}, wl + ((k + 1) & 1) * G::TILE);
       }
-    }
-    if constexpr (SCHED & 2) {
-      if ((SCHED & 1) && NW == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);
-      else __builtin_amdgcn_s_setprio(0);
     }
     if constexpr (NW == 1) sep_lds_sync();  // fragment reads done before the next pair overwrites the planes
   };
@@ -731,30 +682,22 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
   // A/B variants of the RGB non-edge kernel (STRIPE_BLUR_VARIANT=n): 1 = two
   // independent 4-wave workgroups per CU (NW 4, two pairs in flight), 2 = the
   // same with one pair in flight, 3 = the 8-wave windows staging each pair
-  // between the barrier and the MFMAs (round 4's default, EARLY = false),
-  // 4 / 5 / 6 = the default with wave priorities (k_blur_pl SCHED 1 / 2 / 3),
-  // 7 = the default with paired row stores (SCHED 4).
+  // between the barrier and the MFMAs (round 4's default, EARLY = false).
   // (Three pairs in flight, lsb, 254 registers: 0.376 vs 0.354 ms on 16K,
   // 0.047 vs 0.042 on the stripe, profiles/r5/blur/pfd3_*.txt: removed.)
 #define STRIPE_BLUR_LATE(LSB)                                                                        \
   Cfg { 2, 2, 8, dev::k_blur_pl<3, false, 2, 2, 2, LSB, 8, false>, (size_t)dev::PlGeom<3, 2, 8>::LDS }
-  // 4-7: the default shape with wave priorities / paired stores (k_blur_pl SCHED 1-4)
-#define STRIPE_BLUR_PRIO(LSB, SC)                                                                    \
-  Cfg { 2, 2, 8, dev::k_blur_pl<3, false, 2, 2, 2, LSB, 8, true, SC>, (size_t)dev::PlGeom<3, 2, 8>::LDS }
-  static const Cfg variants[2][8] = {
+  static const Cfg variants[2][4] = {
       {STRIPE_BLUR_CFGW(3, false, 2, 2, 2, false, 8), STRIPE_BLUR_CFGW(3, false, 2, 2, 2, false, 4),
-       STRIPE_BLUR_CFGW(3, false, 2, 1, 2, false, 4), STRIPE_BLUR_LATE(false), STRIPE_BLUR_PRIO(false, 1),
-       STRIPE_BLUR_PRIO(false, 2), STRIPE_BLUR_PRIO(false, 3), STRIPE_BLUR_PRIO(false, 4)},
+       STRIPE_BLUR_CFGW(3, false, 2, 1, 2, false, 4), STRIPE_BLUR_LATE(false)},
       {STRIPE_BLUR_CFGW(3, false, 2, 2, 2, true, 8), STRIPE_BLUR_CFGW(3, false, 2, 2, 2, true, 4),
-       STRIPE_BLUR_CFGW(3, false, 2, 1, 2, true, 4), STRIPE_BLUR_LATE(true), STRIPE_BLUR_PRIO(true, 1),
-       STRIPE_BLUR_PRIO(true, 2), STRIPE_BLUR_PRIO(true, 3), STRIPE_BLUR_PRIO(true, 4)}};
+       STRIPE_BLUR_CFGW(3, false, 2, 1, 2, true, 4), STRIPE_BLUR_LATE(true)}};
 #undef STRIPE_BLUR_LATE
-#undef STRIPE_BLUR_PRIO
   static const int env_variant = [] {
     const char* e = std::getenv("STRIPE_BLUR_VARIANT");
     return e ? std::atoi(e) : 0;
   }();
-  const Cfg& cf = (p.cmid == 3 && !edge && env_variant > 0 && env_variant < 8) ? variants[lsb][env_variant]
+  const Cfg& cf = (p.cmid == 3 && !edge && env_variant > 0 && env_variant < 4) ? variants[lsb][env_variant]
                                                                                : cfgs[lsb][p.cmid == 3][edge];
 #undef STRIPE_BLUR_CFG
 #undef STRIPE_BLUR_CFGW

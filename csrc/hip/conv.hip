@@ -335,12 +335,11 @@ struct ConvI8Args {
 // k-step right after its last MFMA of this one (the rest of the step's MFMAs
 // cover the LDS latency), freeing C MT x 4 registers -- what 3 digits at 4
 // m-tiles need to fit without scratch.
-// SCHED (A/B, STRIPE_CONV_SCHED; A1 instances): bit 0 -- no sched_barrier(0)
-// fences around a k-step's MFMA block (the compiler may interleave the B-ring
-// loads and fragment reads into it); bit 1 -- s_setprio(1) over the MFMA block,
-// so a wave in its k-loop wins issue over the other workgroup's wave staging
-// or storing on the same SIMD.
-template <int C, int MT, int ND, int NT = 1, bool A1 = false, int SCHED = 0>
+// (Round 6 measured the k-step without its sched_barrier(0) fences -- 14 %
+// slower exact: the compiler moves the single-buffered A re-reads away from
+// their MFMAs -- and s_setprio(1) over the MFMA block -- null; both removed,
+// profiles/r6/sched/.)
+template <int C, int MT, int ND, int NT = 1, bool A1 = false>
 __global__ __launch_bounds__(256, 2) void k_conv_i8(ConvI8Args ca) {
   const KArgs& a = ca.a;
   const int R = ca.R, nq = ca.nq;
@@ -496,8 +495,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_i8(ConvI8Args ca) {
         if constexpr (A1) {
           // fragment (c, mt): its ND MFMAs, then its next-step read in place
           const uint8_t* pl = cur + 4 * min((q0 / 3) + (i + 1) / 3, nq - 1) * kQPS + aoff[(i + 1) % 3];
-          if constexpr (!(SCHED & 1)) __builtin_amdgcn_sched_barrier(0);
-          if constexpr (SCHED & 2) __builtin_amdgcn_s_setprio(1);
+          __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int c = 0; c < C; ++c)
 #pragma unroll
@@ -508,8 +506,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_i8(ConvI8Args ca) {
                     __builtin_amdgcn_mfma_i32_16x16x64_i8(af[0][c][mt], bq[i % 3][dg], acc[dg][c][mt], 0, 0, 0);
               af[0][c][mt] = *reinterpret_cast<const i32x4*>(pl + c * pstride + 16 * mt * kQPS);
             }
-          if constexpr (SCHED & 2) __builtin_amdgcn_s_setprio(0);
-          if constexpr (!(SCHED & 1)) __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_sched_barrier(0);
         } else {
           read_a(min((q0 / 3) + (i + 1) / 3, nq - 1), (i + 1) % 3, (i + 1) & 1);
           __builtin_amdgcn_sched_barrier(0);
@@ -829,13 +826,6 @@ void launch_conv_mfma(const Pass& p, const PassConsts& pc, const PassLaunch& L, 
       const char* e = std::getenv("STRIPE_CONV_A1");
       return !(e && std::atoi(e) == 0);
     }();
-    // STRIPE_CONV_SCHED=1..3: the RGB single-buffered kernels with the k-loop
-    // scheduling variants (k_conv_i8 SCHED; A/B)
-    static const int env_sched = [] {
-      const char* e = std::getenv("STRIPE_CONV_SCHED");
-      const int v = e ? std::atoi(e) : 0;
-      return v >= 1 && v <= 3 ? v : 0;
-    }();
     auto pick = [&]() {
       if (env_a1 && nt == 1) {
 #define STRIPE_CONVQ1(CC, MM, DD)                                                                            \
@@ -845,15 +835,6 @@ void launch_conv_mfma(const Pass& p, const PassConsts& pc, const PassLaunch& L, 
     }
         STRIPE_CONVQ1(3, 4, 3) STRIPE_CONVQ1(3, 5, 2) STRIPE_CONVQ1(1, 10, 2)
 #undef STRIPE_CONVQ1
-        if (fn && env_sched > 0 && p.cmid == 3) {
-          using KF = void (*)(dev::ConvI8Args);
-          static const KF v3[3] = {dev::k_conv_i8<3, 4, 3, 1, true, 1>, dev::k_conv_i8<3, 4, 3, 1, true, 2>,
-                                   dev::k_conv_i8<3, 4, 3, 1, true, 3>};
-          static const KF v2[3] = {dev::k_conv_i8<3, 5, 2, 1, true, 1>, dev::k_conv_i8<3, 5, 2, 1, true, 2>,
-                                   dev::k_conv_i8<3, 5, 2, 1, true, 3>};
-          if (mt == 4 && nd == 3) fn = v3[env_sched - 1];
-          if (mt == 5 && nd == 2) fn = v2[env_sched - 1];
-        }
         if (fn) return;
       }
 #define STRIPE_CONVQ(CC, MM, DD, NT)                                                                         \

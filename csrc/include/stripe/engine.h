@@ -177,6 +177,17 @@ class Engine {
   int halo_depth() const { return depth_; }
   // EngineConfig::self_halo in effect (the stripe exchanges halo rows with itself)
   bool self_halo() const { return self_halo_; }
+  // Batched exchanges (several engines' halos in one communicator group, e.g.
+  // the frames of a frame stream that share a stream): post_halo() posts the
+  // sends / receives of this engine's next step inside a group the caller
+  // opened (comm group_start / group_end around the posts, on the compute
+  // stream), run_posted() then runs that one step without an exchange of its
+  // own.  Single-pass iterable chains on device engines with neighbours
+  // (posts_halo()); otherwise post_halo() posts nothing and run_posted() is
+  // run(1).
+  bool posts_halo() const;
+  void post_halo();
+  void run_posted();
   // Tuned band heights, occupancy caps and memory policies per pass (after
   // autotune), for reporting.
   std::vector<int> bands() const;
@@ -271,6 +282,9 @@ class Engine {
   uint8_t* origin(const Buffer& b, int C) const;
   uint8_t* root_origin(const Buffer& b, int C) const;
   void exchange_halo(uint8_t* org, int C, int R, hipStream_t s);
+  void post_halo_ops(uint8_t* org, int C, int R, hipStream_t s);
+  int posted_buf_ = -1;     // buffer whose halo post_halo() posted (-1: none)
+  bool halo_done_ = false;  // run_posted(): this step's exchange already happened
   // this rank exchanges halo rows (another active rank, or the self-halo ring)
   bool neighbours() const { return part_.active > 1 || self_halo_; }
   bool has_up() const { return rank_ > 0 || self_halo_; }

@@ -266,6 +266,12 @@ PYBIND11_MODULE(_C, m) {
         c.comm->barrier();
       })
       .def("abort", [](PyComm& c, const std::string& why) { c.comm->abort(why); })
+      // brackets for batched halo posts (Engine.post_halo of several engines)
+      .def("group_start", [](PyComm& c) { c.comm->group_start(); })
+      .def("group_end", [](PyComm& c) {
+        py::gil_scoped_release nogil;
+        c.comm->group_end();
+      })
       .def("identity", [](const PyComm& c) {
         py::dict d;
         for (const auto& kv : c.comm->identity()) d[kv.first.c_str()] = kv.second;
@@ -569,6 +575,15 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("out_channels", &Engine::out_channels)
       .def_property_readonly("halo_depth", &Engine::halo_depth)
       .def_property_readonly("self_halo", &Engine::self_halo)
+      .def_property_readonly("posts_halo", &Engine::posts_halo)
+      .def("post_halo", [](Engine& e) {
+        py::gil_scoped_release nogil;
+        e.post_halo();
+      })
+      .def("run_posted", [](Engine& e) {
+        py::gil_scoped_release nogil;
+        e.run_posted();
+      })
       .def_property_readonly("plan", [](const Engine& e) { return e.plan().describe(); })
       .def_property_readonly("partition", [](const Engine& e) { return e.partition().describe(); })
       .def_property_readonly("stripe", [](const Engine& e) {

@@ -527,6 +527,19 @@ void Engine::exchange_halo(uint8_t* org, int C, int R, hipStream_t s) {
     return;
   }
   comm_->group_start();
+  post_halo_ops(org, C, R, s);
+  comm_->group_end();
+  if (time_halo_) stage_end(Stage::Halo, s);
+}
+
+// The sends and receives of one halo exchange, inside a group the caller opened.
+void Engine::post_halo_ops(uint8_t* org, int C, int R, hipStream_t s) {
+  const Stripe& st = stripe();
+  const int64_t P = pitch(C);
+  const size_t bytes = (size_t)(R * P);
+  uint8_t* base = org - kMarginBytes;
+  const int up = rank_ > 0 ? rank_ - 1 : -1;
+  const int down = rank_ + 1 < part_.active ? rank_ + 1 : -1;
   if (self_halo_) {
     // the rank is its own upper and lower neighbour: the same two sends and
     // two receives an interior rank posts, all to itself.  Sends and receives
@@ -537,7 +550,9 @@ void Engine::exchange_halo(uint8_t* org, int C, int R, hipStream_t s) {
     comm_->recv(base - (int64_t)R * P, bytes, rank_, s);
     comm_->send(base, bytes, rank_, s);
     comm_->recv(base + (int64_t)st.rows * P, bytes, rank_, s);
-  } else if (up >= 0) {
+    return;
+  }
+  if (up >= 0) {
     comm_->send(base, bytes, up, s);
     comm_->recv(base - (int64_t)R * P, bytes, up, s);
   }
@@ -545,8 +560,38 @@ void Engine::exchange_halo(uint8_t* org, int C, int R, hipStream_t s) {
     comm_->send(base + (int64_t)(st.rows - R) * P, bytes, down, s);
     comm_->recv(base + (int64_t)st.rows * P, bytes, down, s);
   }
-  comm_->group_end();
-  if (time_halo_) stage_end(Stage::Halo, s);
+}
+
+bool Engine::posts_halo() const {
+  return device() && comm_ && cfg_.halo && neighbours() && plan_.passes.size() == 1 && plan_.cin == plan_.cout &&
+         plan_.passes[0].R > 0 && stripe().rows > 0;
+}
+
+void Engine::post_halo() {
+  if (!posts_halo()) return;
+  STRIPE_CHECK(cur_c_ == plan_.cin, "post_halo: the engine input has " << cur_c_ << " channels");
+  const Pass& p = plan_.passes[0];
+  STRIPE_CHECK(!self_halo_ || p.R <= stripe().rows, "self-halo of " << p.R << " rows needs a stripe that tall");
+  fault_point("halo", rank_);
+  post_halo_ops(origin(buf_[cur_], p.cin), p.cin, p.R, s_compute_);
+  posted_buf_ = cur_;
+}
+
+void Engine::run_posted() {
+  if (!posts_halo()) {
+    run(1);
+    return;
+  }
+  STRIPE_CHECK(posted_buf_ == cur_, "run_posted: the halo of the current input was not posted (post_halo)");
+  posted_buf_ = -1;
+  halo_done_ = true;
+  try {
+    run(1);
+  } catch (...) {
+    halo_done_ = false;
+    throw;
+  }
+  halo_done_ = false;
 }
 
 PassLaunch Engine::make_launch(const Pass& p, const uint8_t* in, uint8_t* out, int pi) const {
@@ -595,7 +640,7 @@ void Engine::run_pass(const Pass& p, const uint8_t* in, uint8_t* out) {
   if (rows == 0) return;
   const RowGeom g = geom();
   const int R = p.R;
-  const bool xchg = (cfg_.halo && R > 0 && neighbours()) || (device() && schedule_emu() == 1 && R > 0);
+  const bool xchg = !halo_done_ && ((cfg_.halo && R > 0 && neighbours()) || (device() && schedule_emu() == 1 && R > 0));
   if (device() && schedule_emu() == 3 && R > 0 && rows > 2 * R) {  // two launches, one stream, no events
     const size_t pi3 = (size_t)(&p - plan_.passes.data());
     PassLaunch L3 = make_launch(p, in, out, (int)pi3);
@@ -690,7 +735,9 @@ void Engine::run(int iterations) {
     }
   };
   const int cycle = plan_.passes.size() % 2 == 0 ? 1 : 2;
-  if (depth_ >= 1 && cur_c_ == plan_.cin && ((depth_ > 1 && iterations > 1) || plan_.passes.size() > 1)) {
+  if (halo_done_) {  // run_posted: the halo rows already came in the caller's group
+    iterate(iterations);
+  } else if (depth_ >= 1 && cur_c_ == plan_.cin && ((depth_ > 1 && iterations > 1) || plan_.passes.size() > 1)) {
     run_deep(iterations);
   } else if (cfg_.pipeline && cfg_.overlap && pipelined_ok() && cur_c_ == plan_.cin) {
     run_pipelined(iterations);
