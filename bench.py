@@ -10,7 +10,8 @@ exchanges its 2 halo rows with its neighbours (ncclSend/ncclRecv, every step:
 halo depth 1) and filters its stripe.  How the exchange meets the filter is
 measured, not assumed: at N > 1 the three halo schedules (exchange then filter;
 interior rows beside the exchange, boundary rows after it; core / rim / edge
-on three streams), each with frames on one stream or alternating over two, are
+on three streams; serial steps whose exchanges are posted as one group per
+stream and round), each with frames on one stream or alternating over two, are
 timed on the real transport before the timed region and the fastest is kept
 (max over ranks; `halo_schedule` in the record).  Steps are iterated
 (ping-pong), so each step's halo rows are required work.
@@ -89,9 +90,10 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--band", type=int, default=0)
-    ap.add_argument("--halo-schedule", default="auto", choices=["auto", "serial", "overlap", "pipeline"],
+    ap.add_argument("--halo-schedule", default="auto", choices=["auto", "serial", "overlap", "pipeline", "batched"],
                     help="halo schedule of the headline steps at N>1 (auto: time each on the real transport before "
-                         "the timed region and keep the fastest, max over ranks)")
+                         "the timed region and keep the fastest, max over ranks; batched: serial steps with the "
+                         "exchanges of the frames sharing a stream in one group per round)")
     ap.add_argument("--frames", type=int, default=0,
                     help="frames the headline steps over (0: auto -- enough to defeat the Infinity Cache when a "
                          "stripe fits it, else 2 at N>1 so one frame's exchange runs beside the other's filter, "

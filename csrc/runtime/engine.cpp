@@ -379,6 +379,7 @@ void Engine::fill_margins(uint8_t* org, int C, int y0, int y1, int px, Border b,
 }
 
 void Engine::load_synthetic(uint64_t seed) {
+  posted_buf_ = -1;
   TraceRange tr("stripe.load");
   fault_point("load", rank_);
   const Stripe& st = stripe();
@@ -399,6 +400,7 @@ void Engine::load_synthetic(uint64_t seed) {
 }
 
 void Engine::load_packed(const void* src, bool src_device) {
+  posted_buf_ = -1;
   (void)src_device;
   const Stripe& st = stripe();
   const int C = plan_.cin;
@@ -459,6 +461,7 @@ void Engine::load_root_synthetic(uint64_t seed) {
 }
 
 void Engine::scatter() {
+  posted_buf_ = -1;
   const int C = plan_.cin;
   const int64_t P = pitch(C);
   const Stripe& st = stripe();
@@ -578,11 +581,10 @@ void Engine::post_halo() {
 }
 
 void Engine::run_posted() {
-  if (!posts_halo()) {
+  if (!posts_halo() || posted_buf_ != cur_) {  // nothing posted for this input: a step with its own exchange
     run(1);
     return;
   }
-  STRIPE_CHECK(posted_buf_ == cur_, "run_posted: the halo of the current input was not posted (post_halo)");
   posted_buf_ = -1;
   halo_done_ = true;
   try {
@@ -716,6 +718,7 @@ bool Engine::graph_ok() const {
 
 void Engine::run(int iterations) {
   STRIPE_CHECK(iterations >= 1, "iterations must be >= 1");
+  if (!halo_done_) posted_buf_ = -1;  // a post for this input is spent by any other step
   if (cfg_.autotune && !tuned_) autotune_bands();
   STRIPE_CHECK(iterations == 1 || plan_.cout == plan_.cin,
                "iterating a chain needs equal input/output channels (" << plan_.cin << "->" << plan_.cout << ")");
@@ -811,6 +814,7 @@ std::vector<float> Engine::run_timed(int iterations, int per, bool rewind_each) 
 }
 
 void Engine::rewind() {
+  posted_buf_ = -1;
   cur_ = run_in_buf_;
   cur_c_ = plan_.cin;
 }

@@ -447,16 +447,37 @@ class FrameStream:
         for f in self.frames[1:]:
             f.engine.set_tuning(e0.bands, e0.caps, e0.policies, e0.orders)
 
-    SCHEDULES = ("pipeline", "overlap", "serial")
+    SCHEDULES = ("pipeline", "overlap", "serial", "batched")
 
     def set_schedule(self, name: str):
-        """Halo schedule of every frame ("serial" | "overlap" | "pipeline")."""
+        """Halo schedule of every frame ("serial" | "overlap" | "pipeline" |
+        "batched").  "batched" is the serial schedule with the exchanges of
+        all frames that share a stream posted as ONE communicator group, ahead
+        of the first of those frames' steps in each round: one RCCL launch per
+        stream and round instead of one per frame and step (the frames' own
+        order on their stream already puts each frame's previous step before
+        it)."""
+        self.batched = name == "batched"
         for f in self.frames:
-            f.engine.halo_schedule = name
+            f.engine.halo_schedule = "serial" if self.batched else name
+
+    def _batch_candidate(self) -> bool:
+        """Whether the probe times "batched": frames of device engines that
+        exchange halo rows (N > 1, or the self-halo rank).  Decided on what
+        every rank shares -- never on a rank's own stripe -- so every rank
+        times the same candidate list."""
+        if not self.streams or len(self.frames) < 2:
+            return False
+        world = getattr(getattr(self.head, "ctx", None), "world", 2)
+        return world > 1 or bool(getattr(self.head.engine, "self_halo", False))
+
+    def _batches(self) -> bool:
+        """Batched posts apply: device engines that exchange halo rows."""
+        return bool(getattr(self, "batched", False) and self.streams and self.head.engine.posts_halo)
 
     @property
     def schedule(self) -> str:
-        return self.head.engine.halo_schedule
+        return "batched" if self._batches() else self.head.engine.halo_schedule
 
     def pick_schedule(self, reduce_max=None, barrier=None, steps: int = 0, rounds: int = 2) -> dict:
         """Time every halo schedule (interior / boundary overlap, the
@@ -476,7 +497,8 @@ class FrameStream:
         # collective reduce_max): device engines try every schedule, even one a
         # rank's own stripe runs another way (e.g. a thin stripe without the
         # pipeline); host engines have one schedule and time nothing
-        scheds = list(self.SCHEDULES) if self.streams else ["serial"]
+        scheds = ([s for s in self.SCHEDULES if s != "batched" or self._batch_candidate()] if self.streams
+                  else ["serial"])
         if getattr(getattr(self.head, "ctx", None), "world", 2) == 1:
             # one rank exchanges nothing: only schedules that differ on it (none)
             eff = []
@@ -539,10 +561,24 @@ class FrameStream:
         if i is None:
             i = self._i
             self._i += 1
-        f = self.frames[i % len(self.frames)]
+        k = i % len(self.frames)
+        f = self.frames[k]
         if not self.iterable:  # a chain that changes the channel count re-reads its (unchanged) input
             f.engine.rewind()
-        f.run(1)
+        if self._batches():
+            if k < self.nstreams:
+                # the first frame of its stream this round: one group with the
+                # exchanges of every frame on this stream (k, k + s, k + 2s, ...)
+                comm = f.ctx.comm
+                comm.group_start()
+                try:
+                    for g in range(k, len(self.frames), self.nstreams):
+                        self.frames[g].engine.post_halo()
+                finally:
+                    comm.group_end()
+            f.engine.run_posted()  # (a frame whose exchange was not posted makes its own)
+        else:
+            f.run(1)
 
     def synchronize(self):
         for f in self.frames:

@@ -47,7 +47,7 @@ def test_bench_gloo_gpu_processes(tmp_path, n):
     rec = recs[0]
     assert rec["n_gpus"] == n and rec["value"] > 0 and rec["verified_vs_golden"] is True
     assert sum(rec["stripe_rows"]) == 1536
-    # the three halo schedules differ on device engines: each was timed on the
+    # the four halo schedules differ on device engines: each was timed on the
     # real transport and the verified headline ran the fastest
     # (frames rotate here, so one stream and two alternating ones are both
     # tried; processes sharing one GPU take plain streams only --
@@ -56,7 +56,7 @@ def test_bench_gloo_gpu_processes(tmp_path, n):
     import torch
 
     hs = rec["halo_schedule"]
-    scheds = ("serial", "overlap", "pipeline")
+    scheds = ("serial", "overlap", "pipeline", "batched")
     if n > torch.cuda.device_count():
         assert hs["queues"] == "plain"
         assert set(hs["ms"]) == {f"{s}@{k}" for s in scheds for k in (1, 2)}

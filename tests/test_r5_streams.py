@@ -13,7 +13,7 @@ from mpi_cuda_imagemanipulation_amd import parallel
 def _stand_in(cost):
     from types import SimpleNamespace
 
-    frames = [SimpleNamespace(engine=SimpleNamespace(halo_schedule="serial")) for _ in range(4)]
+    frames = [SimpleNamespace(engine=SimpleNamespace(halo_schedule="serial", posts_halo=True)) for _ in range(4)]
     fs = parallel.FrameStream.__new__(parallel.FrameStream)
     fs.frames = frames
     fs._sets = {"dedicated": ["d0", "d1"], "plain": ["p0", "p1"]}
@@ -29,7 +29,7 @@ def _stand_in(cost):
         applied.append((tuple(fs.streams), n))
 
     fs.set_streams = set_streams
-    fs.step = lambda i=None: time.sleep(cost(frames[0].engine.halo_schedule, fs.nstreams, fs.queues))
+    fs.step = lambda i=None: time.sleep(cost(fs.schedule, fs.nstreams, fs.queues))
     fs.synchronize = lambda: None
     return fs, frames
 
@@ -37,7 +37,7 @@ def _stand_in(cost):
 def test_probe_picks_stream_set():
     # two streams on the pool set are fastest here: the probe must land there
     def cost(sched, n, q):
-        base = {"pipeline": 0.004, "overlap": 0.003, "serial": 0.002}[sched]
+        base = {"pipeline": 0.004, "overlap": 0.003, "serial": 0.002, "batched": 0.0035}[sched]
         return base / 2 if (n == 2 and q == "plain") else base
 
     fs, frames = _stand_in(cost)
@@ -98,3 +98,17 @@ def test_shared_gpu_processes_get_no_dedicated_queues(monkeypatch):
     # RCCL runs one rank per GPU
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
     assert not parallel.FrameStream.shares_gpu(SimpleNamespace(transport="rccl", world=8))
+
+
+def test_batched_schedule_is_a_probe_candidate():
+    # the batched exchange (one group per stream and round) is timed like the
+    # other schedules and kept when fastest
+    def cost(sched, n, q):
+        return 0.001 if (sched == "batched" and n == 2) else 0.003
+
+    fs, frames = _stand_in(cost)
+    got = fs.pick_schedule(steps=2, rounds=1)
+    assert got["chosen"] == "batched" and fs.schedule == "batched" and fs.batched
+    assert all(f.engine.halo_schedule == "serial" for f in frames)  # the engines run serial steps
+    fs.set_schedule("overlap")
+    assert not fs.batched and fs.schedule == "overlap"

@@ -77,7 +77,7 @@ CASES = [("gaussian5", 3), ("emboss3", 1), ("sharpen", 3), ("blur:9", 3)]
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("chain,cc", CASES)
-@pytest.mark.parametrize("schedule", ["serial", "overlap", "pipeline"])
+@pytest.mark.parametrize("schedule", ["serial", "overlap", "pipeline", "batched"])
 @pytest.mark.parametrize("streams", [1, 2])
 def test_self_halo_frame_stream_exact_gpu(rccl_ctx, chain, cc, schedule, streams):
     ctx = rccl_ctx
@@ -95,7 +95,11 @@ def test_self_halo_frame_stream_exact_gpu(rccl_ctx, chain, cc, schedule, streams
         fs.step(i)
     fs.synchronize()
     passes = len(C.plan_info(chain, cc)["passes"])
-    assert ctx.comm.identity()["groups"] - before == n_it * F * passes  # one grouped exchange per pass and step
+    groups = ctx.comm.identity()["groups"] - before
+    if schedule == "batched":  # one group per stream and round: the frames sharing a stream post together
+        assert groups == n_it * min(streams, F)
+    else:
+        assert groups == n_it * F * passes  # one grouped exchange per pass and step
     tol = 1 if any(p["kind"] == 3 for p in C.plan_info(chain, cc)["passes"]) else 0
     for f, fr in enumerate(fs.frames):
         img = C.synth_rows(11 + f, W, cc, 0, H)
@@ -137,3 +141,30 @@ def test_self_halo_engine_timings_gpu(rccl_ctx):
     assert t["halo"] > 0 and t["compute"] > 0
     ref = torus_golden(C.synth_rows(1, 1024, 3, 0, 64), "gaussian5", 3)
     assert (d.result_stripe() == ref).all()
+
+
+@pytest.mark.gpu
+def test_batched_posts_survive_partial_rounds_gpu(rccl_ctx):
+    # a loop that stops mid-round leaves a posted exchange behind; the next
+    # loop (and a plain run, a reload) must neither skip nor double-apply it
+    ctx = rccl_ctx
+    W, H, F = 300, 64, 4
+    fs = parallel.FrameStream(ctx, Pipeline("gaussian5", halo_depth=1, self_halo=True), W, H, 3, frames=F, streams=2,
+                              autotune=False)
+    fs.set_schedule("batched")
+    fs.load_synthetic(3)
+    steps = [0, 1, 2, 0, 1, 2, 3, 0, 1]  # frame 3 posted at step 1, never run in the first loop; loops restart at 0
+    for i in steps:
+        fs.step(i)
+    fs.synchronize()
+    runs = [steps.count(f) + 0 for f in range(F)]  # steps of frame f: every i == f
+    for f, fr in enumerate(fs.frames):
+        ref = torus_golden(C.synth_rows(3 + f, W, 3, 0, H), "gaussian5", runs[f]) if runs[f] else \
+            C.synth_rows(3 + f, W, 3, 0, H)
+        assert (fr.result_stripe() == ref).all() if runs[f] else True, f
+    # a reload invalidates the post: the next step makes its own exchange
+    fs.frames[2].engine.post_halo()
+    fs.frames[2].load_synthetic(9)
+    fs.frames[2].engine.run_posted()
+    fs.synchronize()
+    assert (fs.frames[2].result_stripe() == torus_golden(C.synth_rows(9, W, 3, 0, H), "gaussian5", 1)).all()

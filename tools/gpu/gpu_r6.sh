@@ -97,6 +97,18 @@ blurpst)
     done
   done
   ;;
+batched)
+  # the batched exchange schedule (one group per stream and round): GPU tests,
+  # then the self-halo share with the probe choosing among all schedules,
+  # three processes, and with batched / serial pinned, alternating
+  timeout -k 10 900 python -u -m pytest tests/test_r6_selfhalo.py tests/test_r5_streams.py tests/test_gpu_shared.py -m gpu -q -x --timeout 300 --timeout-method thread > $O/tests.txt 2>&1 || exit 2
+  timeout -k 10 300 python bench.py $SHARE > $O/share_plain.json 2> $O/share_plain.err || exit 3
+  for r in 1 2 3; do
+    timeout -k 10 300 python bench.py $SHARE --self-halo >> $O/share_self_auto.json 2>> $O/share_self_auto.err || exit 3
+    timeout -k 10 300 python bench.py $SHARE --self-halo --halo-schedule batched >> $O/share_self_batched.json 2>> $O/share_self_batched.err || exit 3
+    timeout -k 10 300 python bench.py $SHARE --self-halo --halo-schedule serial >> $O/share_self_serial.json 2>> $O/share_self_serial.err || exit 3
+  done
+  ;;
 *)
   echo "unknown study $S" >&2
   exit 1
