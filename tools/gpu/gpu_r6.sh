@@ -109,6 +109,16 @@ batched)
     timeout -k 10 300 python bench.py $SHARE --self-halo --halo-schedule serial >> $O/share_self_serial.json 2>> $O/share_self_serial.err || exit 3
   done
   ;;
+frames8)
+  # more frames per stream: the batched exchange's groups cover more frames
+  # (4 frames: 2 per stream; 8 frames: 4 per stream), alternating
+  for r in 1 2 3; do
+    for F in 4 8; do
+      timeout -k 10 300 python bench.py $SHARE --self-halo --frames $F >> $O/share_self_f$F.json 2>> $O/share_self_f$F.err || exit 3
+      timeout -k 10 300 python bench.py $SHARE --frames $F >> $O/share_plain_f$F.json 2>> $O/share_plain_f$F.err || exit 3
+    done
+  done
+  ;;
 *)
   echo "unknown study $S" >&2
   exit 1
