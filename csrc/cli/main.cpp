@@ -441,7 +441,7 @@ int cmd_bench(const Args& a) {
       // round-robin, each engine on its own stream (parallel.FrameStream's
       // native counterpart: one frame's kernel boundary overlaps the next)
       const int nframes = scope == "resident" ? std::max(1, a.geti("frames", 1)) : 1;
-      std::vector<double> sched_ms(3, 0.0);  // frames mode: per-schedule step time, max over ranks
+      std::vector<double> sched_ms(4, 0.0);  // frames mode: per-schedule step time, max over ranks
       int chosen = -1;
       auto body = [&](int r) {
         try {
@@ -475,7 +475,8 @@ int cmd_bench(const Args& a) {
             }
             // one GPU per rank (not `local` ranks sharing one): each frame on a
             // stream with a hardware queue of its own (Engine::dedicated_stream)
-            if ((backend != "local" || N == 1) && cfg.backend == BackendKind::Device) {
+            const bool shared_streams = (backend != "local" || N == 1) && cfg.backend == BackendKind::Device;
+            if (shared_streams) {
               const int dev = std::max(0, fr[0]->config().device);
               if (plain_q) {
                 HIP_CHECK(hipSetDevice(dev));
@@ -488,23 +489,54 @@ int cmd_bench(const Args& a) {
             fr[0]->tune();
             for (int f = 1; f < nframes; ++f) fr[f]->set_tuning(fr[0]->bands(), fr[0]->caps(), fr[0]->policies(), fr[0]->orders());
             const bool it_ok = fr[0]->plan().cin == fr[0]->plan().cout;
+            // batched (schedule 3, parallel.FrameStream's "batched"): the frames
+            // sharing a stream post their exchanges as one group per round, at
+            // the first of them; each frame's step then runs without its own
+            const int nstr = shared_streams ? std::min(2, nframes) : 0;
+            const bool batch_ok = nstr > 0 && nframes > nstr;  // the same on every rank
+            bool batched = false;
             auto fstep = [&](int i) {
-              Engine& fe = *fr[(size_t)(i % nframes)];
+              const int k = i % nframes;
+              Engine& fe = *fr[(size_t)k];
               if (!it_ok) fe.rewind();
-              fe.run(1);
+              if (!batched) {
+                fe.run(1);
+                return;
+              }
+              if (k < nstr) {
+                g.comms[r]->group_start();
+                try {
+                  for (int q = k; q < nframes; q += nstr) fr[(size_t)q]->post_halo();
+                } catch (...) {
+                  try {
+                    g.comms[r]->group_end();
+                  } catch (...) {
+                  }
+                  throw;
+                }
+                g.comms[r]->group_end();
+              }
+              fe.run_posted();
             };
             // halo schedule by measurement (bench.py's FrameStream.pick_schedule):
-            // every rank times the same three schedules, the max over ranks
-            // decides; --halo-schedule serial|overlap|pipeline fixes one
+            // every rank times the same schedules, the max over ranks decides;
+            // --halo-schedule serial|overlap|pipeline|batched fixes one
             const std::string hs = a.get("halo-schedule", "auto");
             if (hs != "auto") {
-              STRIPE_CHECK(hs == "serial" || hs == "overlap" || hs == "pipeline",
-                           "--halo-schedule must be auto, serial, overlap or pipeline");
-              for (auto& fe : fr) fe->set_halo_schedule(hs == "serial" ? 0 : hs == "overlap" ? 1 : 2);
+              STRIPE_CHECK(hs == "serial" || hs == "overlap" || hs == "pipeline" || hs == "batched",
+                           "--halo-schedule must be auto, serial, overlap, pipeline or batched");
+              batched = hs == "batched" && batch_ok;
+              for (auto& fe : fr) fe->set_halo_schedule(hs == "serial" || hs == "batched" ? 0 : hs == "overlap" ? 1 : 2);
             } else if (N > 1 && backend != "host") {
               const int m = std::max(20, 4 * nframes);
-              for (int sc = 0; sc < 3; ++sc) {
-                for (auto& fe : fr) fe->set_halo_schedule(sc);
+              for (int sc = 0; sc < 4; ++sc) {
+                if (sc == 3 && !batch_ok) {
+                  std::lock_guard<std::mutex> lk(mu);
+                  sched_ms[3] = 1e30;
+                  continue;
+                }
+                batched = sc == 3;
+                for (auto& fe : fr) fe->set_halo_schedule(sc == 3 ? 0 : sc);
                 for (int i = 0; i < 2 * nframes; ++i) fstep(i);
                 for (auto& fe : fr) fe->synchronize();
                 g.comms[r]->barrier();
@@ -520,11 +552,12 @@ int cmd_bench(const Args& a) {
               int best = 0;
               {
                 std::lock_guard<std::mutex> lk(mu);
-                for (int sc = 1; sc < 3; ++sc)
+                for (int sc = 1; sc < 4; ++sc)
                   if (sched_ms[(size_t)sc] < sched_ms[(size_t)best]) best = sc;
                 chosen = best;
               }
-              for (auto& fe : fr) fe->set_halo_schedule(best);
+              batched = best == 3;
+              for (auto& fe : fr) fe->set_halo_schedule(best == 3 ? 0 : best);
             }
             for (int i = 0; i < warmup; ++i) fstep(i);
             for (auto& fe : fr) fe->synchronize();
@@ -604,13 +637,15 @@ int cmd_bench(const Args& a) {
       double ms = 0;
       for (double v : per_rank) ms = std::max(ms, v);
       const double mpx = (double)W * H / (ms * 1e-3) / 1e6;
-      static const char* kSched[] = {"serial", "overlap", "pipeline"};
-      char sched[160];
+      static const char* kSched[] = {"serial", "overlap", "pipeline", "batched"};
+      char sched[200];
+      char bat[40] = "";  // batched: only where it was a candidate
+      if (sched_ms[3] < 1e29) std::snprintf(bat, sizeof bat, ",\"batched\":%.5f", sched_ms[3]);
       if (chosen >= 0)
         std::snprintf(sched, sizeof sched,
                       ",\"halo_schedule\":{\"chosen\":\"%s\",\"ms\":{\"serial\":%.5f,\"overlap\":%.5f,"
-                      "\"pipeline\":%.5f}}",
-                      kSched[chosen], sched_ms[0], sched_ms[1], sched_ms[2]);
+                      "\"pipeline\":%.5f%s}}",
+                      kSched[chosen], sched_ms[0], sched_ms[1], sched_ms[2], bat);
       else
         sched[0] = '\0';
       char buf[768];
