@@ -827,14 +827,29 @@ def main():
                 eng.host_input()[...] = C.synth_rows(a.seed, W, Cc, row0, rows)
             eng.run_e2e(8)
             eng.synchronize()
+            # row chunks of the upload / filter / download pipeline: its fill
+            # and drain cost about one chunk each way, so more chunks pay where
+            # the link overlaps the two directions and cost per-chunk overhead
+            # where it does not (profiles/r5/e2e/): time 8 and 16 (max over
+            # ranks), keep the faster
+            chunk_ms = {}
+            for ch in (8, 16):
+                barrier()
+                t0 = time.perf_counter()
+                for _ in range(2):
+                    eng.run_e2e(ch)
+                eng.synchronize()
+                chunk_ms[ch] = max_over_ranks((time.perf_counter() - t0) * 1e3 / 2)
+            chunks = min(chunk_ms, key=chunk_ms.get)
             barrier()
             t0 = time.perf_counter()
             for _ in range(a.e2e_steps):
-                eng.run_e2e(8)
+                eng.run_e2e(chunks)
             eng.synchronize()
             barrier()
             ems = max_over_ranks((time.perf_counter() - t0) * 1e3) / a.e2e_steps
-            scopes["e2e"] = {"mpx_s": round(W * H / (ems * 1e-3) / 1e6, 1), "ms": round(ems, 5)}
+            scopes["e2e"] = {"mpx_s": round(W * H / (ems * 1e-3) / 1e6, 1), "ms": round(ems, 5), "chunks": chunks,
+                             "chunk_probe_ms": {str(k): round(v, 3) for k, v in chunk_ms.items()}}
             stages["e2e"] = {k: round(v, 4) for k, v in dp.stage_times().items()
                              if k in ("h2d", "compute", "halo", "d2h", "e2e")}
             if rows > 0:
