@@ -15,7 +15,7 @@
 //               leaves each lane with 4 consecutive output pixels of one row
 //               (RGB: 12 interleaved bytes, one dwordx3 store).
 //
-// Precision: u8 inputs are exact in f16; weights and X are split into f16
+// Precision: u8 inputs are exact in f16 (as subnormals, below); weights and X are split into f16
 // hi + lo parts (2 MFMAs for the horizontal pass, 3 for the vertical), so the
 // f32 result is within ~1e-5 of the f64 golden (conv
 // passes match within 1 LSB, ties only).  The ":lsb" mode (LSB below) takes
@@ -59,6 +59,7 @@ struct SepArgs {
   int R, L, nstrips;
   int a0, a2;  // group-grid origins of ranges 0 / 1 (global row multiple of 32)
   float bias;  // LSB mode: 128 * sum(h) * sum(v), the x - 128 shift of the input
+  float hinit;  // LSB: horizontal accumulator start, -128 * sum(scaled h) * 2^-24 (the centring)
 };
 
 __device__ __forceinline__ void sep_lds_sync() {
@@ -90,15 +91,17 @@ __device__ __forceinline__ uint32_t pack_u8x4(f4 v) {
   return o;
 }
 
-// 2 input bytes -> 2 exact f16 (one dword): (1024 + b) built by byte permute,
-// minus 1024 (b), or minus 1152 (b - 128, the centred input of the LSB mode).
-template <bool CENTRED = false>
-__device__ __forceinline__ uint32_t bytes_to_h2(uint32_t d, uint32_t sel) {
-  const uint32_t biased = __builtin_amdgcn_perm(0x64646464u, d, sel);
-  half2v h = __builtin_bit_cast(half2v, biased);
-  constexpr _Float16 k = CENTRED ? (_Float16)1152.0f : (_Float16)1024.0f;
-  h = h - half2v{k, k};
-  return __builtin_bit_cast(uint32_t, h);
+// Subnormal staging: byte b becomes the f16 bit pattern 0x00bb, the exact
+// subnormal b * 2^-24 (the MFMA keeps f16 subnormal inputs), so a pair of
+// bytes is ONE v_perm (zero high bytes from selector 0x0C).  The horizontal
+// weights are stored scaled by 2^(24 - e) and the vertical ones by 2^e
+// (prepare_sep_consts), so X and the output keep their units; the LSB mode's
+// x - 128 centring is the horizontal accumulator's start value.  (Round 6:
+// replaced (1024 + b) f16 built by a perm and a packed subtract per pair --
+// 2.5x the staging VALU; 1-3 % faster on every shape, profiles/r6/subn/.)
+// RGB: d0 d1 d2 = R0 G0 B0 R1 | G1 B1 R2 G2 | B2 R3 G3 B3.
+__device__ __forceinline__ uint32_t sub_pair(uint32_t hi, uint32_t lo, uint32_t sel) {
+  return __builtin_amdgcn_perm(hi, lo, sel);
 }
 
 // 2 f32 -> 2 f16, round to nearest even (the LSB mode's single-part X).
@@ -109,8 +112,8 @@ __device__ __forceinline__ uint32_t f32x2_to_h2(float x, float y) {
 
 // Planar kernel.  A wave owns a strip of NX x-tiles of 16 pixels (all C
 // channels) and a band of rows.  Each 32-row X pair is staged into LDS as C
-// f16 channel PLANES (RGB is de-interleaved while staging: 3 gathers + 6
-// biased byte->f16 perms per 4 pixels), so the horizontal Toeplitz product of
+// f16 channel PLANES (RGB is de-interleaved while staging: 6 byte->subnormal
+// f16 perms per 4 pixels), so the horizontal Toeplitz product of
 // one channel needs a 64-pixel window per 16 outputs: 2 k-steps instead of the
 // 4 k-steps a 128-byte interleaved window takes (RGB: 8 horizontal MFMAs per
 // 16 output bytes instead of 16, 20 in all instead of 28).  The vertical
@@ -289,29 +292,19 @@ __global__ __launch_bounds__(blur_threads(NW), OCC * 256 / blur_threads(NW)) voi
       if (!unit_ok(i)) continue;  // idle lanes of the last load (lane-divergent, LDS only)
       const int dst = (srow[i % P] + RSTEP * (i / P)) * G::STRIDE + 2 * scol[i % P];
       if constexpr (C == 3) {
-        // bytes R0 G0 B0 R1 | G1 B1 R2 G2 | B2 R3 G3 B3 -> three planes of 4 f16
         const uint32_t d0 = pf[B][i].x, d1 = pf[B][i].y, d2 = pf[B][i].z;
-        const uint32_t p01 = __builtin_amdgcn_perm(d1, d0, 0x04010300u);  // R0 R1 G0 G1
-        const uint32_t p12 = __builtin_amdgcn_perm(d2, d1, 0x06030502u);  // R2 R3 G2 G3
-        const uint32_t pb = __builtin_amdgcn_perm(d2, d1, 0x07040401u);   // B1 B2 -- B3 (byte 2 unused)
-        const uint32_t r01 = bytes_to_h2<LSB>(p01, 0x04010400u), g01 = bytes_to_h2<LSB>(p01, 0x04030402u);
-        const uint32_t r23 = bytes_to_h2<LSB>(p12, 0x04010400u), g23 = bytes_to_h2<LSB>(p12, 0x04030402u);
-        const uint32_t b01 = bytes_to_h2<LSB>(__builtin_amdgcn_perm(d0, pb, 0x00000006u), 0x04010400u);  // B0 B1
-        const uint32_t b23 = bytes_to_h2<LSB>(pb, 0x04030401u);                                         // B2 B3
+        const uint32_t r01 = sub_pair(d1, d0, 0x0C030C00u), r23 = sub_pair(d2, d1, 0x0C050C02u);
+        const uint32_t g01 = sub_pair(d1, d0, 0x0C040C01u), g23 = sub_pair(d2, d1, 0x0C060C03u);
+        const uint32_t b01 = sub_pair(d1, d0, 0x0C050C02u), b23 = sub_pair(d2, d1, 0x0C070C04u);
         *reinterpret_cast<u2*>(wl + dst) = u2{r01, r23};
         *reinterpret_cast<u2*>(wl + G::PLANE + dst) = u2{g01, g23};
         *reinterpret_cast<u2*>(wl + 2 * G::PLANE + dst) = u2{b01, b23};
       } else {
         const u4 d = pf[B][i];
-        u4 lo, hi;
-        lo.x = bytes_to_h2<LSB>(d.x, 0x04010400u);
-        lo.y = bytes_to_h2<LSB>(d.x, 0x04030402u);
-        lo.z = bytes_to_h2<LSB>(d.y, 0x04010400u);
-        lo.w = bytes_to_h2<LSB>(d.y, 0x04030402u);
-        hi.x = bytes_to_h2<LSB>(d.z, 0x04010400u);
-        hi.y = bytes_to_h2<LSB>(d.z, 0x04030402u);
-        hi.z = bytes_to_h2<LSB>(d.w, 0x04010400u);
-        hi.w = bytes_to_h2<LSB>(d.w, 0x04030402u);
+        const u4 lo = {sub_pair(d.x, d.x, 0x0C010C00u), sub_pair(d.x, d.x, 0x0C030C02u),
+                       sub_pair(d.y, d.y, 0x0C010C00u), sub_pair(d.y, d.y, 0x0C030C02u)};
+        const u4 hi = {sub_pair(d.z, d.z, 0x0C010C00u), sub_pair(d.z, d.z, 0x0C030C02u),
+                       sub_pair(d.w, d.w, 0x0C010C00u), sub_pair(d.w, d.w, 0x0C030C02u)};
         *reinterpret_cast<u4*>(wl + dst) = lo;
         *reinterpret_cast<u4*>(wl + dst + 16) = hi;
       }
@@ -375,8 +368,9 @@ __global__ __launch_bounds__(blur_threads(NW), OCC * 256 / blur_threads(NW)) voi
     };
     // horizontal: X tiles of rows 0..15 and 16..31 of the pair
     auto hmfma = [&](const half8 (&f)[2][2], f4 (&x)[2]) __attribute__((always_inline)) {
-      x[0] = f4{0.f, 0.f, 0.f, 0.f};
-      x[1] = f4{0.f, 0.f, 0.f, 0.f};
+      const float x0 = LSB ? sa.hinit : 0.f;
+      x[0] = f4{x0, x0, x0, x0};
+      x[1] = f4{x0, x0, x0, x0};
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -505,11 +499,26 @@ __global__ __launch_bounds__(blur_threads(NW), OCC * 256 / blur_threads(NW)) voi
 
 }  // namespace dev
 
+// Weight scaling of the subnormal staging: horizontal weights x 2^kexp,
+// vertical x 2^(24 - kexp), kexp the largest shift keeping every scaled
+// horizontal weight <= 2^15 (hi + lo parts normal f16, well inside the f16
+// range).  False when the vertical weights would then leave that range too
+// (max|h| * max|v| > 64: such a sepconv runs on the general conv kernel).
+static bool sep_scale(const Pass& p, int* kexp_out) {
+  double maxh = 0, maxv = 0;
+  for (float w : p.sep_h) maxh = std::max(maxh, std::fabs((double)w));
+  for (float w : p.sep_v) maxv = std::max(maxv, std::fabs((double)w));
+  int kexp = 24;
+  while (kexp > 0 && maxh * std::ldexp(1.0, kexp) > 32768.0) --kexp;
+  if (kexp_out) *kexp_out = kexp;
+  return maxh * std::ldexp(1.0, kexp) <= 32768.0 && maxv * std::ldexp(1.0, 24 - kexp) <= 32768.0;
+}
+
 bool sep_supported(const Pass& p) {
   // planar kernel: 64-pixel horizontal window per 16 outputs (R <= 16) and the
   // 48-byte left reach of the staged window within the buffers' x-margin
   return !p.sep_h.empty() && p.sep_v.size() == p.sep_h.size() && (p.cmid == 1 || p.cmid == 3) && p.R <= 16 &&
-         16 * p.cmid <= kMarginBytes;
+         16 * p.cmid <= kMarginBytes && sep_scale(p, nullptr);
 }
 
 // Per-lane weight fragments.  Lane l (g = l >> 4, n = l & 15), element j:
@@ -561,6 +570,10 @@ void prepare_sep_consts(const Pass& p, PassConsts* pc, hipStream_t s) {
       STRIPE_LOG(Info, -1, "blur" << K << " lsb: f16 weights could miss by " << bound << " LSB, using hi + lo parts");
     }
   }
+  // subnormal staging: weights scaled by sep_scale's powers of two
+  int kexp = 24;
+  sep_scale(p, &kexp);
+  const float hs = (float)std::ldexp(1.0, kexp), vs = (float)std::ldexp(1.0, 24 - kexp);
   std::vector<_Float16> host((size_t)dev::kSepEntries * 64 * 8, (_Float16)0.f);
   auto put = [&](int e, int lane, int j, float w, int hl) {
     const _Float16 whi = (_Float16)w;
@@ -572,18 +585,23 @@ void prepare_sep_consts(const Pass& p, PassConsts* pc, hipStream_t s) {
     for (int j = 0; j < 8; ++j) {
       for (int sidx = 0; sidx < 2; ++sidx) {
         const int t = 32 * sidx + 8 * g + j - 16 - n + R;
-        const float w = (t >= 0 && t < K) ? p.sep_h[(size_t)t] : 0.f;
+        const float w = (t >= 0 && t < K) ? p.sep_h[(size_t)t] * hs : 0.f;
         for (int hl = 0; hl < 2; ++hl) put(sidx * 2 + hl, lane, j, w, hl);
       }
       for (int q = 0; q < 2; ++q)
         for (int sidx = 0; sidx < 2; ++sidx) {
           const int hr = 32 * sidx + 16 * (j >> 2) + 4 * g + (j & 3);
           const int t = hr - 16 - 16 * q - n + R;
-          const float w = (t >= 0 && t < K) ? p.sep_v[(size_t)t] : 0.f;
+          const float w = (t >= 0 && t < K) ? p.sep_v[(size_t)t] * vs : 0.f;
           for (int hl = 0; hl < 2; ++hl) put(4 + q * 4 + sidx * 2 + hl, lane, j, w, hl);
         }
     }
   }
+  // LSB: X = sum h~ (b - 128) = sum h~ b - 128 sum h~, h~ the (scaled) f16
+  // weights the MFMA multiplies: the shift is the accumulator's start value
+  double shs = 0;
+  for (float w : p.sep_h) shs += (double)(float)(_Float16)(w * hs);
+  pc->sep_hinit = -128.0 * shs * std::ldexp(1.0, -24);
   pc->conv_bytes = host.size() * sizeof(_Float16);
   HIP_CHECK(hipMalloc(&pc->conv, pc->conv_bytes));
   HIP_CHECK(hipMemcpyAsync(pc->conv, host.data(), pc->conv_bytes, hipMemcpyHostToDevice, s));
@@ -633,7 +651,6 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
   a.in_zero = (uint32_t)L.in_zero;
   a.out_bytes = (uint32_t)L.out_bytes;
   a.out_org = (uint32_t)L.out_org;
-  sa.tw = reinterpret_cast<const dev::u4*>(pc.conv);
   sa.R = p.R;
   sa.L = 16 * p.cmid;
   // kernel configuration: x-tiles per strip, pairs prefetched ahead, waves per
@@ -679,6 +696,8 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
   // latency than they save)
   const bool lsb = pc.conv_mode == 2 && p.cmid == 3;
   sa.bias = (float)pc.conv_bias;
+  sa.hinit = (float)pc.sep_hinit;
+  sa.tw = reinterpret_cast<const dev::u4*>(pc.conv);
   // A/B variants of the RGB non-edge kernel (STRIPE_BLUR_VARIANT=n): 1 = two
   // independent 4-wave workgroups per CU (NW 4, two pairs in flight), 2 = the
   // same with one pair in flight, 3 = the 8-wave windows staging each pair

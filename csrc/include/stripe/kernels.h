@@ -36,6 +36,7 @@ struct PassConsts {
   int conv_mode = 0;         // general conv: 0 f16 hi+lo row pairs, 1 i8 weight digits (k_conv_i8)
   double conv_scale = 0;     // i8 digits: weights = W_int * conv_scale (a power of two)
   double conv_bias = 0;      // i8 digits: 128 * sum(W_int) * conv_scale (the x - 128 shift)
+  double sep_hinit = 0;      // separable blur, subnormal staging: horizontal accumulator start (lsb centring)
 };
 
 struct PassLaunch {

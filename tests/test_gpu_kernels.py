@@ -112,6 +112,24 @@ def test_mfma_sepconv_asymmetric(m, rng, C, K):
     assert d.max() <= 1 and (d != 0).sum() <= max(2, d.size // 2000), (d.max(), (d != 0).sum())
 
 
+@pytest.mark.parametrize("scale", [8.0, 16.0])
+def test_mfma_sepconv_large_weights(m, rng, scale):
+    # the separable kernel stages bytes as f16 subnormals and scales the
+    # weights by powers of two (h x 2^k, v x 2^(24-k)): max|h| * max|v| <= 64
+    # stays on it (scale 8), larger products run on the general conv kernel
+    # (scale 16); both must match the golden path
+    K = 5
+    h = rng.uniform(0.25, 1.0, K) * scale
+    v = rng.uniform(0.25, 1.0, K) * scale
+    h[K // 2] = v[K // 2] = scale
+    chain = f"sepconv:{K}:" + ";".join(repr(float(x)) for x in h) + ":" + ";".join(repr(float(x)) for x in v)
+    img = (rng.integers(0, 256, size=(48, 200, 3), dtype=np.uint8) % 3 == 0).astype(np.uint8)
+    got = _run(m, img, chain, "reflect101")
+    ref = m._C.golden_apply(img, chain, "reflect101", True)
+    d = np.abs(got.astype(int) - ref.astype(int))
+    assert d.max() <= 1 and (d != 0).sum() <= max(2, d.size // 2000), (scale, d.max(), (d != 0).sum())
+
+
 def test_mfma_sep_matches_general_conv(m, rng):
     # the same rank-one window through the separable and the general (Toeplitz) MFMA kernels
     K = 9

@@ -12,6 +12,8 @@
 #             device copies (STRIPE_SELF_HALO_COPY); blur:31 wave-priority
 #             variants and conv:31 k-loop scheduling variants (A/B,
 #             alternating), each variant's numerics checked first   -> r6/batch1
+#   subn / subn2  blur:31 subnormal staging A/B                   -> r6/subn*
+#   valu      the separable-VALU blur comparator beside the MFMA kernel -> r6/valu
 #   local     the `local` hub's halo rounds: GPU tests of every local-rank
 #             path, then 4 local ranks on 8192^2 gray sobel at halo depth 1
 #             (rounds vs grouped send / receive, each halo schedule) and at
@@ -95,6 +97,44 @@ blurpst)
       STRIPE_BLUR_VARIANT=$v timeout -k 10 120 python tools/kbench.py --chains "blur:31|blur:31:lsb" --shape 16384x16384x3 --iters 30 >> $O/blur_v${v}_16k.txt 2>&1 || exit 4
       STRIPE_BLUR_VARIANT=$v timeout -k 10 120 python tools/kbench.py --chains "blur:31|blur:31:lsb" --shape 16384x2048x3 --iters 60 >> $O/blur_v${v}_stripe.txt 2>&1 || exit 4
     done
+  done
+  ;;
+subn)
+  # subnormal staging (STRIPE_BLUR_VARIANT=4 early / 5 late staging): numerics
+  # first, then A/B with the default, alternating
+  for v in 4 5; do
+    STRIPE_BLUR_VARIANT=$v timeout -k 10 600 python -u -m pytest tests/test_oracle_conv.py tests/test_gpu_large.py -m gpu -q -x --timeout 200 --timeout-method thread > $O/tests_v$v.txt 2>&1 || exit 2
+  done
+  for r in 1 2 3; do
+    for v in 0 4 5; do
+      STRIPE_BLUR_VARIANT=$v timeout -k 10 120 python tools/kbench.py --chains "blur:31|blur:31:lsb" --shape 16384x16384x3 --iters 30 >> $O/blur_v${v}_16k.txt 2>&1 || exit 4
+      STRIPE_BLUR_VARIANT=$v timeout -k 10 120 python tools/kbench.py --chains "blur:31|blur:31:lsb" --shape 16384x2048x3 --iters 60 >> $O/blur_v${v}_stripe.txt 2>&1 || exit 4
+    done
+  done
+  ;;
+subn2)
+  # subnormal staging as the default of every blur instance: the blur GPU
+  # tests, then A/B against the biased staging (STRIPE_BLUR_VARIANT=9) on
+  # RGB, gray and W % 4 != 0 frames, alternating
+  timeout -k 10 600 python -u -m pytest tests/test_oracle_conv.py tests/test_gpu_large.py tests/test_gpu_kernels.py -m gpu -q -x --timeout 200 --timeout-method thread > $O/tests.txt 2>&1 || exit 2
+  for r in 1 2 3; do
+    for v in 0 9; do
+      STRIPE_BLUR_VARIANT=$v timeout -k 10 120 python tools/kbench.py --chains "blur:31|blur:31:lsb" --shape 16384x16384x3 --iters 30 >> $O/blur_v${v}_16k.txt 2>&1 || exit 4
+      STRIPE_BLUR_VARIANT=$v timeout -k 10 120 python tools/kbench.py --chains "blur:31|blur:31:lsb" --shape 16384x2048x3 --iters 60 >> $O/blur_v${v}_stripe.txt 2>&1 || exit 4
+      STRIPE_BLUR_VARIANT=$v timeout -k 10 120 python tools/kbench.py --chains "blur:31" --shape 16384x16384x1 --iters 30 >> $O/blur_v${v}_gray.txt 2>&1 || exit 4
+      STRIPE_BLUR_VARIANT=$v timeout -k 10 120 python tools/kbench.py --chains "blur:31|blur:31:lsb" --shape 16383x4099x3 --iters 60 >> $O/blur_v${v}_edge.txt 2>&1 || exit 4
+    done
+  done
+  ;;
+valu)
+  # the separable-VALU comparator beside the MFMA kernel, and
+  # the blur / sepconv GPU tests of the subnormal staging
+  timeout -k 10 600 python -u -m pytest tests/test_oracle_conv.py tests/test_gpu_kernels.py -m gpu -q -x --timeout 200 --timeout-method thread > $O/tests.txt 2>&1 || exit 2
+  for r in 1 2; do
+    timeout -k 10 120 bin/blur_valu 16384 16384 10 >> $O/valu_16k.txt 2>&1 || exit 3
+    timeout -k 10 120 bin/blur_valu 16384 2048 40 >> $O/valu_stripe.txt 2>&1 || exit 3
+    timeout -k 10 120 python tools/kbench.py --chains "blur:31|blur:31:lsb" --shape 16384x16384x3 --iters 30 >> $O/mfma_16k.txt 2>&1 || exit 4
+    timeout -k 10 120 python tools/kbench.py --chains "blur:31|blur:31:lsb" --shape 16384x2048x3 --iters 60 >> $O/mfma_stripe.txt 2>&1 || exit 4
   done
   ;;
 batched)
