@@ -13,6 +13,8 @@
 #             variants and conv:31 k-loop scheduling variants (A/B,
 #             alternating), each variant's numerics checked first   -> r6/batch1
 #   subn / subn2  blur:31 subnormal staging A/B                   -> r6/subn*
+#   prof      rocprofv3 kernel traces of the final bench / self-halo share,
+#             blur:31 counters                                     -> r6/prof
 #   valu      the separable-VALU blur comparator beside the MFMA kernel -> r6/valu
 #   local     the `local` hub's halo rounds: GPU tests of every local-rank
 #             path, then 4 local ranks on 8192^2 gray sobel at halo depth 1
@@ -136,6 +138,14 @@ valu)
     timeout -k 10 120 python tools/kbench.py --chains "blur:31|blur:31:lsb" --shape 16384x16384x3 --iters 30 >> $O/mfma_16k.txt 2>&1 || exit 4
     timeout -k 10 120 python tools/kbench.py --chains "blur:31|blur:31:lsb" --shape 16384x2048x3 --iters 60 >> $O/mfma_stripe.txt 2>&1 || exit 4
   done
+  ;;
+prof)
+  # kernel traces of the final headline bench (N=1) and of the self-halo N=8
+  # share; counters of blur:31 / blur:31:lsb after the subnormal staging
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_n1 -o n1 -- python3 bench.py --steps 20 --warmup 5 --dist-steps 0 --ref-steps 0 --e2e-steps 0 --deep-steps 0 > $O/prof_n1.log 2>&1 || exit 3
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_self -o self -- python3 bench.py $SHARE --self-halo --steps 50 > $O/prof_self.log 2>&1 || exit 3
+  timeout -k 10 900 bash scripts/profile.sh "blur:31:lsb" 16384x16384x3 gpurun_out/r6/prof/blur_lsb > $O/blur_lsb.txt 2>&1 || exit 4
+  timeout -k 10 900 bash scripts/profile.sh "blur:31" 16384x16384x3 gpurun_out/r6/prof/blur_exact > $O/blur_exact.txt 2>&1 || exit 4
   ;;
 batched)
   # the batched exchange schedule (one group per stream and round): GPU tests,
