@@ -147,6 +147,16 @@ prof)
   timeout -k 10 900 bash scripts/profile.sh "blur:31:lsb" 16384x16384x3 gpurun_out/r6/prof/blur_lsb > $O/blur_lsb.txt 2>&1 || exit 4
   timeout -k 10 900 bash scripts/profile.sh "blur:31" 16384x16384x3 gpurun_out/r6/prof/blur_exact > $O/blur_exact.txt 2>&1 || exit 4
   ;;
+dma)
+  # LDS-DMA ring blur kernel (STRIPE_BLUR_VARIANT=4): numerics first, then A/B
+  STRIPE_BLUR_VARIANT=4 timeout -k 10 300 python -u -m pytest tests/test_oracle_conv.py tests/test_gpu_large.py tests/test_gpu_kernels.py -m gpu -q -x -k "blur or sep" --timeout 120 --timeout-method thread > $O/tests_v4.txt 2>&1 || exit 2
+  for r in 1 2 3; do
+    for v in 0 4; do
+      STRIPE_BLUR_VARIANT=$v timeout -k 10 120 python tools/kbench.py --chains "blur:31|blur:31:lsb" --shape 16384x16384x3 --iters 30 >> $O/blur_v${v}_16k.txt 2>&1 || exit 4
+      STRIPE_BLUR_VARIANT=$v timeout -k 10 120 python tools/kbench.py --chains "blur:31|blur:31:lsb" --shape 16384x2048x3 --iters 60 >> $O/blur_v${v}_stripe.txt 2>&1 || exit 4
+    done
+  done
+  ;;
 batched)
   # the batched exchange schedule (one group per stream and round): GPU tests,
   # then the self-halo share with the probe choosing among all schedules,
