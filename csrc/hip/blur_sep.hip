@@ -498,319 +498,6 @@ __global__ __launch_bounds__(blur_threads(NW), OCC * 256 / blur_threads(NW)) voi
 }
 
 
-// LDS-DMA variant (A/B, STRIPE_BLUR_VARIANT=4): RGB, 8 waves sharing one
-// window of 2-tile strips.  The raw window bytes of each 32-row pair arrive
-// through buffer_load ... lds (no VGPR destination) in a ring of 3 LDS slots,
-// three pairs ahead; each step waits for its own slot with a counted vmcnt,
-// converts it into the single f16 plane buffer between two raw barriers, then
-// re-issues the slot for pair k + 3 and runs the pair's MFMAs.  LDS: 57 KiB of
-// planes + 3 x 32 KiB slots (29184 B of raw rows each, padded to whole 1 KiB
-// DMA pieces).
-constexpr int kDmaSlot = 32768;
-
-// One 1 KiB LDS-DMA piece: buffer_load_dwordx4 ... lds, lane l's 16 bytes to
-// LDS byte lds_addr + 16 l (lds_addr wave-uniform, in M0).  Inline asm, so the
-// compiler does not track it: hipcc treats a pending LDS DMA as aliasing every
-// later LDS read and waited for all three slots before each step's staging
-// (vmcnt(4)), collapsing the ring to one pair ahead.  The kernel counts the
-// pieces itself (wait_vm).  M0 is saved and restored around the piece.
-__device__ __forceinline__ void dma_piece(__amdgpu_buffer_rsrc_t rsrc, uint32_t lds_addr, uint32_t voff) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %1\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %2, %3, 0 offen lds\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "s"(lds_addr), "v"(voff), "s"(rsrc)
-      : "memory");
-}
-
-// s_waitcnt vmcnt(N) (inline asm: the compiler's own wait insertion never
-// sees the DMA pieces, so it would not merge or strengthen this one)
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-template <bool LSB>
-__global__ __launch_bounds__(512, 1) void k_blur_dma(SepArgs sa) {
-  constexpr int C = 3, NX = 2, NW = 8;
-  using G = PlGeom<C, NX, NW>;
-  constexpr int RB = G::WPX * C;                 // raw row bytes (912)
-  constexpr int NDMA = kDmaSlot / 1024 / NW;     // 1 KiB DMA pieces per wave per pair (4)
-  static_assert(32 * RB <= kDmaSlot && RB % 16 == 0 && G::TILE % 16 == 0, "raw slot geometry");
-  constexpr int LPL = G::LPL;                    // staging units (4 px) per lane per pair
-  const KArgs& a = sa.a;
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  uint8_t* const wt = lds;                       // f16 planes (single buffer)
-  uint8_t* const raw = lds + G::TILE;            // 3 raw slots
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int sl = threadIdx.x;
-  const int nsg = (sa.nstrips + NW - 1) / NW;
-  const int gt = xcd_remap((int)blockIdx.x, (int)gridDim.x, a.nxcd);
-  if (gt >= nsg * a.nbands) return;  // workgroup-uniform
-  const int by = gt / nsg, sgx = (gt % nsg) * NW, strip = sgx + wave;
-  int base, ys, ye;
-  if (by < a.nb0) {
-    base = sa.a0 + by * a.band;
-    ys = max(base, a.ry0);
-    ye = min(base + a.band, a.ry1);
-  } else {
-    base = sa.a2 + (by - a.nb0) * a.band;
-    ys = max(base, a.ry2);
-    ye = min(base + a.band, a.ry3);
-  }
-  const int R = sa.R;
-  constexpr int NHL = LSB ? 1 : 2;
-  half8 bh[2][NHL], bv[2][2][NHL];
-#pragma unroll
-  for (int s = 0; s < 2; ++s)
-#pragma unroll
-    for (int hl = 0; hl < NHL; ++hl) bh[s][hl] = __builtin_bit_cast(half8, sa.tw[(s * 2 + hl) * 64 + lane]);
-#pragma unroll
-  for (int q = 0; q < 2; ++q)
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int hl = 0; hl < NHL; ++hl)
-        bv[q][s][hl] = __builtin_bit_cast(half8, sa.tw[(4 + q * 4 + s * 2 + hl) * 64 + lane]);
-  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);
-  const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
-  const int lo_ok = max(-R, -a.row0);
-  const int hi_ok = min(a.rows - 1 + R, a.Hg - 1 - a.row0);
-  const int sx = strip * G::PX;
-  const int wx = sgx * G::PX - 16;
-  const int m = lane & 15, g = lane >> 4;
-  const int yh0 = base - 16;
-  const int ngroups = (ye - base + 31) >> 5;
-
-  // DMA pieces: piece i of this wave covers slot bytes [1024 (NDMA wave + i), +1024),
-  // lane-linear: raw row o / RB, byte o % RB of the window
-  // (the raw rows of a lane's pieces: o = 1024 (NDMA wave + i) + 16 lane ->
-  // row o / RB, byte o % RB; recomputed per issue)
-  auto issue = [&](int p, int S) __attribute__((always_inline)) {
-    const int yt = yh0 + 32 * p;
-    const bool exists = p <= ngroups;  // pairs 0 .. ngroups; later issues keep the counts uniform
-    uint32_t off[NDMA];
-    int ln = lane;
-    asm volatile("" : "+v"(ln));  // keep the per-lane offsets out of loop-invariant registers
-    if (__builtin_expect(yt >= lo_ok && yt + 31 <= hi_ok, 1)) {
-      // interior pair (wave-uniform branch)
-      const uint32_t sb = a.in_org + (uint32_t)((int64_t)yt * a.in_pitch);
-#pragma unroll
-      for (int i = 0; i < NDMA; ++i) {
-        const int o = 1024 * (NDMA * wave + i) + 16 * ln;
-        const int row = o / RB;
-        const uint32_t v = sb + (uint32_t)(row * a.in_pitch) + (uint32_t)(wx * C + o % RB);
-        off[i] = (exists && row < 32) ? v : kOOB;
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < NDMA; ++i) {
-        const int o = 1024 * (NDMA * wave + i) + 16 * ln;
-        const int row = o / RB;
-        // rows beyond the stripe + halo feed only zero weights: clamp, then border-map
-        const int y = min(max(yt + row, -R), a.rows - 1 + R);
-        const uint32_t v = in_row_off(a, y) + (uint32_t)(wx * C + o % RB);
-        off[i] = (exists && row < 32) ? v : kOOB;
-      }
-    }
-    const uint32_t slot_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)(raw + S * kDmaSlot);
-#pragma unroll
-    for (int i = 0; i < NDMA; ++i)
-      dma_piece(rin, __builtin_amdgcn_readfirstlane(slot_lds + 1024 * (NDMA * wave + i)), off[i]);
-  };
-  // staging units: unit u = sl + 512 i -> pair row u / U, 4 pixels at 4 (u % U)
-  // (recomputed per step: registers are the scarce resource here)
-  auto stage = [&](int S) __attribute__((always_inline)) {
-    const uint8_t* rs = raw + S * kDmaSlot;
-    int su = sl;
-    asm volatile("" : "+v"(su));  // recomputed per step (see issue)
-    __builtin_assume(su >= 0 && su < 512);
-#pragma unroll
-    for (int i = 0; i < LPL; ++i) {
-      const int u = su + 512 * i;
-      const int row = u / G::U, uc = u % G::U;
-      if (row >= 32) continue;  // only the last unit's idle lanes (lane-divergent, LDS only)
-      const uint32_t rsrc_off = (uint32_t)(row * RB + 12 * uc), pdst = (uint32_t)(row * G::STRIDE + 8 * uc);
-      const uint32_t* src = reinterpret_cast<const uint32_t*>(rs + rsrc_off);
-      const uint32_t d0 = src[0], d1 = src[1], d2 = src[2];
-      const uint32_t r01 = sub_pair(d1, d0, 0x0C030C00u), r23 = sub_pair(d2, d1, 0x0C050C02u);
-      const uint32_t g01 = sub_pair(d1, d0, 0x0C040C01u), g23 = sub_pair(d2, d1, 0x0C060C03u);
-      const uint32_t b01 = sub_pair(d1, d0, 0x0C050C02u), b23 = sub_pair(d2, d1, 0x0C070C04u);
-      *reinterpret_cast<u2*>(wt + pdst) = u2{r01, r23};
-      *reinterpret_cast<u2*>(wt + G::PLANE + pdst) = u2{g01, g23};
-      *reinterpret_cast<u2*>(wt + 2 * G::PLANE + pdst) = u2{b01, b23};
-    }
-  };
-  auto lds_barrier = [&]() __attribute__((always_inline)) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-  };
-  f4 acc[C][NX][2];
-  // one pair step: N = this wave's vector-memory operations issued after pair
-  // k's DMA pieces (later pieces and output stores), so the counted wait
-  // retires exactly pair k's pieces
-  // (one step per loop iteration with the slot k mod 3 a runtime scalar: an
-  // unrolled 3-step loop with compile-time slots spilled registers)
-  auto step = [&](auto fin_c, auto start_c, auto n_c, int k) __attribute__((always_inline)) {
-    constexpr bool FIN = decltype(fin_c)::value, START = decltype(start_c)::value;
-    const int slot = __builtin_amdgcn_readfirstlane(k - 3 * (k / 3));
-    wait_vm<decltype(n_c)::value>();
-    lds_barrier();  // every wave's pieces of pair k landed; pair k - 1's planes read
-    stage(slot);
-    lds_barrier();  // planes of pair k visible; slot free
-    issue(k + 3, slot);
-    const int yg = base + 32 * (k - 1);
-    uint32_t rowoff[2];
-    if constexpr (FIN) {
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int y = yg + 16 * q + m;
-        rowoff[q] = (y >= ys && y < ye) ? a.out_org + (uint32_t)((int64_t)y * a.out_pitch) : kOOB;
-      }
-    }
-    constexpr int T = NX * C;
-    auto hread = [&](int t, half8 (&f)[2][2]) __attribute__((always_inline)) {
-      const int i = t / C, c = t % C;
-      const uint8_t* fb = wt + c * G::PLANE + m * G::STRIDE + 2 * (wave * G::PX + 16 * i + 8 * g);
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        f[0][s] = *reinterpret_cast<const half8*>(fb + 64 * s);
-        f[1][s] = *reinterpret_cast<const half8*>(fb + 16 * G::STRIDE + 64 * s);
-      }
-    };
-    auto hmfma = [&](const half8 (&f)[2][2], f4 (&x)[2]) __attribute__((always_inline)) {
-      const float x0 = LSB ? sa.hinit : 0.f;
-      x[0] = f4{x0, x0, x0, x0};
-      x[1] = f4{x0, x0, x0, x0};
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int hl = 0; hl < NHL; ++hl)
-#pragma unroll
-          for (int h = 0; h < 2; ++h) x[h] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f[h][s], bh[s][hl], x[h], 0, 0, 0);
-    };
-    uint32_t wo[2][C];
-    auto vert = [&](int t, const f4 (&x)[2]) __attribute__((always_inline)) {
-      const int i = t / C, c = t % C;
-      f4 o4[2], n4[2];
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        o4[q] = acc[c][i][q];
-        n4[q] = LSB ? f4{sa.bias, sa.bias, sa.bias, sa.bias} : f4{0.f, 0.f, 0.f, 0.f};
-      }
-      if constexpr (LSB) {
-        const u4 uh = {f32x2_to_h2(x[0][0], x[0][1]), f32x2_to_h2(x[0][2], x[0][3]), f32x2_to_h2(x[1][0], x[1][1]),
-                       f32x2_to_h2(x[1][2], x[1][3])};
-        const half8 ah = __builtin_bit_cast(half8, uh);
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          if constexpr (FIN) o4[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bv[q][1][0], o4[q], 0, 0, 0);
-          if constexpr (START) n4[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bv[q][0][0], n4[q], 0, 0, 0);
-        }
-      } else {
-        uint32_t h[4], l[4];
-        split_h2(x[0][0], x[0][1], h[0], l[0]);
-        split_h2(x[0][2], x[0][3], h[1], l[1]);
-        split_h2(x[1][0], x[1][1], h[2], l[2]);
-        split_h2(x[1][2], x[1][3], h[3], l[3]);
-        const u4 uh = {h[0], h[1], h[2], h[3]}, ul = {l[0], l[1], l[2], l[3]};
-        const half8 ah = __builtin_bit_cast(half8, uh), al = __builtin_bit_cast(half8, ul);
-#pragma unroll
-        for (int st = 0; st < 3; ++st)
-#pragma unroll
-          for (int q = 0; q < 2; ++q) {
-            const half8 av = st == 2 ? al : ah;
-            if constexpr (FIN) o4[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, bv[q][1][st == 1], o4[q], 0, 0, 0);
-            if constexpr (START) n4[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, bv[q][0][st == 1], n4[q], 0, 0, 0);
-          }
-      }
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        if constexpr (START) acc[c][i][q] = n4[q];
-        if constexpr (FIN) {
-          if (c == 0) {
-#pragma unroll
-            for (int w = 0; w < C; ++w) wo[q][w] = 0;
-          }
-#pragma unroll
-          for (int px = 0; px < 4; ++px) {
-            const int e = C * px + c;
-            wo[q][e >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(o4[q][px], e & 3, wo[q][e >> 2]);
-          }
-        }
-      }
-      if constexpr (FIN) {
-        if (c != C - 1) return;
-        typedef uint32_t u3 __attribute__((ext_vector_type(3)));
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const uint32_t off = rowoff[q] + (uint32_t)((sx + 16 * i + 4 * g) * C);
-          const uint32_t ok = (sx + 16 * i + 4 * g + 4 <= a.W) ? 0u : kOOB;  // W % 4 == 0: whole groups
-          __builtin_amdgcn_raw_buffer_store_b96(u3{wo[q][0], wo[q][1], wo[q][2]}, rout, off | ok, 0, 0);
-        }
-      }
-    };
-    half8 F[2][2][2];
-    f4 X[2][2];
-    hread(0, F[0]);
-    hread(1, F[1]);
-    hmfma(F[0], X[0]);
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-      if (t + 1 < T) hmfma(F[(t + 1) & 1], X[(t + 1) & 1]);
-      if (t + 2 < T) hread(t + 2, F[t & 1]);
-      vert(t, X[t & 1]);
-    }
-  };
-  using T_ = std::integral_constant<bool, true>;
-  using F_ = std::integral_constant<bool, false>;
-  // vector-memory ops a wave issues per step: NDMA pieces, then 2 NX output
-  // stores when the step finishes a group (every step but the first)
-  constexpr int D = NDMA, W = 2 * NX;
-  issue(0, 0);
-  issue(1, 1);
-  issue(2, 2);
-  // younger than pair k's pieces -- k = 0: pairs 1, 2; k = 1: pairs 2, 3 (no
-  // stores yet); k = 2: pair 3, pair 4, the stores of step 1; k = 3: pair 4,
-  // pair 5, the stores of steps 1 and 2; k >= 4: also those of step k - 3
-  // (pairs 0 .. ngroups: a band has ngroups >= 1)
-  step(F_{}, T_{}, std::integral_constant<int, 2 * D>{}, 0);
-  // (early returns, this one included although a band has ngroups >= 1: without
-  // them hipcc spilled 28-48 registers of this kernel)
-  if (ngroups == 0) {
-    wait_vm<0>();
-    return;
-  }
-  if (ngroups == 1) {
-    step(T_{}, F_{}, std::integral_constant<int, 2 * D>{}, 1);
-    wait_vm<0>();
-    return;
-  }
-  step(T_{}, T_{}, std::integral_constant<int, 2 * D>{}, 1);
-  if (ngroups == 2) {
-    step(T_{}, F_{}, std::integral_constant<int, 2 * D + W>{}, 2);
-    wait_vm<0>();
-    return;
-  }
-  step(T_{}, T_{}, std::integral_constant<int, 2 * D + W>{}, 2);
-  if (ngroups == 3) {
-    step(T_{}, F_{}, std::integral_constant<int, 2 * D + 2 * W>{}, 3);
-    wait_vm<0>();
-    return;
-  }
-  step(T_{}, T_{}, std::integral_constant<int, 2 * D + 2 * W>{}, 3);
-  using NS = std::integral_constant<int, 2 * D + 3 * W>;
-  for (int k = 4; k < ngroups; ++k) step(T_{}, T_{}, NS{}, k);
-  step(T_{}, F_{}, NS{}, ngroups);
-  wait_vm<0>();  // no DMA may still target LDS when the workgroup retires
-}
-
 }  // namespace dev
 
 // Weight scaling of the subnormal staging: horizontal weights x 2^kexp,
@@ -1015,26 +702,24 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
   // A/B variants of the RGB non-edge kernel (STRIPE_BLUR_VARIANT=n): 1 = two
   // independent 4-wave workgroups per CU (NW 4, two pairs in flight), 2 = the
   // same with one pair in flight, 3 = the 8-wave windows staging each pair
-  // between the barrier and the MFMAs (round 4's default, EARLY = false), 4 =
-  // the LDS-DMA ring (k_blur_dma).
+  // between the barrier and the MFMAs (round 4's default, EARLY = false).
+  // (Round 6: an LDS-DMA ring three pairs ahead, one f16 buffer staged between
+  // two barriers, was exact but 12-17 % slower, profiles/r6/dma/: removed.)
   // (Three pairs in flight, lsb, 254 registers: 0.376 vs 0.354 ms on 16K,
   // 0.047 vs 0.042 on the stripe, profiles/r5/blur/pfd3_*.txt: removed.)
 #define STRIPE_BLUR_LATE(LSB)                                                                        \
   Cfg { 2, 2, 8, dev::k_blur_pl<3, false, 2, 2, 2, LSB, 8, false>, (size_t)dev::PlGeom<3, 2, 8>::LDS }
-#define STRIPE_BLUR_DMA(LSB) \
-  Cfg { 2, 2, 8, dev::k_blur_dma<LSB>, (size_t)dev::PlGeom<3, 2, 8>::TILE + 3 * dev::kDmaSlot }
-  static const Cfg variants[2][5] = {
+  static const Cfg variants[2][4] = {
       {STRIPE_BLUR_CFGW(3, false, 2, 2, 2, false, 8), STRIPE_BLUR_CFGW(3, false, 2, 2, 2, false, 4),
-       STRIPE_BLUR_CFGW(3, false, 2, 1, 2, false, 4), STRIPE_BLUR_LATE(false), STRIPE_BLUR_DMA(false)},
+       STRIPE_BLUR_CFGW(3, false, 2, 1, 2, false, 4), STRIPE_BLUR_LATE(false)},
       {STRIPE_BLUR_CFGW(3, false, 2, 2, 2, true, 8), STRIPE_BLUR_CFGW(3, false, 2, 2, 2, true, 4),
-       STRIPE_BLUR_CFGW(3, false, 2, 1, 2, true, 4), STRIPE_BLUR_LATE(true), STRIPE_BLUR_DMA(true)}};
+       STRIPE_BLUR_CFGW(3, false, 2, 1, 2, true, 4), STRIPE_BLUR_LATE(true)}};
 #undef STRIPE_BLUR_LATE
-#undef STRIPE_BLUR_DMA
   static const int env_variant = [] {
     const char* e = std::getenv("STRIPE_BLUR_VARIANT");
     return e ? std::atoi(e) : 0;
   }();
-  const Cfg& cf = (p.cmid == 3 && !edge && env_variant > 0 && env_variant < 5) ? variants[lsb][env_variant]
+  const Cfg& cf = (p.cmid == 3 && !edge && env_variant > 0 && env_variant < 4) ? variants[lsb][env_variant]
                                                                                : cfgs[lsb][p.cmid == 3][edge];
 #undef STRIPE_BLUR_CFG
 #undef STRIPE_BLUR_CFGW
