@@ -704,7 +704,7 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
   // same with one pair in flight, 3 = the 8-wave windows staging each pair
   // between the barrier and the MFMAs (round 4's default, EARLY = false).
   // (Round 6: an LDS-DMA ring three pairs ahead, one f16 buffer staged between
-  // two barriers, was exact but 12-17 % slower, profiles/r6/dma/: removed.)
+  // two barriers, was exact but 13-25 % slower, profiles/r6/dma/: removed.)
   // (Three pairs in flight, lsb, 254 registers: 0.376 vs 0.354 ms on 16K,
   // 0.047 vs 0.042 on the stripe, profiles/r5/blur/pfd3_*.txt: removed.)
 #define STRIPE_BLUR_LATE(LSB)                                                                        \
