@@ -157,6 +157,17 @@ dma)
     done
   done
   ;;
+shapes)
+  # the RGB blur's workgroup shapes again, after the subnormal staging:
+  # 0 = 8 waves sharing a window (default), 1 / 2 = two independent 4-wave
+  # workgroups per CU (two / one pairs in flight), 3 = late staging
+  for r in 1 2 3; do
+    for v in 0 1 2 3; do
+      STRIPE_BLUR_VARIANT=$v timeout -k 10 120 python tools/kbench.py --chains "blur:31|blur:31:lsb" --shape 16384x16384x3 --iters 30 >> $O/blur_v${v}_16k.txt 2>&1 || exit 4
+      STRIPE_BLUR_VARIANT=$v timeout -k 10 120 python tools/kbench.py --chains "blur:31|blur:31:lsb" --shape 16384x2048x3 --iters 60 >> $O/blur_v${v}_stripe.txt 2>&1 || exit 4
+    done
+  done
+  ;;
 batched)
   # the batched exchange schedule (one group per stream and round): GPU tests,
   # then the self-halo share with the probe choosing among all schedules,
