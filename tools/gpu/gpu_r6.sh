@@ -168,6 +168,19 @@ shapes)
     done
   done
   ;;
+occ)
+  # one x-tile per wave, 12 / 16 waves sharing a window (3-4 waves per SIMD):
+  # numerics of each variant first, then A/B with the default
+  for v in 4 5 6; do
+    STRIPE_BLUR_VARIANT=$v timeout -k 10 300 python -u -m pytest tests/test_oracle_conv.py tests/test_gpu_large.py tests/test_gpu_kernels.py -m gpu -q -x -k "blur or sep" --timeout 120 --timeout-method thread > $O/tests_v$v.txt 2>&1 || exit 2
+  done
+  for r in 1 2 3; do
+    for v in 0 4 5 6; do
+      STRIPE_BLUR_VARIANT=$v timeout -k 10 120 python tools/kbench.py --chains "blur:31|blur:31:lsb" --shape 16384x16384x3 --iters 30 >> $O/blur_v${v}_16k.txt 2>&1 || exit 4
+      STRIPE_BLUR_VARIANT=$v timeout -k 10 120 python tools/kbench.py --chains "blur:31|blur:31:lsb" --shape 16384x2048x3 --iters 60 >> $O/blur_v${v}_stripe.txt 2>&1 || exit 4
+    done
+  done
+  ;;
 batched)
   # the batched exchange schedule (one group per stream and round): GPU tests,
   # then the self-halo share with the probe choosing among all schedules,
