@@ -151,7 +151,7 @@ struct PlGeom {
   // a double-buffered window
   static constexpr int LDS = NW == 1 ? kSepWaves * TILE : 2 * TILE;
   static constexpr int THREADS = blur_threads(NW);  // workgroup size
-  static_assert(NW == 1 || NW == 4 || NW == 8 || NW == 12 || NW == 16, "a shared window spans the whole workgroup");
+  static_assert(NW == 1 || NW == 4 || NW == 8, "a shared window spans the whole workgroup");
   static_assert(WPX % UPX == 0, "staged row must be whole loads");
   static_assert(STRIDE % 64 == 32 && STRIDE >= 2 * WPX, "plane stride");
 };
@@ -703,30 +703,25 @@ void launch_blur_sep(const Pass& p, const PassConsts& pc, const PassLaunch& L, h
   // independent 4-wave workgroups per CU (NW 4, two pairs in flight), 2 = the
   // same with one pair in flight, 3 = the 8-wave windows staging each pair
   // between the barrier and the MFMAs (round 4's default, EARLY = false).
-  // 4-6: one x-tile per wave, 12 or 16 waves sharing a window (3-4 waves per
-  // SIMD at 116-147 registers): 4 = 16 waves / 1 pair (lsb; exact: 12 waves),
-  // 5 = 12 waves / 2 pairs (lsb; exact as 4), 6 = 12 waves / 1 pair.
-  // (Round 6: an LDS-DMA ring three pairs ahead, one f16 buffer staged between
+  // (Round 6: one x-tile per wave with 12 or 16 waves sharing the window, 3-4
+  // waves per SIMD at 116-147 registers, was 5-25 % slower, profiles/r6/occ/;
+  // an LDS-DMA ring three pairs ahead, one f16 buffer staged between
   // two barriers, was exact but 13-25 % slower, profiles/r6/dma/: removed.)
   // (Three pairs in flight, lsb, 254 registers: 0.376 vs 0.354 ms on 16K,
   // 0.047 vs 0.042 on the stripe, profiles/r5/blur/pfd3_*.txt: removed.)
 #define STRIPE_BLUR_LATE(LSB)                                                                        \
   Cfg { 2, 2, 8, dev::k_blur_pl<3, false, 2, 2, 2, LSB, 8, false>, (size_t)dev::PlGeom<3, 2, 8>::LDS }
-  static const Cfg variants[2][7] = {
+  static const Cfg variants[2][4] = {
       {STRIPE_BLUR_CFGW(3, false, 2, 2, 2, false, 8), STRIPE_BLUR_CFGW(3, false, 2, 2, 2, false, 4),
-       STRIPE_BLUR_CFGW(3, false, 2, 1, 2, false, 4), STRIPE_BLUR_LATE(false),
-       STRIPE_BLUR_CFGW(3, false, 1, 1, 3, false, 12), STRIPE_BLUR_CFGW(3, false, 1, 1, 3, false, 12),
-       STRIPE_BLUR_CFGW(3, false, 1, 1, 3, false, 12)},
+       STRIPE_BLUR_CFGW(3, false, 2, 1, 2, false, 4), STRIPE_BLUR_LATE(false)},
       {STRIPE_BLUR_CFGW(3, false, 2, 2, 2, true, 8), STRIPE_BLUR_CFGW(3, false, 2, 2, 2, true, 4),
-       STRIPE_BLUR_CFGW(3, false, 2, 1, 2, true, 4), STRIPE_BLUR_LATE(true),
-       STRIPE_BLUR_CFGW(3, false, 1, 1, 4, true, 16), STRIPE_BLUR_CFGW(3, false, 1, 2, 3, true, 12),
-       STRIPE_BLUR_CFGW(3, false, 1, 1, 3, true, 12)}};
+       STRIPE_BLUR_CFGW(3, false, 2, 1, 2, true, 4), STRIPE_BLUR_LATE(true)}};
 #undef STRIPE_BLUR_LATE
   static const int env_variant = [] {
     const char* e = std::getenv("STRIPE_BLUR_VARIANT");
     return e ? std::atoi(e) : 0;
   }();
-  const Cfg& cf = (p.cmid == 3 && !edge && env_variant > 0 && env_variant < 7) ? variants[lsb][env_variant]
+  const Cfg& cf = (p.cmid == 3 && !edge && env_variant > 0 && env_variant < 4) ? variants[lsb][env_variant]
                                                                                : cfgs[lsb][p.cmid == 3][edge];
 #undef STRIPE_BLUR_CFG
 #undef STRIPE_BLUR_CFGW
