@@ -38,6 +38,11 @@ def test_frame_stream_example():
     assert "frames/s" in out and "schedule serial" in out
 
 
+def test_large_kernels_example():
+    out = _run("examples/large_kernels.py", "--shape", "120x70x3", "--iters", "1")
+    assert "on host" in out and out.count("max |diff| vs golden") == 4
+
+
 def _run_gpu(*args):
     r = subprocess.run([sys.executable, *args], capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stdout + r.stderr[-3000:]
@@ -66,3 +71,9 @@ def test_reference_flow_example_gpu(C, tmp_path):
 def test_frame_stream_example_gpu():
     out = _run_gpu("examples/frame_stream.py", "--backend", "rccl", "--shape", "2048x1024x3", "--frames", "16")
     assert "frames/s" in out and "1 rank(s) (rccl)" in out
+
+
+@pytest.mark.gpu
+def test_large_kernels_example_gpu():
+    out = _run_gpu("examples/large_kernels.py", "--shape", "1024x512x3", "--iters", "2")
+    assert "on GPU" in out and out.count("max |diff| vs golden") == 4
