@@ -15,6 +15,8 @@
 #   subn / subn2  blur:31 subnormal staging A/B                   -> r6/subn*
 #   prof      rocprofv3 kernel traces of the final bench / self-halo share,
 #             blur:31 counters                                     -> r6/prof
+#   curve     one-GPU proxy of the 1/2/4/8 scaling curve (each N's share with
+#             its RCCL exchange through self-halo)                  -> r6/curve
 #   valu      the separable-VALU blur comparator beside the MFMA kernel -> r6/valu
 #   local     the `local` hub's halo rounds: GPU tests of every local-rank
 #             path, then 4 local ranks on 8192^2 gray sobel at halo depth 1
@@ -178,6 +180,20 @@ occ)
     for v in 0 4 5 6; do
       STRIPE_BLUR_VARIANT=$v timeout -k 10 120 python tools/kbench.py --chains "blur:31|blur:31:lsb" --shape 16384x16384x3 --iters 30 >> $O/blur_v${v}_16k.txt 2>&1 || exit 4
       STRIPE_BLUR_VARIANT=$v timeout -k 10 120 python tools/kbench.py --chains "blur:31|blur:31:lsb" --shape 16384x2048x3 --iters 60 >> $O/blur_v${v}_stripe.txt 2>&1 || exit 4
+    done
+  done
+  ;;
+curve)
+  # one-GPU proxy of the 1/2/4/8 strong-scaling curve: each N's per-rank share
+  # of the 16K RGB frame (16384 x 16384/N) with and without its RCCL halo
+  # exchange (self-halo: the rank is its own two neighbours), two processes each
+  X="--dist-steps 0 --ref-steps 0 --e2e-steps 0 --deep-steps 0"
+  for r in 1 2; do
+    timeout -k 10 300 python bench.py --steps 50 --warmup 10 $X >> $O/n1.json 2>> $O/n1.err || exit 3
+    for h in 8192 4096 2048; do
+      st=$((200 * 2048 / h)); [ $st -lt 50 ] && st=50
+      timeout -k 10 300 python bench.py --height $h --steps $st --warmup 20 $X >> $O/share_${h}_plain.json 2>> $O/share_${h}_plain.err || exit 3
+      timeout -k 10 300 python bench.py --height $h --steps $st --warmup 20 $X --self-halo >> $O/share_${h}_self.json 2>> $O/share_${h}_self.err || exit 3
     done
   done
   ;;
