@@ -90,10 +90,11 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--band", type=int, default=0)
-    ap.add_argument("--halo-schedule", default="auto", choices=["auto", "serial", "overlap", "pipeline", "batched"],
+    ap.add_argument("--halo-schedule", default="auto", choices=["auto", "serial", "overlap", "pipeline", "batched", "ahead"],
                     help="halo schedule of the headline steps at N>1 (auto: time each on the real transport before "
                          "the timed region and keep the fastest, max over ranks; batched: serial steps with the "
-                         "exchanges of the frames sharing a stream in one group per round)")
+                         "exchanges of the frames sharing a stream in one group per round; ahead: each frame's next "
+                         "exchange posted right after its step on a communication stream of its own)")
     ap.add_argument("--frames", type=int, default=0,
                     help="frames the headline steps over (0: auto -- enough to defeat the Infinity Cache when a "
                          "stripe fits it, else 2 at N>1 so one frame's exchange runs beside the other's filter, "

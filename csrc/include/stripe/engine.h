@@ -188,6 +188,15 @@ class Engine {
   bool posts_halo() const;
   void post_halo();
   void run_posted();
+  // The "ahead" form: the exchange for the engine's current input as a group
+  // of its own on stream `comm`, ordered after the work queued on the compute
+  // stream so far (the step that wrote that input); run_posted() makes the
+  // compute stream wait for it.  A frame stream posts each frame's next
+  // exchange right after its step, a whole round before that step needs the
+  // rows, so the exchange runs beside the other frames' filters instead of in
+  // front of this one's.  Any other use of the input first waits for a
+  // pending exchange (settle_post).
+  void post_halo_ahead(hipStream_t comm);
   // Tuned band heights, occupancy caps and memory policies per pass (after
   // autotune), for reporting.
   std::vector<int> bands() const;
@@ -284,6 +293,11 @@ class Engine {
   void exchange_halo(uint8_t* org, int C, int R, hipStream_t s);
   void post_halo_ops(uint8_t* org, int C, int R, hipStream_t s);
   int posted_buf_ = -1;     // buffer whose halo post_halo() posted (-1: none)
+  bool posted_ahead_ = false;    // that post is post_halo_ahead's, on another stream
+  hipEvent_t ahead_ev_[2] = {};  // post_halo_ahead: input written (compute), exchange done (comm)
+  // drop a post nobody consumed; a pending ahead exchange is first waited for
+  // on the compute stream (it may still write this input's halo rows)
+  void settle_post();
   bool halo_done_ = false;  // run_posted(): this step's exchange already happened
   // this rank exchanges halo rows (another active rank, or the self-halo ring)
   bool neighbours() const { return part_.active > 1 || self_halo_; }

@@ -584,6 +584,10 @@ PYBIND11_MODULE(_C, m) {
         py::gil_scoped_release nogil;
         e.run_posted();
       })
+      .def("post_halo_ahead", [](Engine& e, uintptr_t s) {
+        py::gil_scoped_release nogil;
+        e.post_halo_ahead(as_stream(s));
+      }, py::arg("stream"))
       .def_property_readonly("plan", [](const Engine& e) { return e.plan().describe(); })
       .def_property_readonly("partition", [](const Engine& e) { return e.partition().describe(); })
       .def_property_readonly("stripe", [](const Engine& e) {

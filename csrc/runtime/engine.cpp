@@ -183,6 +183,8 @@ Engine::~Engine() {
       if (g) (void)hipGraphExecDestroy(g);
     for (auto& e : pev_)
       if (e) (void)hipEventDestroy(e);
+    for (auto& e : ahead_ev_)
+      if (e) (void)hipEventDestroy(e);
     for (auto& e : dist_ev_) (void)hipEventDestroy(e);
     if (s_edge_) (void)hipStreamDestroy(s_edge_);
     for (auto& e : ev_h2d_) (void)hipEventDestroy(e);
@@ -379,7 +381,7 @@ void Engine::fill_margins(uint8_t* org, int C, int y0, int y1, int px, Border b,
 }
 
 void Engine::load_synthetic(uint64_t seed) {
-  posted_buf_ = -1;
+  settle_post();
   TraceRange tr("stripe.load");
   fault_point("load", rank_);
   const Stripe& st = stripe();
@@ -400,7 +402,7 @@ void Engine::load_synthetic(uint64_t seed) {
 }
 
 void Engine::load_packed(const void* src, bool src_device) {
-  posted_buf_ = -1;
+  settle_post();
   (void)src_device;
   const Stripe& st = stripe();
   const int C = plan_.cin;
@@ -461,7 +463,7 @@ void Engine::load_root_synthetic(uint64_t seed) {
 }
 
 void Engine::scatter() {
-  posted_buf_ = -1;
+  settle_post();
   const int C = plan_.cin;
   const int64_t P = pitch(C);
   const Stripe& st = stripe();
@@ -572,6 +574,7 @@ bool Engine::posts_halo() const {
 
 void Engine::post_halo() {
   if (!posts_halo()) return;
+  settle_post();
   STRIPE_CHECK(cur_c_ == plan_.cin, "post_halo: the engine input has " << cur_c_ << " channels");
   const Pass& p = plan_.passes[0];
   STRIPE_CHECK(!self_halo_ || p.R <= stripe().rows, "self-halo of " << p.R << " rows needs a stripe that tall");
@@ -580,12 +583,39 @@ void Engine::post_halo() {
   posted_buf_ = cur_;
 }
 
+void Engine::post_halo_ahead(hipStream_t comm) {
+  if (!posts_halo()) return;
+  STRIPE_CHECK(comm != nullptr, "post_halo_ahead needs a stream");
+  STRIPE_CHECK(cur_c_ == plan_.cin, "post_halo_ahead: the engine input has " << cur_c_ << " channels");
+  if (posted_buf_ == cur_) return;  // this input's exchange is already posted
+  settle_post();
+  const Pass& p = plan_.passes[0];
+  STRIPE_CHECK(!self_halo_ || p.R <= stripe().rows, "self-halo of " << p.R << " rows needs a stripe that tall");
+  for (auto& e : ahead_ev_)
+    if (!e) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  fault_point("halo", rank_);
+  HIP_CHECK(hipEventRecord(ahead_ev_[0], s_compute_));
+  HIP_CHECK(hipStreamWaitEvent(comm, ahead_ev_[0], 0));
+  comm_->group_start();
+  post_halo_ops(origin(buf_[cur_], p.cin), p.cin, p.R, comm);
+  comm_->group_end();
+  HIP_CHECK(hipEventRecord(ahead_ev_[1], comm));
+  posted_buf_ = cur_;
+  posted_ahead_ = true;
+}
+
+void Engine::settle_post() {
+  if (posted_ahead_) HIP_CHECK(hipStreamWaitEvent(s_compute_, ahead_ev_[1], 0));
+  posted_ahead_ = false;
+  posted_buf_ = -1;
+}
+
 void Engine::run_posted() {
   if (!posts_halo() || posted_buf_ != cur_) {  // nothing posted for this input: a step with its own exchange
     run(1);
     return;
   }
-  posted_buf_ = -1;
+  settle_post();  // an ahead exchange: the compute stream waits for it
   halo_done_ = true;
   try {
     run(1);
@@ -718,7 +748,7 @@ bool Engine::graph_ok() const {
 
 void Engine::run(int iterations) {
   STRIPE_CHECK(iterations >= 1, "iterations must be >= 1");
-  if (!halo_done_) posted_buf_ = -1;  // a post for this input is spent by any other step
+  if (!halo_done_) settle_post();  // a post for this input is spent by any other step
   if (cfg_.autotune && !tuned_) autotune_bands();
   STRIPE_CHECK(iterations == 1 || plan_.cout == plan_.cin,
                "iterating a chain needs equal input/output channels (" << plan_.cin << "->" << plan_.cout << ")");
@@ -814,7 +844,7 @@ std::vector<float> Engine::run_timed(int iterations, int per, bool rewind_each) 
 }
 
 void Engine::rewind() {
-  posted_buf_ = -1;
+  settle_post();
   cur_ = run_in_buf_;
   cur_c_ = plan_.cin;
 }
@@ -894,6 +924,7 @@ std::string Engine::store_root_jpeg(int quality) {
 void Engine::synchronize() {
   if (!device()) return;
   TraceRange tr("stripe.synchronize");
+  if (posted_ahead_) HIP_CHECK(hipEventSynchronize(ahead_ev_[1]));  // an exchange in flight on another stream
   wait_stream(s_compute_);
   wait_stream(s_comm_);
   wait_stream(s_edge_);

@@ -358,8 +358,11 @@ class FrameStream:
             # profiles/r5/shared/); freed with the last frame that uses them
             holder = _PlainStreams(ctx.gpu, nmax)
             self._sets["plain"] = [torch.cuda.ExternalStream(h, device=ctx.gpu) for h in holder.handles]
+            # the "ahead" schedule's exchanges run on a stream of their own
+            self._comm_streams = _PlainStreams(ctx.gpu, 1)
             for f in self.frames:
                 f._plain_streams = holder
+                f._comm_streams = self._comm_streams
             if pin == "pool":  # the set's earlier name
                 pin = "plain"
             kinds = [k for k in ("dedicated", "plain") if k in self._sets]
@@ -447,22 +450,27 @@ class FrameStream:
         for f in self.frames[1:]:
             f.engine.set_tuning(e0.bands, e0.caps, e0.policies, e0.orders)
 
-    SCHEDULES = ("pipeline", "overlap", "serial", "batched")
+    SCHEDULES = ("pipeline", "overlap", "serial", "batched", "ahead")
 
     def set_schedule(self, name: str):
         """Halo schedule of every frame ("serial" | "overlap" | "pipeline" |
-        "batched").  "batched" is the serial schedule with the exchanges of
-        all frames that share a stream posted as ONE communicator group, ahead
-        of the first of those frames' steps in each round: one RCCL launch per
-        stream and round instead of one per frame and step (the frames' own
-        order on their stream already puts each frame's previous step before
-        it)."""
+        "batched" | "ahead").  "batched" is the serial schedule with the
+        exchanges of all frames that share a stream posted as ONE communicator
+        group, ahead of the first of those frames' steps in each round: one
+        RCCL launch per stream and round instead of one per frame and step
+        (the frames' own order on their stream already puts each frame's
+        previous step before it).  "ahead" posts each frame's next exchange
+        right after its step, on a communication stream of its own
+        (Engine.post_halo_ahead): the rows are needed a whole round later, so
+        the exchange runs beside the other frames' filters and the frame's
+        next step only waits for an event that has long fired."""
         self.batched = name == "batched"
+        self.ahead = name == "ahead"
         for f in self.frames:
-            f.engine.halo_schedule = "serial" if self.batched else name
+            f.engine.halo_schedule = "serial" if (self.batched or self.ahead) else name
 
     def _batch_candidate(self) -> bool:
-        """Whether the probe times "batched": frames of device engines that
+        """Whether the probe times "batched" and "ahead": frames of device engines that
         exchange halo rows (N > 1, or the self-halo rank).  Decided on what
         every rank shares -- never on a rank's own stripe -- so every rank
         times the same candidate list."""
@@ -475,9 +483,15 @@ class FrameStream:
         """Batched posts apply: device engines that exchange halo rows."""
         return bool(getattr(self, "batched", False) and self.streams and self.head.engine.posts_halo)
 
+    def _aheads(self) -> bool:
+        """Ahead posts apply: device engines that exchange halo rows."""
+        return bool(getattr(self, "ahead", False) and self.streams and self.head.engine.posts_halo)
+
     @property
     def schedule(self) -> str:
-        return "batched" if self._batches() else self.head.engine.halo_schedule
+        if self._batches():
+            return "batched"
+        return "ahead" if self._aheads() else self.head.engine.halo_schedule
 
     def pick_schedule(self, reduce_max=None, barrier=None, steps: int = 0, rounds: int = 2) -> dict:
         """Time every halo schedule (interior / boundary overlap, the
@@ -497,8 +511,8 @@ class FrameStream:
         # collective reduce_max): device engines try every schedule, even one a
         # rank's own stripe runs another way (e.g. a thin stripe without the
         # pipeline); host engines have one schedule and time nothing
-        scheds = ([s for s in self.SCHEDULES if s != "batched" or self._batch_candidate()] if self.streams
-                  else ["serial"])
+        scheds = ([s for s in self.SCHEDULES if s not in ("batched", "ahead") or self._batch_candidate()]
+                  if self.streams else ["serial"])
         if getattr(getattr(self.head, "ctx", None), "world", 2) == 1:
             # one rank exchanges nothing: only schedules that differ on it (none)
             eff = []
@@ -577,6 +591,11 @@ class FrameStream:
                 finally:
                     comm.group_end()
             f.engine.run_posted()  # (a frame whose exchange was not posted makes its own)
+        elif self._aheads():
+            # this step's exchange was posted a round ago (the first round makes
+            # its own); the next one is posted now, on the communication stream
+            f.engine.run_posted()
+            f.engine.post_halo_ahead(self._comm_streams.handles[0])
         else:
             f.run(1)
 

@@ -56,7 +56,7 @@ def test_bench_gloo_gpu_processes(tmp_path, n):
     import torch
 
     hs = rec["halo_schedule"]
-    scheds = ("serial", "overlap", "pipeline", "batched")
+    scheds = ("serial", "overlap", "pipeline", "batched", "ahead")
     if n > torch.cuda.device_count():
         assert hs["queues"] == "plain"
         assert set(hs["ms"]) == {f"{s}@{k}" for s in scheds for k in (1, 2)}

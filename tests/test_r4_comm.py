@@ -383,10 +383,10 @@ def test_frame_stream_pick_schedule_takes_fastest_max_over_ranks():
     fs.synchronize = lambda: None
     seen = []
     got = fs.pick_schedule(lambda v: seen.append(v) or v, steps=3, rounds=2)
-    # (two frames on device streams at N > 1: the batched exchange is a
-    # candidate too; its engines step the serial schedule)
-    assert got["chosen"] == "overlap" and set(got["ms"]) == set(cost) | {"batched"}
-    assert len(seen) == 8 and all(f.engine.halo_schedule == "overlap" for f in frames)
+    # (two frames on device streams at N > 1: the batched and ahead exchanges
+    # are candidates too; their engines step the serial schedule)
+    assert got["chosen"] == "overlap" and set(got["ms"]) == set(cost) | {"batched", "ahead"}
+    assert len(seen) == 10 and all(f.engine.halo_schedule == "overlap" for f in frames)
     assert got["ms"]["overlap"] < got["ms"]["serial"] < got["ms"]["pipeline"]
 
 

@@ -37,7 +37,7 @@ def _stand_in(cost):
 def test_probe_picks_stream_set():
     # two streams on the pool set are fastest here: the probe must land there
     def cost(sched, n, q):
-        base = {"pipeline": 0.004, "overlap": 0.003, "serial": 0.002, "batched": 0.0035}[sched]
+        base = {"pipeline": 0.004, "overlap": 0.003, "serial": 0.002, "batched": 0.0035, "ahead": 0.0037}[sched]
         return base / 2 if (n == 2 and q == "plain") else base
 
     fs, frames = _stand_in(cost)
@@ -112,3 +112,17 @@ def test_batched_schedule_is_a_probe_candidate():
     assert all(f.engine.halo_schedule == "serial" for f in frames)  # the engines run serial steps
     fs.set_schedule("overlap")
     assert not fs.batched and fs.schedule == "overlap"
+
+
+def test_ahead_schedule_is_a_probe_candidate():
+    # the ahead exchange (each frame's next exchange posted right after its
+    # step, on a communication stream) is timed too and kept when fastest
+    def cost(sched, n, q):
+        return 0.001 if (sched == "ahead" and n == 2) else 0.003
+
+    fs, frames = _stand_in(cost)
+    got = fs.pick_schedule(steps=2, rounds=1)
+    assert got["chosen"] == "ahead" and fs.schedule == "ahead" and fs.ahead and not fs.batched
+    assert all(f.engine.halo_schedule == "serial" for f in frames)  # the engines run serial steps
+    fs.set_schedule("batched")
+    assert not fs.ahead and fs.schedule == "batched"

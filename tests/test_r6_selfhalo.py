@@ -77,7 +77,7 @@ CASES = [("gaussian5", 3), ("emboss3", 1), ("sharpen", 3), ("blur:9", 3)]
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("chain,cc", CASES)
-@pytest.mark.parametrize("schedule", ["serial", "overlap", "pipeline", "batched"])
+@pytest.mark.parametrize("schedule", ["serial", "overlap", "pipeline", "batched", "ahead"])
 @pytest.mark.parametrize("streams", [1, 2])
 def test_self_halo_frame_stream_exact_gpu(rccl_ctx, chain, cc, schedule, streams):
     ctx = rccl_ctx
@@ -98,6 +98,8 @@ def test_self_halo_frame_stream_exact_gpu(rccl_ctx, chain, cc, schedule, streams
     groups = ctx.comm.identity()["groups"] - before
     if schedule == "batched":  # one group per stream and round: the frames sharing a stream post together
         assert groups == n_it * min(streams, F)
+    elif schedule == "ahead":  # the first round's own exchanges, then one post after every step
+        assert groups == F + n_it * F
     else:
         assert groups == n_it * F * passes  # one grouped exchange per pass and step
     tol = 1 if any(p["kind"] == 3 for p in C.plan_info(chain, cc)["passes"]) else 0
@@ -169,4 +171,38 @@ def test_batched_posts_survive_partial_rounds_gpu(rccl_ctx):
     fs.frames[2].load_synthetic(9)
     fs.frames[2].engine.run_posted()
     fs.synchronize()
+    assert (fs.frames[2].result_stripe() == torus_golden(C.synth_rows(9, W, 3, 0, H), "gaussian5", 1)).all()
+
+
+@pytest.mark.gpu
+def test_ahead_posts_survive_partial_rounds_gpu(rccl_ctx):
+    # ahead posts (next exchange on the communication stream right after each
+    # step): loops that stop mid-round, a plain run and a reload between a post
+    # and its step must neither skip nor double-apply an exchange
+    ctx = rccl_ctx
+    W, H, F = 300, 64, 4
+    fs = parallel.FrameStream(ctx, Pipeline("gaussian5", halo_depth=1, self_halo=True), W, H, 3, frames=F, streams=2,
+                              autotune=False)
+    fs.set_schedule("ahead")
+    assert fs.schedule == "ahead"
+    fs.load_synthetic(3)
+    steps = [0, 1, 2, 0, 1, 2, 3, 0, 1]
+    for i in steps:
+        fs.step(i)
+    fs.synchronize()
+    for f, fr in enumerate(fs.frames):
+        ref = torus_golden(C.synth_rows(3 + f, W, 3, 0, H), "gaussian5", steps.count(f))
+        assert (fr.result_stripe() == ref).all(), f
+    # a plain run after a post: it waits for the posted exchange, then makes its own
+    e1 = fs.frames[1].engine
+    e1.post_halo_ahead(fs._comm_streams.handles[0])
+    fs.frames[1].run(1)
+    # a reload after a post: the pending exchange lands first, the reload wins
+    e2 = fs.frames[2].engine
+    e2.post_halo_ahead(fs._comm_streams.handles[0])
+    fs.frames[2].load_synthetic(9)
+    e2.run_posted()
+    fs.synchronize()
+    assert (fs.frames[1].result_stripe() ==
+            torus_golden(C.synth_rows(4, W, 3, 0, H), "gaussian5", steps.count(1) + 1)).all()
     assert (fs.frames[2].result_stripe() == torus_golden(C.synth_rows(9, W, 3, 0, H), "gaussian5", 1)).all()

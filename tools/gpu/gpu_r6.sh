@@ -15,6 +15,7 @@
 #   subn / subn2  blur:31 subnormal staging A/B                   -> r6/subn*
 #   prof      rocprofv3 kernel traces of the final bench / self-halo share,
 #             blur:31 counters                                     -> r6/prof
+#   ahead     the ahead halo schedule: tests, self-halo shares       -> r6/ahead
 #   curve     one-GPU proxy of the 1/2/4/8 scaling curve (each N's share with
 #             its RCCL exchange through self-halo)                  -> r6/curve
 #   valu      the separable-VALU blur comparator beside the MFMA kernel -> r6/valu
@@ -194,6 +195,21 @@ curve)
       st=$((200 * 2048 / h)); [ $st -lt 50 ] && st=50
       timeout -k 10 300 python bench.py --height $h --steps $st --warmup 20 $X >> $O/share_${h}_plain.json 2>> $O/share_${h}_plain.err || exit 3
       timeout -k 10 300 python bench.py --height $h --steps $st --warmup 20 $X --self-halo >> $O/share_${h}_self.json 2>> $O/share_${h}_self.err || exit 3
+    done
+  done
+  ;;
+ahead)
+  # the "ahead" schedule (each frame's next exchange posted right after its
+  # step on a communication stream): GPU tests, then the self-halo shares with
+  # the probe's pick and with ahead / batched pinned, alternating
+  timeout -k 10 900 python -u -m pytest tests/test_r6_selfhalo.py tests/test_r5_streams.py tests/test_gpu_shared.py -m gpu -q -x --timeout 300 --timeout-method thread > $O/tests.txt 2>&1 || exit 2
+  X="--dist-steps 0 --ref-steps 0 --e2e-steps 0 --deep-steps 0 --warmup 20"
+  for r in 1 2; do
+    for h in 2048 4096; do
+      st=$((200 * 2048 / h))
+      timeout -k 10 300 python bench.py --height $h --steps $st $X --self-halo >> $O/share_${h}_auto.json 2>> $O/share_${h}_auto.err || exit 3
+      timeout -k 10 300 python bench.py --height $h --steps $st $X --self-halo --halo-schedule ahead >> $O/share_${h}_ahead.json 2>> $O/share_${h}_ahead.err || exit 3
+      timeout -k 10 300 python bench.py --height $h --steps $st $X --self-halo --halo-schedule batched >> $O/share_${h}_batched.json 2>> $O/share_${h}_batched.err || exit 3
     done
   done
   ;;
