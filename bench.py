@@ -831,10 +831,10 @@ def main():
             # row chunks of the upload / filter / download pipeline: its fill
             # and drain cost about one chunk each way, so more chunks pay where
             # the link overlaps the two directions and cost per-chunk overhead
-            # where it does not (profiles/r5/e2e/): time 8 and 16 (max over
-            # ranks), keep the faster
+            # where it does not (profiles/r5/e2e/): time 8, 16 and 32 (max
+            # over ranks), keep the fastest
             chunk_ms = {}
-            for ch in (8, 16):
+            for ch in (8, 16, 32):
                 barrier()
                 t0 = time.perf_counter()
                 for _ in range(2):
