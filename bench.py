@@ -34,7 +34,8 @@ reported beside it as named scopes, never as `value`.
 Order of work (the timed region holds nothing but the K steps):
   identity (what RCCL and the runtime report, gathered to rank 0) -> autotune
   (band height x occupancy cap x memory policy, on cold data when the frames
-  rotate; also ramps the clock) -> halo-schedule probe (N > 1) -> W warmup steps -> K timed steps (barrier +
+  rotate, each stage's candidates timed round-robin; collective at N > 1:
+  every candidate's time is the slowest rank's; also ramps the clock) -> halo-schedule probe (N > 1) -> W warmup steps -> K timed steps (barrier +
   device sync on both sides, max over ranks) -> per-step device events of
   max(K, 20) more steps -> golden verification -> copy roofline -> the other
   scopes, each skipped once the wall-time budget is spent.
@@ -312,7 +313,7 @@ def main():
         dp.engine.set_tuning([a.band] * len(dp.engine.bands), [-1] * len(dp.engine.bands))
     row0, rows = dp.stripe
     fs.load_synthetic(a.seed)
-    fs.tune()
+    fs.tune(max_over_ranks)  # collective at N > 1: every rank decides on the slowest rank's timings
     # which halo schedule is fastest depends on the link and the transport's
     # per-exchange cost: at N>1 measure them here, untimed, on every rank
     # (N = 1 exchanges nothing, but runs the same frames x streams probe, so

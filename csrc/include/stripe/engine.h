@@ -13,6 +13,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <functional>
 #include <memory>
 #include <string>
 #include <vector>
@@ -208,6 +209,12 @@ class Engine {
   void tune() {
     if (cfg_.autotune && !tuned_) autotune_bands();
   }
+  // A collective tune: every candidate's median time goes through `f` (e.g.
+  // max over the ranks of a job) before the autotune compares, so every rank
+  // decides on the same numbers.  Every rank must then tune together, with
+  // rows of its own (an empty stripe skips the tune).  An empty function
+  // restores the per-rank tune.
+  void set_tune_reduce(std::function<float(float)> f) { tune_reduce_ = std::move(f); }
   // Adopt another engine's tuning (same chain and stripe shape; skips autotune).
   // `policies` may be empty (keep each pass's memory policy).
   void set_tuning(const std::vector<int>& bands, const std::vector<int>& caps,
@@ -288,6 +295,7 @@ class Engine {
   };
   void autotune_bands();
   bool tuned_ = false;
+  std::function<float(float)> tune_reduce_;  // set_tune_reduce
   uint8_t* origin(const Buffer& b, int C) const;
   uint8_t* root_origin(const Buffer& b, int C) const;
   void exchange_halo(uint8_t* org, int C, int R, hipStream_t s);

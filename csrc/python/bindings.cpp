@@ -674,6 +674,25 @@ PYBIND11_MODULE(_C, m) {
         py::gil_scoped_release nogil;
         e.tune();
       })
+      .def("set_tune_reduce", [](Engine& e, py::object f) {
+        if (f.is_none()) {
+          e.set_tune_reduce({});
+          return;
+        }
+        // called from the (GIL-released) autotune: take the GIL for the call
+        // (the function may be dropped where the GIL is released: release the
+        // Python reference under the GIL)
+        std::shared_ptr<py::object> fn(new py::object(f), [](py::object* o) {
+          py::gil_scoped_acquire gil;
+          delete o;
+        });
+        e.set_tune_reduce([fn](float v) {
+          py::gil_scoped_acquire gil;
+          return (*fn)(v).cast<float>();
+        });
+      }, py::arg("reduce"),
+           "Collective autotune: each candidate's median (ms) goes through reduce(v) -> float (e.g. max over "
+           "ranks) before the comparison; None restores the per-rank tune.  Every rank must then tune together.")
       .def_property_readonly("dist_direct", &Engine::dist_direct)
       .def("store_packed_ptr", [](Engine& e, uintptr_t p, bool dev) {
         py::gil_scoped_release nogil;

@@ -320,6 +320,8 @@ class FrameStream:
                  autotune: bool = True, stage_timing: bool = False):
         info = C.plan_info(pipeline.spec.chain, Cc, pipeline.spec.border, pipeline.fuse)
         part, _ = C.plan_rows(H, ctx.world, max(1, info["max_radius"]))
+        self.world = ctx.world
+        self.every_rank_has_rows = all(r > 0 for _, r in part)
         self.iterable = info["cin"] == info["cout"]
         self.ws_max = max(r for _, r in part) * W * (info["cin"] + info["cout"])  # per-GPU bytes of one step
         self.fits_mall = self.ws_max <= MALL_BYTES
@@ -442,11 +444,24 @@ class FrameStream:
         for i, f in enumerate(self.frames):
             f.load_synthetic(seed + i)
 
-    def tune(self):
+    def tune(self, reduce_max=None):
         """Autotune frame 0 (on cold scratch stripes when the frames rotate to
-        defeat the cache) and give every frame its tuning."""
+        defeat the cache) and give every frame its tuning.  With reduce_max
+        (max over the ranks of the job) on device engines at N > 1, the tune
+        is collective: each candidate's time is the slowest rank's, so every
+        rank runs the configuration that is best for the job's step (the max
+        over ranks), not one its own timing noise picked.  Every rank calls
+        tune() together."""
         e0 = self.head.engine
-        e0.tune()
+        collective = (reduce_max is not None and getattr(self, "world", 1) > 1 and bool(self.streams)
+                      and getattr(self, "every_rank_has_rows", False))
+        if collective:
+            e0.set_tune_reduce(reduce_max)
+        try:
+            e0.tune()
+        finally:
+            if collective:
+                e0.set_tune_reduce(None)
         for f in self.frames[1:]:
             f.engine.set_tuning(e0.bands, e0.caps, e0.policies, e0.orders)
 

@@ -213,6 +213,46 @@ ahead)
     done
   done
   ;;
+tune)
+  # the round-robin autotune: GPU tests of the tuner and of the collective
+  # tune through bench.py (gloo-gpu processes), then the tuned configs and
+  # step times of the N=8 share (one and two streams) and the 16K headline
+  timeout -k 10 900 python -u -m pytest tests/test_r6_tune.py tests/test_r5_order.py tests/test_gpu_shared.py -m gpu -q -x --timeout 300 --timeout-method thread > $O/tests.txt 2>&1 || exit 2
+  X="--steps 200 --warmup 20 --dist-steps 0 --ref-steps 0 --e2e-steps 0 --deep-steps 0"
+  for r in 1 2 3; do
+    timeout -k 10 300 python bench.py --height 2048 $X >> $O/share_auto.json 2>> $O/share_auto.err || exit 3
+    STRIPE_NT=1 timeout -k 10 300 python bench.py --height 2048 $X >> $O/share_nt1.json 2>> $O/share_nt1.err || exit 3
+    timeout -k 10 300 python bench.py --height 2048 $X --streams 1 >> $O/share_s1.json 2>> $O/share_s1.err || exit 3
+    timeout -k 10 300 python bench.py --steps 20 --warmup 5 --dist-steps 0 --ref-steps 0 --e2e-steps 0 --deep-steps 0 >> $O/n1.json 2>> $O/n1.err || exit 3
+  done
+  ;;
+onestream)
+  # the N=8 share's cold step on one stream vs the probe's pick (VERDICT r5
+  # item 5: one-stream step <= 0.042 ms), no exchange, three processes each
+  X="--height 2048 --steps 200 --warmup 20 --dist-steps 0 --ref-steps 0 --e2e-steps 0 --deep-steps 0"
+  for r in 1 2 3; do
+    timeout -k 10 300 python bench.py $X --streams 1 >> $O/share_s1.json 2>> $O/share_s1.err || exit 3
+    timeout -k 10 300 python bench.py $X >> $O/share_auto.json 2>> $O/share_auto.err || exit 3
+  done
+  ;;
+onestream3)
+  # one stream: does the step time depend on how many steps are queued?
+  X="--height 2048 --warmup 20 --dist-steps 0 --ref-steps 0 --e2e-steps 0 --deep-steps 0"
+  for r in 1 2; do
+    for k in 30 60 120 400; do
+      timeout -k 10 300 python bench.py $X --streams 1 --steps $k >> $O/share_s1_k$k.json 2>> $O/share_s1_k$k.err || exit 3
+    done
+  done
+  ;;
+onestream2)
+  # one stream with a long warmup (clock ramp?) vs the default warmup
+  X="--height 2048 --steps 200 --dist-steps 0 --ref-steps 0 --e2e-steps 0 --deep-steps 0"
+  for r in 1 2; do
+    timeout -k 10 300 python bench.py $X --streams 1 --warmup 20 >> $O/share_s1_w20.json 2>> $O/share_s1_w20.err || exit 3
+    timeout -k 10 300 python bench.py $X --streams 1 --warmup 2000 >> $O/share_s1_w2000.json 2>> $O/share_s1_w2000.err || exit 3
+    timeout -k 10 300 python bench.py $X --streams 1 --warmup 20 --frames 8 >> $O/share_s1_f8.json 2>> $O/share_s1_f8.err || exit 3
+  done
+  ;;
 batched)
   # the batched exchange schedule (one group per stream and round): GPU tests,
   # then the self-halo share with the probe choosing among all schedules,
