@@ -215,6 +215,11 @@ class Engine {
   // rows of its own (an empty stripe skips the tune).  An empty function
   // restores the per-rank tune.
   void set_tune_reduce(std::function<float(float)> f) { tune_reduce_ = std::move(f); }
+  // Streams a cold stripe's steps alternate over (1 or 2, default 2): the cold
+  // tune times its candidates the same way (a frame stream pinned to one
+  // stream tunes on one: 2-stream tunings chose 24-32-row bands that ran its
+  // one-stream steps at 0.046-0.052 ms, profiles/r6/tune/).
+  void set_tune_streams(int n) { tune_streams_ = n <= 1 ? 1 : 2; }
   // Adopt another engine's tuning (same chain and stripe shape; skips autotune).
   // `policies` may be empty (keep each pass's memory policy).
   void set_tuning(const std::vector<int>& bands, const std::vector<int>& caps,
@@ -296,6 +301,7 @@ class Engine {
   void autotune_bands();
   bool tuned_ = false;
   std::function<float(float)> tune_reduce_;  // set_tune_reduce
+  int tune_streams_ = 2;                     // set_tune_streams
   uint8_t* origin(const Buffer& b, int C) const;
   uint8_t* root_origin(const Buffer& b, int C) const;
   void exchange_halo(uint8_t* org, int C, int R, hipStream_t s);

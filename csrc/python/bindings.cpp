@@ -674,6 +674,8 @@ PYBIND11_MODULE(_C, m) {
         py::gil_scoped_release nogil;
         e.tune();
       })
+      .def("set_tune_streams", &Engine::set_tune_streams, py::arg("n"),
+           "Streams a cold stripe's steps alternate over (1 or 2): the cold tune times its candidates that way.")
       .def("set_tune_reduce", [](Engine& e, py::object f) {
         if (f.is_none()) {
           e.set_tune_reduce({});

@@ -109,7 +109,7 @@ void Engine::autotune_bands() {
   // compute stream and a second one
   hipStream_t s2 = nullptr;
   hipEvent_t e_fork = nullptr, e_join = nullptr;
-  if (nrot > 0) {
+  if (nrot > 0 && tune_streams_ > 1) {
     HIP_CHECK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
     HIP_CHECK(hipEventCreateWithFlags(&e_fork, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&e_join, hipEventDisableTiming));
@@ -135,7 +135,7 @@ void Engine::autotune_bands() {
         launch_pass(p, prt_[i].pc, L, s_compute_);
         return;
       }
-      hipStream_t ls = (rot & 1) ? s2 : s_compute_;
+      hipStream_t ls = (s2 && (rot & 1)) ? s2 : s_compute_;
       // the same launch on the next scratch pair (same sizes and offsets)
       const Buffer& bi = scratch[(size_t)(2 * (rot % nrot))];
       const Buffer& bo = scratch[(size_t)(2 * (rot % nrot) + 1)];

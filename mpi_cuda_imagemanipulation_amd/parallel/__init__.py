@@ -453,6 +453,9 @@ class FrameStream:
         over ranks), not one its own timing noise picked.  Every rank calls
         tune() together."""
         e0 = self.head.engine
+        # a frame stream held to one stream tunes on one (cold tunes otherwise
+        # alternate two, the probe's usual pick)
+        e0.set_tune_streams(max(self.stream_options) if self.streams else 1)
         collective = (reduce_max is not None and getattr(self, "world", 1) > 1 and bool(self.streams)
                       and getattr(self, "every_rank_has_rows", False))
         if collective:

@@ -226,6 +226,16 @@ tune)
     timeout -k 10 300 python bench.py --steps 20 --warmup 5 --dist-steps 0 --ref-steps 0 --e2e-steps 0 --deep-steps 0 >> $O/n1.json 2>> $O/n1.err || exit 3
   done
   ;;
+tune1)
+  # the one-stream tune (set_tune_streams): a frame stream pinned to one
+  # stream, and the probe's pick, three processes each
+  timeout -k 10 600 python -u -m pytest tests/test_r6_tune.py -m gpu -q -x --timeout 200 --timeout-method thread > $O/tests.txt 2>&1 || exit 2
+  X="--height 2048 --steps 200 --warmup 20 --dist-steps 0 --ref-steps 0 --e2e-steps 0 --deep-steps 0"
+  for r in 1 2 3; do
+    timeout -k 10 300 python bench.py $X --streams 1 >> $O/share_s1.json 2>> $O/share_s1.err || exit 3
+    timeout -k 10 300 python bench.py $X >> $O/share_auto.json 2>> $O/share_auto.err || exit 3
+  done
+  ;;
 onestream)
   # the N=8 share's cold step on one stream vs the probe's pick (VERDICT r5
   # item 5: one-stream step <= 0.042 ms), no exchange, three processes each
