@@ -236,6 +236,17 @@ tune1)
     timeout -k 10 300 python bench.py $X >> $O/share_auto.json 2>> $O/share_auto.err || exit 3
   done
   ;;
+bands1)
+  # 16K headline on two streams at fixed bands (is the one-stream tune's 16
+  # right when the probe keeps two streams?), two alternating rounds
+  X="--steps 100 --warmup 10 --streams 2 --dist-steps 0 --ref-steps 0 --e2e-steps 0 --deep-steps 0"
+  for r in 1 2; do
+    for b in 12 16 24 32; do
+      timeout -k 10 300 python bench.py $X --band $b >> $O/n1_b$b.json 2>> $O/n1_b$b.err || exit 3
+    done
+    timeout -k 10 300 python bench.py $X >> $O/n1_auto.json 2>> $O/n1_auto.err || exit 3
+  done
+  ;;
 onestream)
   # the N=8 share's cold step on one stream vs the probe's pick (VERDICT r5
   # item 5: one-stream step <= 0.042 ms), no exchange, three processes each
