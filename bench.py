@@ -346,6 +346,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(a.steps):
         step(i)
+    t_issue = time.perf_counter()  # the host's issue time (no sync yet): near t1 - t0 means host-bound steps
     sync_frames()
     sync()
     barrier()
@@ -494,6 +495,10 @@ def main():
         # per copy (events between copies, vs step_ms_device) and back to back
         # (burst, vs the host-clock ms_per_step)
         "step_ms_device": step_ms,
+        # rank 0's host time to issue the K timed steps, per step (the GPU
+        # time is ms_per_step: a host issue time close to it means the host
+        # loop, not the GPU, sets the step)
+        "host_issue_ms_per_step": round((t_issue - t0) * 1e3 / a.steps, 5),
         "bytes_per_step_per_gpu": step_bytes,
         "copy_roofline_ms": None if copy_ms is None else round(copy_ms, 5),
         "frac_of_copy_roofline": None if not (copy_ms and med) else round(copy_ms / med, 4),

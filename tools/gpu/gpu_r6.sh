@@ -247,6 +247,16 @@ bands1)
     timeout -k 10 300 python bench.py $X >> $O/n1_auto.json 2>> $O/n1_auto.err || exit 3
   done
   ;;
+hostissue)
+  # the host's issue time per step beside the step time: N=8 share with and
+  # without the RCCL exchange, and the 16K headline
+  X="--steps 200 --warmup 20 --dist-steps 0 --ref-steps 0 --e2e-steps 0 --deep-steps 0"
+  for r in 1 2; do
+    timeout -k 10 300 python bench.py --height 2048 $X >> $O/share_plain.json 2>> $O/share_plain.err || exit 3
+    timeout -k 10 300 python bench.py --height 2048 $X --self-halo >> $O/share_self.json 2>> $O/share_self.err || exit 3
+    timeout -k 10 300 python bench.py --steps 50 --warmup 5 --dist-steps 0 --ref-steps 0 --e2e-steps 0 --deep-steps 0 >> $O/n1.json 2>> $O/n1.err || exit 3
+  done
+  ;;
 onestream)
   # the N=8 share's cold step on one stream vs the probe's pick (VERDICT r5
   # item 5: one-stream step <= 0.042 ms), no exchange, three processes each
