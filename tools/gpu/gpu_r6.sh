@@ -257,6 +257,17 @@ hostissue)
     timeout -k 10 300 python bench.py --steps 50 --warmup 5 --dist-steps 0 --ref-steps 0 --e2e-steps 0 --deep-steps 0 >> $O/n1.json 2>> $O/n1.err || exit 3
   done
   ;;
+streams4)
+  # the N=8 share's frames on 2 vs 3 vs 4 streams (4 frames; pinned counts,
+  # each with its own tune), alternating
+  X="--height 2048 --steps 200 --warmup 20 --dist-steps 0 --ref-steps 0 --e2e-steps 0 --deep-steps 0"
+  for r in 1 2; do
+    for n in 2 3 4; do
+      timeout -k 10 300 python bench.py $X --streams $n >> $O/share_s$n.json 2>> $O/share_s$n.err || exit 3
+    done
+    timeout -k 10 300 python bench.py $X --streams 4 --frames 8 >> $O/share_s4_f8.json 2>> $O/share_s4_f8.err || exit 3
+  done
+  ;;
 onestream)
   # the N=8 share's cold step on one stream vs the probe's pick (VERDICT r5
   # item 5: one-stream step <= 0.042 ms), no exchange, three processes each
