@@ -81,6 +81,27 @@ local)
     done
   done
   ;;
+local2)
+  # one shared stream for the local ranks of one GPU (STRIPE_LOCAL_STREAMS=own:
+  # a stream per rank, round 6's first form): the tests of every local-rank
+  # path, then depth 1 and the automatic depth, alternating.  The shared
+  # stream lost and was removed after the run (profiles/r6/local2/); today
+  # both settings run a stream per rank
+  timeout -k 10 900 python -u -m pytest tests/test_r6_local.py tests/test_gpu_engine.py tests/test_dist_pipelined.py tests/test_deep_halo.py tests/test_advice_r2.py tests/test_weighted_split.py tests/test_n8.py tests/test_multi_gpu.py tests/test_r5_order.py tests/test_resilience.py -m gpu -q -x --timeout 200 --timeout-method thread > $O/tests.txt 2>&1 || exit 2
+  CFG3="bin/stripe bench --synthetic 8192x8192x1 --chain sobel --ranks 4 --iters 64 --warmup 8 --scope resident --backend local"
+  for r in 1 2; do
+    for st in own shared; do
+      for rounds in 0 1; do
+        for sc in serial overlap; do
+          echo "streams $st rounds $rounds schedule $sc depth 1" >> $O/cfg3_depth1.txt
+          STRIPE_LOCAL_STREAMS=$st STRIPE_LOCAL_ROUNDS=$rounds STRIPE_HALO_SCHEDULE=$sc timeout -k 10 120 $CFG3 --halo-depth 1 2>&1 | grep -v amdgpu.ids >> $O/cfg3_depth1.txt || exit 3
+        done
+      done
+      echo "streams $st depth auto" >> $O/cfg3_auto.txt
+      STRIPE_LOCAL_STREAMS=$st timeout -k 10 120 $CFG3 2>&1 | grep -v amdgpu.ids >> $O/cfg3_auto.txt || exit 3
+    done
+  done
+  ;;
 blurdiag)
   # which memory stream sets blur:31's time: loads / stores masked out of range
   # (STRIPE_BLUR_VARIANT 7 / 8 / 9, wrong output, timing only), alternating
