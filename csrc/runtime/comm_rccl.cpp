@@ -191,7 +191,7 @@ class RcclComm final : public Comm {
     if (!s) return;
     const auto t0 = std::chrono::steady_clock::now();
     const double limit = comm_timeout_s();
-    for (int it = 0;; ++it) {
+    for (;;) {
       enter();
       const hipError_t e = hipStreamQuery(s);
       if (e == hipSuccess) {
