@@ -81,6 +81,32 @@ local)
     done
   done
   ;;
+kpf)
+  # k_sep rows in flight per lane (STRIPE_KPF, non-skip non-gray instances):
+  # the default build (4) vs packages built with 6 and 8 under build_alt_kpf*/
+  # (imported first, so bench.py runs them), the headline (the driver's
+  # command) and the N=8 share, alternating
+  PK="import sys; sys.path.insert(0, sys.argv[1]); import mpi_cuda_imagemanipulation_amd as m, runpy; print('package', m._C.__file__, file=sys.stderr); sys.argv = sys.argv[2:]; runpy.run_path(sys.argv[0], run_name='__main__')"
+  for r in 1 2 3; do
+    for v in 4 6 8; do
+      P=.; [ $v != 4 ] && P=build_alt_kpf$v
+      timeout -k 10 300 python -c "$PK" $P bench.py --gpus 1 --steps 20 --warmup 5 >> $O/head_kpf$v.json 2>> $O/head_kpf$v.err || exit 3
+      timeout -k 10 300 python -c "$PK" $P bench.py $SHARE >> $O/share_kpf$v.json 2>> $O/share_kpf$v.err || exit 3
+    done
+  done
+  ;;
+kpf2)
+  # the same packages through tools/kbench.py: every k_sep filter family, the
+  # 16K frame and the N=8 share, tuned bands, alternating
+  PK="import sys; sys.path.insert(0, sys.argv[1]); import mpi_cuda_imagemanipulation_amd as m, runpy; print('package', m._C.__file__, file=sys.stderr); sys.argv = sys.argv[2:]; runpy.run_path(sys.argv[0], run_name='__main__')"
+  for r in 1 2 3; do
+    for v in 4 8 6; do
+      P=.; [ $v != 4 ] && P=build_alt_kpf$v
+      timeout -k 10 200 python -c "$PK" $P tools/kbench.py --shape 16384x16384x3 --chains "gaussian5|gaussian3|box5|sobel|sharpen" --bands=-1 --iters 30 >> $O/k16_kpf$v.json 2>> $O/kpf$v.err || exit 3
+      timeout -k 10 200 python -c "$PK" $P tools/kbench.py --shape 16384x2048x3 --chains "gaussian5|gaussian3|box5|sobel|sharpen" --bands=-1 --iters 100 >> $O/kshare_kpf$v.json 2>> $O/kpf$v.err || exit 3
+    done
+  done
+  ;;
 local2)
   # one shared stream for the local ranks of one GPU (STRIPE_LOCAL_STREAMS=own:
   # a stream per rank, round 6's first form): the tests of every local-rank
