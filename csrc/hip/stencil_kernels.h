@@ -584,7 +584,7 @@ __device__ __forceinline__ void sep_task(const KArgs& a, const WaveTask& t, cons
   // kernel is bound by); loads past the band re-read its last input row
   // (unconditional: no branch around the load)
   // (a gray prologue reads 48 bytes per row: 2 rows give more bytes in flight
-  // than 4 plain rows, at 24 fewer registers; 6 or 8 plain rows ran 5-8 %
+  // than 4 plain rows, at 24 fewer registers; 6 or 8 plain rows ran 2-11 %
   // slower on warm N=8 shares and no faster on 16K frames, profiles/r6/kpf/)
   constexpr int kPF = is_gray(PRO) ? 2 : 4;
   RawChunk<PRO> nx[kPF];
