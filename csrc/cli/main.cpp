@@ -680,7 +680,7 @@ void usage() {
                "        [--scope resident|device,dist,e2e] [--backend rccl|local|host] [--json out.json]\n"
                "        [--no-overlap] [--no-pipeline] [--graphs] [--band ROWS] [--halo-depth K] [--dist-chunks K]\n"
                "        [--frames F]  (resident: a stream of F independent frames, cache-cold tuning)\n"
-               "        [--halo-schedule auto|serial|overlap|pipeline]  (frames at N > 1: auto times all three)\n"
+               "        [--halo-schedule auto|serial|overlap|pipeline|batched]  (frames at N > 1: auto times each)\n"
                "  cmp   a.ppm b.ppm [--tol T]\n"
                "  gen   --synthetic WxHxC [--seed S] --output out.ppm|out.jpg\n"
                "  convert --input in.ppm|in.jpg --output out.ppm|out.jpg [--quality 95]\n"
