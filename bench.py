@@ -6,15 +6,20 @@ row-partitioned over N MI355X (one process per GPU, RCCL over xGMI).
     (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
 
 One step = one full-frame gaussian5 pass over the distributed frame: every rank
-exchanges its 2 halo rows with its neighbours (ncclSend/ncclRecv, every step:
-halo depth 1) and filters its stripe.  How the exchange meets the filter is
-measured, not assumed: at N > 1 the three halo schedules (exchange then filter;
-interior rows beside the exchange, boundary rows after it; core / rim / edge
-on three streams; serial steps whose exchanges are posted as one group per
-stream and round), each with frames on one stream or alternating over two, are
-timed on the real transport before the timed region and the fastest is kept
-(max over ranks; `halo_schedule` in the record).  Steps are iterated
-(ping-pong), so each step's halo rows are required work.
+filters its stripe with the halo rows its neighbours sent (ncclSend/ncclRecv).
+How the exchange meets the filter is measured, not assumed.  At N > 1 the
+probe times every halo schedule on the real transport before the timed region
+and keeps the fastest (max over ranks; `halo_schedule` in the record):
+  * exchange then filter;
+  * interior rows beside the exchange, boundary rows after it;
+  * core / rim / edge on three streams;
+  * serial steps whose exchanges go out as one group per stream and round;
+  * each frame's next exchange posted right after its step;
+  * the "+deep" forms: a frame exchanges k*2 rows every k-th step and
+    recomputes a shrinking band of its neighbours' rows in between
+    (bit-identical; `halo_depth` in the record).
+Each is timed with the frames on one stream or alternating over two.  Steps
+are iterated (ping-pong), so each step's halo rows are required work.
 
 Cache temperature of the headline.  A step's per-GPU working set is its stripe
 in + out: 1.61 GB on one GPU, 201 MB on each of 8.  When it fits the 256 MiB
@@ -91,11 +96,14 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--band", type=int, default=0)
-    ap.add_argument("--halo-schedule", default="auto", choices=["auto", "serial", "overlap", "pipeline", "batched", "ahead"],
+    ap.add_argument("--halo-schedule", default="auto",
+                    choices=["auto", "serial", "overlap", "pipeline", "batched", "ahead", "serial+deep", "batched+deep",
+                             "ahead+deep"],
                     help="halo schedule of the headline steps at N>1 (auto: time each on the real transport before "
                          "the timed region and keep the fastest, max over ranks; batched: serial steps with the "
                          "exchanges of the frames sharing a stream in one group per round; ahead: each frame's next "
-                         "exchange posted right after its step on a communication stream of its own)")
+                         "exchange posted right after its step on a communication stream of its own; +deep: "
+                         "a frame exchanges k*S rows every k-th step, --halo-depth)")
     ap.add_argument("--frames", type=int, default=0,
                     help="frames the headline steps over (0: auto -- enough to defeat the Infinity Cache when a "
                          "stripe fits it, else 2 at N>1 so one frame's exchange runs beside the other's filter, "
@@ -106,7 +114,9 @@ def parse():
                          "kernel boundary overlaps the next frame's step; 1: strictly serial steps)")
     ap.add_argument("--deep-steps", type=int, default=-1, help="steps of the deep-halo scope (-1: --steps; 0: skip)")
     ap.add_argument("--halo-depth", type=int, default=0,
-                    help="steps per exchange of the resident_deep scope (0: auto); the headline exchanges every step")
+                    help="steps per deep-halo exchange (0: auto; 1: every step): the headline's deep schedules "
+                         "(serial+deep, batched+deep, ahead+deep: a frame exchanges k*S rows every k-th step) and the "
+                         "resident_deep scope")
     ap.add_argument("--dist-steps", type=int, default=5, help="steps of each dist-scope measurement (0: skip)")
     ap.add_argument("--ref-steps", type=int, default=3, help="steps of the ref-window measurement (0: skip)")
     ap.add_argument("--e2e-steps", type=int, default=3, help="steps of the e2e-scope measurement (0: skip)")
@@ -302,7 +312,9 @@ def main():
     if a.self_halo:
         # the ref-window and e2e scopes verify a non-periodic frame: not run here
         a.ref_steps = a.e2e_steps = 0
-    pipe1 = Pipeline(a.chain, overlap=not a.no_overlap, halo_depth=1, self_halo=a.self_halo)
+    # the frames' engines hold a deep halo (a.halo_depth, auto by default) so the
+    # probe can time the deep schedules; the others exchange every step
+    pipe1 = Pipeline(a.chain, overlap=not a.no_overlap, halo_depth=a.halo_depth, self_halo=a.self_halo)
     fs = parallel.FrameStream(ctx, pipe1, W, H, Cc, frames=a.frames, streams=a.streams, autotune=not a.no_autotune)
     ws_max, fits_mall, cold = fs.ws_max, fs.fits_mall, fs.cold
     nframes, nstreams = len(fs), fs.nstreams
@@ -444,6 +456,11 @@ def main():
             ok &= same(out[0:reach], ref[2 * reach:3 * reach])
         verify = all_ok(ok)
 
+    # the other scopes run one step per input (or their own schedule): the
+    # head engine leaves the deep block here
+    head_depth = fs.depth if fs.deep else 1
+    fs.set_deep(False)
+
     # ---- same-box roofline: the framework's hand-written linear copy of the
     # same bytes per step (csrc/hip/pointwise.hip k_copy_linear: one 16-byte
     # chunk per lane, the faster of two store policies), rotating over enough
@@ -459,7 +476,7 @@ def main():
     copy_ms = copy["event_ms"] if copy else None
 
     scopes = {"resident": {"mpx_s": round(mpx, 1), "ms": round(ms_per_step, 5), "verified": verify,
-                           "frames": nframes, "streams": nstreams, "halo_depth": 1, "cache": fs.cache}}
+                           "frames": nframes, "streams": nstreams, "halo_depth": head_depth, "cache": fs.cache}}
     med = step_ms["median"] if step_ms else None
     rec = {
         "metric": METRIC,
@@ -514,7 +531,7 @@ def main():
                   "task_orders": dp.engine.orders,
                   "cold": cold, "streaming_policy": fs.streaming},
         "cache": fs.cache,
-        "halo_depth": 1,
+        "halo_depth": head_depth,
         "halo_schedule": sched,
         "self_halo": bool(a.self_halo),
         "exchange_cost": exchange_cost(comm_before, comm_after, a.steps),
@@ -567,14 +584,22 @@ def main():
         if nframes == 1 or not iterable:
             return
         ramp()
+        we = dp
+        if dp.engine.halo_depth > 1:  # run(n) would run a deep block: this scope exchanges every step
+            we = parallel.DistributedPipeline(ctx, Pipeline(a.chain, overlap=not a.no_overlap, halo_depth=1), W, H, Cc)
+            we.engine.set_tuning(dp.engine.bands, dp.engine.caps, dp.engine.policies, dp.engine.orders)
+            we.load_synthetic(a.seed)
+            we.run(2)
+            we.synchronize()
         sync()
         barrier()
         t0 = time.perf_counter()
-        dp.run(a.steps)
-        dp.synchronize()
+        we.run(a.steps)
+        we.synchronize()
         sync()
         barrier()
         wms = max_over_ranks((time.perf_counter() - t0) * 1e3) / a.steps
+        del we
         scopes["resident_warm"] = {"mpx_s": round(W * H / (wms * 1e-3) / 1e6, 1), "ms": round(wms, 5),
                                    "frames": 1, "halo_depth": 1}
 

@@ -198,6 +198,20 @@ class Engine {
   // front of this one's.  Any other use of the input first waits for a
   // pending exchange (settle_post).
   void post_halo_ahead(hipStream_t comm);
+  // Deep steps ("deep frames"): run(1) advances a deep-halo block by one
+  // step.  Every halo_depth()-th step exchanges k*S rows, where S is the
+  // chain's reach; the k - 1 steps after it recompute a shrinking band of the
+  // neighbours' rows and exchange nothing.  The result is bit-exact, and one
+  // exchange serves k steps.  run(n) does the same in one call (run_deep).
+  // Step by step, a frame stream keeps its frames interleaved: every step of
+  // every frame still reads a cold stripe.  post_halo / post_halo_ahead /
+  // run_posted post the k*S rows on the steps that exchange and nothing on
+  // the others.  Only with halo_depth() > 1 (EngineConfig::halo_depth; the
+  // buffers hold k*S halo rows); loading new input restarts the block.
+  void set_deep_steps(bool on);
+  bool deep_steps() const { return deep_steps_; }
+  // the next step exchanges halo rows (deep steps: the first of a block)
+  bool exchange_due() const { return !deep_stepping() || deep_phase_ == 0; }
   // Tuned band heights, occupancy caps and memory policies per pass (after
   // autotune), for reporting.
   std::vector<int> bands() const;
@@ -312,6 +326,10 @@ class Engine {
   // drop a post nobody consumed; a pending ahead exchange is first waited for
   // on the compute stream (it may still write this input's halo rows)
   void settle_post();
+  bool deep_stepping() const;
+  void deep_step();
+  bool deep_steps_ = false;  // set_deep_steps
+  int deep_phase_ = 0;       // steps of the current deep block done (0: the next one exchanges)
   bool halo_done_ = false;  // run_posted(): this step's exchange already happened
   // this rank exchanges halo rows (another active rank, or the self-halo ring)
   bool neighbours() const { return part_.active > 1 || self_halo_; }

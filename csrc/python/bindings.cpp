@@ -576,6 +576,11 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("halo_depth", &Engine::halo_depth)
       .def_property_readonly("self_halo", &Engine::self_halo)
       .def_property_readonly("posts_halo", &Engine::posts_halo)
+      .def_property("deep_steps", &Engine::deep_steps, [](Engine& e, bool on) {
+        py::gil_scoped_release nogil;
+        e.set_deep_steps(on);
+      })
+      .def_property_readonly("exchange_due", &Engine::exchange_due)
       .def("post_halo", [](Engine& e) {
         py::gil_scoped_release nogil;
         e.post_halo();

@@ -382,6 +382,7 @@ void Engine::fill_margins(uint8_t* org, int C, int y0, int y1, int px, Border b,
 
 void Engine::load_synthetic(uint64_t seed) {
   settle_post();
+  deep_phase_ = 0;
   TraceRange tr("stripe.load");
   fault_point("load", rank_);
   const Stripe& st = stripe();
@@ -403,6 +404,7 @@ void Engine::load_synthetic(uint64_t seed) {
 
 void Engine::load_packed(const void* src, bool src_device) {
   settle_post();
+  deep_phase_ = 0;
   (void)src_device;
   const Stripe& st = stripe();
   const int C = plan_.cin;
@@ -464,6 +466,7 @@ void Engine::load_root_synthetic(uint64_t seed) {
 
 void Engine::scatter() {
   settle_post();
+  deep_phase_ = 0;
   const int C = plan_.cin;
   const int64_t P = pitch(C);
   const Stripe& st = stripe();
@@ -578,8 +581,9 @@ void Engine::post_halo() {
   STRIPE_CHECK(cur_c_ == plan_.cin, "post_halo: the engine input has " << cur_c_ << " channels");
   const Pass& p = plan_.passes[0];
   STRIPE_CHECK(!self_halo_ || p.R <= stripe().rows, "self-halo of " << p.R << " rows needs a stripe that tall");
+  if (!exchange_due()) return;  // a deep block's later step: nothing to exchange
   fault_point("halo", rank_);
-  post_halo_ops(origin(buf_[cur_], p.cin), p.cin, p.R, s_compute_);
+  post_halo_ops(origin(buf_[cur_], p.cin), p.cin, deep_stepping() ? depth_ * chain_reach() : p.R, s_compute_);
   posted_buf_ = cur_;
 }
 
@@ -589,6 +593,7 @@ void Engine::post_halo_ahead(hipStream_t comm) {
   STRIPE_CHECK(cur_c_ == plan_.cin, "post_halo_ahead: the engine input has " << cur_c_ << " channels");
   if (posted_buf_ == cur_) return;  // this input's exchange is already posted
   settle_post();
+  if (!exchange_due()) return;  // a deep block's later step: nothing to exchange
   const Pass& p = plan_.passes[0];
   STRIPE_CHECK(!self_halo_ || p.R <= stripe().rows, "self-halo of " << p.R << " rows needs a stripe that tall");
   for (auto& e : ahead_ev_)
@@ -597,7 +602,7 @@ void Engine::post_halo_ahead(hipStream_t comm) {
   HIP_CHECK(hipEventRecord(ahead_ev_[0], s_compute_));
   HIP_CHECK(hipStreamWaitEvent(comm, ahead_ev_[0], 0));
   comm_->group_start();
-  post_halo_ops(origin(buf_[cur_], p.cin), p.cin, p.R, comm);
+  post_halo_ops(origin(buf_[cur_], p.cin), p.cin, deep_stepping() ? depth_ * chain_reach() : p.R, comm);
   comm_->group_end();
   HIP_CHECK(hipEventRecord(ahead_ev_[1], comm));
   posted_buf_ = cur_;
@@ -768,7 +773,14 @@ void Engine::run(int iterations) {
     }
   };
   const int cycle = plan_.passes.size() % 2 == 0 ? 1 : 2;
-  if (halo_done_) {  // run_posted: the halo rows already came in the caller's group
+  if (deep_stepping() && cur_c_ == plan_.cin) {  // set_deep_steps: one deep-block step per iteration
+    for (int it = 0; it < iterations; ++it) {
+      time_halo_ = it == iterations - 1;
+      deep_step();
+      halo_done_ = false;  // a posted exchange serves the first step only
+    }
+    cur_c_ = plan_.cout;
+  } else if (halo_done_) {  // run_posted: the halo rows already came in the caller's group
     iterate(iterations);
   } else if (depth_ >= 1 && cur_c_ == plan_.cin && ((depth_ > 1 && iterations > 1) || plan_.passes.size() > 1)) {
     run_deep(iterations);
@@ -845,6 +857,7 @@ std::vector<float> Engine::run_timed(int iterations, int per, bool rewind_each) 
 
 void Engine::rewind() {
   settle_post();
+  deep_phase_ = 0;
   cur_ = run_in_buf_;
   cur_c_ = plan_.cin;
 }

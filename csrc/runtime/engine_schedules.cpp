@@ -149,7 +149,7 @@ int Engine::chain_reach() const {
 }
 
 int Engine::choose_depth() const {
-  if (!cfg_.halo || part_.active <= 1) return 0;
+  if (!cfg_.halo || !neighbours()) return 0;  // (self-halo: one rank, its own neighbours)
   if (const char* e = std::getenv("STRIPE_DEEP"); e && std::atoi(e) == 0) return 0;  // A/B: per-pass exchange
   const int S = chain_reach();
   if (S <= 0) return 0;
@@ -177,7 +177,7 @@ int Engine::choose_depth() const {
 void Engine::run_deep(int iterations) {
   const int S = chain_reach(), rows = stripe().rows;
   if (rows == 0) return;
-  const bool up = rank_ > 0, down = rank_ + 1 < part_.active;
+  const bool up = has_up(), down = has_down();
   const Pass& p0 = plan_.passes[0];
   const int R0 = p0.R;
   // the block's exchange flies on the comm stream beside the first pass's
@@ -240,6 +240,50 @@ void Engine::run_deep(int iterations) {
   }
   cur_c_ = plan_.cout;
   time_halo_ = true;
+}
+
+void Engine::set_deep_steps(bool on) {
+  settle_post();
+  deep_steps_ = on;
+  deep_phase_ = 0;
+}
+
+bool Engine::deep_stepping() const {
+  return deep_steps_ && depth_ > 1 && plan_.cin == plan_.cout && chain_reach() > 0;
+}
+
+// One step of a deep-halo block (set_deep_steps): run_deep's loop body for
+// step deep_phase_ of a depth_-step block, so callers can interleave other work
+// (a frame stream's other frames) between the steps.  The block's first step
+// exchanges depth_ * S rows (unless run_posted's group already did); step i
+// then computes its passes over the stripe plus (depth_ - i) * S - R rows of
+// each neighbour, rows every later step of the block reads.
+void Engine::deep_step() {
+  const int S = chain_reach(), rows = stripe().rows, m = depth_, i = deep_phase_;
+  deep_phase_ = (i + 1) % m;
+  if (rows == 0) return;
+  const bool up = has_up(), down = has_down();
+  const Pass& p0 = plan_.passes[0];
+  if (i == 0 && !halo_done_) exchange_halo(origin(buf_[cur_], p0.cin), p0.cin, m * S, s_compute_);
+  int reach = (m - i) * S;  // halo rows valid in the current input
+  for (size_t k = 0; k < plan_.passes.size(); ++k) {
+    const Pass& p = plan_.passes[k];
+    reach -= p.R;  // halo rows this pass's output must cover
+    const int y0 = up ? -reach : 0, y1 = rows + (down ? reach : 0);
+    uint8_t* in = origin(buf_[cur_], p.cin);
+    uint8_t* out = origin(buf_[cur_ ^ 1], p.cout);
+    if (device()) {
+      PassLaunch L = make_launch(p, in, out, (int)k);
+      L.ext = reach;
+      L.nrange = 1;
+      L.ry[0] = y0;
+      L.ry[1] = y1;
+      launch_pass(p, prt_[k].pc, L, s_compute_);
+    } else {
+      cpu_pass(p, ConstView{in, pitch(p.cin)}, MutView{out, pitch(p.cout)}, cfg_.W, geom(), y0, y1, host_threads());
+    }
+    cur_ ^= 1;
+  }
 }
 
 }  // namespace stripe

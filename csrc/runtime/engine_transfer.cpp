@@ -80,6 +80,7 @@ void Engine::run_e2e(int chunks) {
   HIP_CHECK(hipStreamWaitEvent(s_h2d_, ev_[3], 0));  // ...and this step's input buffer is free
   cur_ = 0;
   cur_c_ = cin;
+  deep_phase_ = 0;
   uint8_t* in_org = origin(buf_[0], cin);
   uint8_t* hin_dev = nullptr;
   uint8_t* hout_dev = nullptr;
@@ -437,6 +438,7 @@ void Engine::run_dist(int chunks) {
   run_in_buf_ = 0;
   cur_ = 1;
   cur_c_ = cout;
+  deep_phase_ = 0;
   out_buf_ = 1;
   out_c_ = cout;
 }
@@ -501,6 +503,7 @@ void Engine::run_to_host(void* dst, int chunks) {
   stage_end(Stage::E2E, s_d2h_);
   join_d2h();
   if (single) {  // the input stays current: the next step filters the same frame
+    deep_phase_ = 0;
     cur_ = in_buf;
     cur_c_ = plan_.cin;
     run_in_buf_ = in_buf;

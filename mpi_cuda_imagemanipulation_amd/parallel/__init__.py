@@ -375,6 +375,10 @@ class FrameStream:
                 f.engine.stage_timing = stage_timing
         self.set_streams(nmax)
         self._i = 0
+        # steps per deep-halo block the frames' engines allow (halo_depth of
+        # the pipeline; 1: every step exchanges), and whether they use it
+        self.depth = max(1, self.head.engine.halo_depth)
+        self.deep = False
 
     @staticmethod
     def shares_gpu(ctx: DistContext) -> bool:
@@ -469,6 +473,18 @@ class FrameStream:
             f.engine.set_tuning(e0.bands, e0.caps, e0.policies, e0.orders)
 
     SCHEDULES = ("pipeline", "overlap", "serial", "batched", "ahead")
+    # with a deep halo (depth > 1): these schedules, each frame exchanging
+    # depth * S rows every depth-th step (Engine.deep_steps)
+    DEEP_SCHEDULES = ("serial+deep", "batched+deep", "ahead+deep")
+
+    def set_deep(self, on: bool):
+        """Deep steps for every frame: a frame exchanges depth * S rows on
+        every depth-th step and none on the others, bit-exact
+        (Engine.deep_steps).  Each step is still one step of the next frame, so
+        every step reads a cold stripe.  No-op at depth 1."""
+        self.deep = bool(on) and getattr(self, "depth", 1) > 1
+        for f in self.frames:
+            f.engine.deep_steps = self.deep
 
     def set_schedule(self, name: str):
         """Halo schedule of every frame ("serial" | "overlap" | "pipeline" |
@@ -481,11 +497,16 @@ class FrameStream:
         right after its step, on a communication stream of its own
         (Engine.post_halo_ahead): the rows are needed a whole round later, so
         the exchange runs beside the other frames' filters and the frame's
-        next step only waits for an event that has long fired."""
-        self.batched = name == "batched"
-        self.ahead = name == "ahead"
+        next step only waits for an event that has long fired.
+        A "+deep" suffix (DEEP_SCHEDULES) adds deep steps (set_deep)."""
+        base, _, deep = name.partition("+")
+        if deep not in ("", "deep"):
+            raise ValueError(f"unknown halo schedule {name!r}")
+        self.set_deep(deep == "deep")
+        self.batched = base == "batched"
+        self.ahead = base == "ahead"
         for f in self.frames:
-            f.engine.halo_schedule = "serial" if (self.batched or self.ahead) else name
+            f.engine.halo_schedule = "serial" if (self.batched or self.ahead) else base
 
     def _batch_candidate(self) -> bool:
         """Whether the probe times "batched" and "ahead": frames of device engines that
@@ -505,11 +526,21 @@ class FrameStream:
         """Ahead posts apply: device engines that exchange halo rows."""
         return bool(getattr(self, "ahead", False) and self.streams and self.head.engine.posts_halo)
 
+    def _deep_candidate(self) -> bool:
+        """Whether the probe times the DEEP_SCHEDULES: frames that exchange
+        halo rows (as _batch_candidate) with a halo depth above 1 (the same on
+        every rank: the engines derive it from the whole partition)."""
+        return getattr(self, "depth", 1) > 1 and self._batch_candidate()
+
     @property
     def schedule(self) -> str:
         if self._batches():
-            return "batched"
-        return "ahead" if self._aheads() else self.head.engine.halo_schedule
+            base = "batched"
+        elif self._aheads():
+            base = "ahead"
+        else:
+            base = self.head.engine.halo_schedule
+        return base + ("+deep" if getattr(self, "deep", False) and self.head.engine.posts_halo else "")
 
     def pick_schedule(self, reduce_max=None, barrier=None, steps: int = 0, rounds: int = 2) -> dict:
         """Time every halo schedule (interior / boundary overlap, the
@@ -531,6 +562,8 @@ class FrameStream:
         # pipeline); host engines have one schedule and time nothing
         scheds = ([s for s in self.SCHEDULES if s not in ("batched", "ahead") or self._batch_candidate()]
                   if self.streams else ["serial"])
+        if self.streams and self._deep_candidate():
+            scheds += list(self.DEEP_SCHEDULES)
         if getattr(getattr(self.head, "ctx", None), "world", 2) == 1:
             # one rank exchanges nothing: only schedules that differ on it (none)
             eff = []
@@ -598,7 +631,7 @@ class FrameStream:
         if not self.iterable:  # a chain that changes the channel count re-reads its (unchanged) input
             f.engine.rewind()
         if self._batches():
-            if k < self.nstreams:
+            if k < self.nstreams and f.engine.exchange_due:
                 # the first frame of its stream this round: one group with the
                 # exchanges of every frame on this stream (k, k + s, k + 2s, ...)
                 comm = f.ctx.comm

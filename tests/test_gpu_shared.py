@@ -56,7 +56,9 @@ def test_bench_gloo_gpu_processes(tmp_path, n):
     import torch
 
     hs = rec["halo_schedule"]
-    scheds = ("serial", "overlap", "pipeline", "batched", "ahead")
+    # (768- / 384-row stripes: an auto halo depth of 4 / 2, so the deep
+    # schedules are candidates too)
+    scheds = ("serial", "overlap", "pipeline", "batched", "ahead", "serial+deep", "batched+deep", "ahead+deep")
     if n > torch.cuda.device_count():
         assert hs["queues"] == "plain"
         assert set(hs["ms"]) == {f"{s}@{k}" for s in scheds for k in (1, 2)}
@@ -66,6 +68,7 @@ def test_bench_gloo_gpu_processes(tmp_path, n):
     multi = any("/" in k for k in hs["ms"])
     key = f"{hs['chosen']}@{hs['streams']}" + (f"/{hs['queues']}" if hs["streams"] > 1 and multi else "")
     assert key == min(hs["ms"], key=hs["ms"].get) and rec["streams"] == hs["streams"]
+    assert (rec["halo_depth"] > 1) == ("+deep" in hs["chosen"])  # the record names the depth the steps ran
     for name, sc in rec["scopes"].items():
         assert "error" not in sc, (name, sc)
         if "verified" in sc:

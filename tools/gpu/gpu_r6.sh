@@ -81,6 +81,21 @@ local)
     done
   done
   ;;
+deep)
+  # deep frames (a frame exchanges k*2 rows every k-th step): GPU tests, then
+  # the self-halo N=8 share (RCCL loopback every exchange) under the probe
+  # (deep schedules among the candidates) and pinned schedules, alternating;
+  # then the self-halo shares of N = 2 / 4 (the curve proxy) under the probe
+  timeout -k 10 900 python -u -m pytest tests/test_r6_deep_frames.py tests/test_r6_selfhalo.py tests/test_gpu_shared.py tests/test_deep_halo.py tests/test_r5_streams.py tests/test_r4_comm.py -m gpu -q -x --timeout 200 --timeout-method thread > $O/tests.txt 2>&1 || exit 2
+  for r in 1 2; do
+    for sc in auto batched batched+deep serial+deep ahead+deep; do
+      timeout -k 10 300 python bench.py $SHARE --self-halo --halo-schedule $sc >> $O/self_${sc}.json 2>> $O/self_${sc}.err || exit 3
+    done
+  done
+  for h in 8192 4096; do
+    timeout -k 10 300 python bench.py --height $h --steps 100 --warmup 10 --dist-steps 0 --ref-steps 0 --e2e-steps 0 --deep-steps 0 --self-halo >> $O/curve_h$h.json 2>> $O/curve_h$h.err || exit 3
+  done
+  ;;
 kpf)
   # k_sep rows in flight per lane (STRIPE_KPF, non-skip non-gray instances):
   # the default build (4) vs packages built with 6 and 8 under build_alt_kpf*/
