@@ -134,6 +134,14 @@ for sched in ("serial", "overlap", "pipeline"):
 # interleave character by character
 with open(f"result_{ctx.rank}.json", "w") as fh:
     json.dump(bad, fh)
+# explicit teardown: engines (and their communicator) before the process
+# group, every rank together, so no gloo work or thread outlives it at exit
+import gc, torch, torch.distributed as dist
+del fs
+gc.collect()
+torch.cuda.synchronize()
+dist.barrier()
+dist.destroy_process_group()
 '''
 
 

@@ -65,6 +65,15 @@ for chain, depth, sched, n_it in json.loads(os.environ["CASES"]):
     res.append({"chain": chain, "depth": fs.depth, "sched": fs.schedule, "deep": fs.deep, "worst": worst})
 with open(f"result_{ctx.rank}.json", "w") as fh:
     json.dump(res, fh)
+# explicit teardown: engines before the process group, every rank together
+import gc, torch.distributed as dist
+del fs
+gc.collect()
+if ctx.device:
+    import torch
+    torch.cuda.synchronize()
+dist.barrier()
+dist.destroy_process_group()
 '''
 
 
