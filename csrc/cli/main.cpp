@@ -441,7 +441,7 @@ int cmd_bench(const Args& a) {
       // round-robin, each engine on its own stream (parallel.FrameStream's
       // native counterpart: one frame's kernel boundary overlaps the next)
       const int nframes = scope == "resident" ? std::max(1, a.geti("frames", 1)) : 1;
-      std::vector<double> sched_ms(4, 0.0);  // frames mode: per-schedule step time, max over ranks
+      std::vector<double> sched_ms(5, 0.0);  // frames mode: per-schedule step time, max over ranks
       int chosen = -1;
       auto body = [&](int r) {
         try {
@@ -494,7 +494,18 @@ int cmd_bench(const Args& a) {
             // the first of them; each frame's step then runs without its own
             const int nstr = shared_streams ? std::min(2, nframes) : 0;
             const bool batch_ok = nstr > 0 && nframes > nstr;  // the same on every rank
+            // serial+deep (schedule 4, parallel.FrameStream's): each frame
+            // exchanges k*S rows every k-th step (Engine::set_deep_steps);
+            // the depth comes from the whole partition, the same on every rank
+            const bool deep_ok = fr[0]->halo_depth() > 1 && fr[0]->plan().cin == fr[0]->plan().cout;
             bool batched = false;
+            auto set_sched = [&](int sc) {
+              batched = sc == 3;
+              for (auto& fe : fr) {
+                fe->set_halo_schedule(sc >= 3 ? 0 : sc);
+                fe->set_deep_steps(sc == 4);
+              }
+            };
             auto fstep = [&](int i) {
               const int k = i % nframes;
               Engine& fe = *fr[(size_t)k];
@@ -523,20 +534,20 @@ int cmd_bench(const Args& a) {
             // --halo-schedule serial|overlap|pipeline|batched fixes one
             const std::string hs = a.get("halo-schedule", "auto");
             if (hs != "auto") {
-              STRIPE_CHECK(hs == "serial" || hs == "overlap" || hs == "pipeline" || hs == "batched",
-                           "--halo-schedule must be auto, serial, overlap, pipeline or batched");
-              batched = hs == "batched" && batch_ok;
-              for (auto& fe : fr) fe->set_halo_schedule(hs == "serial" || hs == "batched" ? 0 : hs == "overlap" ? 1 : 2);
+              STRIPE_CHECK(hs == "serial" || hs == "overlap" || hs == "pipeline" || hs == "batched" ||
+                               hs == "serial+deep",
+                           "--halo-schedule must be auto, serial, overlap, pipeline, batched or serial+deep");
+              set_sched(hs == "serial" ? 0 : hs == "overlap" ? 1 : hs == "pipeline" ? 2 : hs == "batched" ? 3 : 4);
+              batched = batched && batch_ok;
             } else if (N > 1 && backend != "host") {
               const int m = std::max(20, 4 * nframes);
-              for (int sc = 0; sc < 4; ++sc) {
-                if (sc == 3 && !batch_ok) {
+              for (int sc = 0; sc < 5; ++sc) {
+                if ((sc == 3 && !batch_ok) || (sc == 4 && !deep_ok)) {
                   std::lock_guard<std::mutex> lk(mu);
-                  sched_ms[3] = 1e30;
+                  sched_ms[(size_t)sc] = 1e30;
                   continue;
                 }
-                batched = sc == 3;
-                for (auto& fe : fr) fe->set_halo_schedule(sc == 3 ? 0 : sc);
+                set_sched(sc);
                 for (int i = 0; i < 2 * nframes; ++i) fstep(i);
                 for (auto& fe : fr) fe->synchronize();
                 g.comms[r]->barrier();
@@ -552,12 +563,11 @@ int cmd_bench(const Args& a) {
               int best = 0;
               {
                 std::lock_guard<std::mutex> lk(mu);
-                for (int sc = 1; sc < 4; ++sc)
+                for (int sc = 1; sc < 5; ++sc)
                   if (sched_ms[(size_t)sc] < sched_ms[(size_t)best]) best = sc;
                 chosen = best;
               }
-              batched = best == 3;
-              for (auto& fe : fr) fe->set_halo_schedule(best == 3 ? 0 : best);
+              set_sched(best);
             }
             for (int i = 0; i < warmup; ++i) fstep(i);
             for (auto& fe : fr) fe->synchronize();
@@ -637,10 +647,12 @@ int cmd_bench(const Args& a) {
       double ms = 0;
       for (double v : per_rank) ms = std::max(ms, v);
       const double mpx = (double)W * H / (ms * 1e-3) / 1e6;
-      static const char* kSched[] = {"serial", "overlap", "pipeline", "batched"};
-      char sched[200];
-      char bat[40] = "";  // batched: only where it was a candidate
+      static const char* kSched[] = {"serial", "overlap", "pipeline", "batched", "serial+deep"};
+      char sched[240];
+      char bat[80] = "";  // batched / serial+deep: only where they were candidates
       if (sched_ms[3] < 1e29) std::snprintf(bat, sizeof bat, ",\"batched\":%.5f", sched_ms[3]);
+      if (sched_ms[4] < 1e29)
+        std::snprintf(bat + std::strlen(bat), sizeof bat - std::strlen(bat), ",\"serial+deep\":%.5f", sched_ms[4]);
       if (chosen >= 0)
         std::snprintf(sched, sizeof sched,
                       ",\"halo_schedule\":{\"chosen\":\"%s\",\"ms\":{\"serial\":%.5f,\"overlap\":%.5f,"
@@ -680,7 +692,7 @@ void usage() {
                "        [--scope resident|device,dist,e2e] [--backend rccl|local|host] [--json out.json]\n"
                "        [--no-overlap] [--no-pipeline] [--graphs] [--band ROWS] [--halo-depth K] [--dist-chunks K]\n"
                "        [--frames F]  (resident: a stream of F independent frames, cache-cold tuning)\n"
-               "        [--halo-schedule auto|serial|overlap|pipeline|batched]  (frames at N > 1: auto times each)\n"
+               "        [--halo-schedule auto|serial|overlap|pipeline|batched|serial+deep]  (frames at N > 1: auto times each)\n"
                "  cmp   a.ppm b.ppm [--tol T]\n"
                "  gen   --synthetic WxHxC [--seed S] --output out.ppm|out.jpg\n"
                "  convert --input in.ppm|in.jpg --output out.ppm|out.jpg [--quality 95]\n"

@@ -119,6 +119,11 @@ def test_bench_frames_host(tmp_path):
     run("bench", "--synthetic", "128x64x3", "--chain", "gaussian5", "--ranks", "2", "--iters", "2", "--warmup", "1",
         "--frames", "2", "--backend", "host", "--halo-schedule", "overlap", "--json", js2)
     assert json.loads(js2.read_text().splitlines()[0])["value"] > 0
+    # deep frames pinned (k*S rows every k-th step; 32-row stripes: depth 8)
+    js3 = tmp_path / "f3.json"
+    run("bench", "--synthetic", "128x64x3", "--chain", "gaussian5", "--ranks", "2", "--iters", "9", "--warmup", "1",
+        "--frames", "2", "--backend", "host", "--halo-schedule", "serial+deep", "--json", js3)
+    assert json.loads(js3.read_text().splitlines()[0])["value"] > 0
 
 
 @pytest.mark.gpu
