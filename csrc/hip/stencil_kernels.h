@@ -270,9 +270,14 @@ __device__ __forceinline__ void apply_skip(const KArgs& a, int gy, int R, const 
   }
 }
 
-// After a band: edge waves rewrite the x-margins of their output rows (margin
-// pixel m <- pixel border_index(m) of the same row).  The wave's own stores are
-// complete after vmcnt(0); reads use sc0 (L2) so they see them.
+// After a band: waves rewrite the x-margins of their output rows (margin
+// pixel m <- pixel border_index(m) of the same row).  A margin byte is written
+// by the wave whose tile stored its source byte: that wave's own stores are
+// complete after vmcnt(0), and the reads use sc0 (L2) so they see them.  (The
+// row's edge tile cannot copy them all: when the last tile holds fewer than
+// px + 1 pixels, a right-margin source byte belongs to the tile before it --
+// another wave, unordered with this one; e.g. 333-pixel RGB rows, whose last
+// tile holds 7 bytes.)  Constant-border zeros are written by the edge tiles.
 // C: stencil channels (the wave tiling covers W * C bytes); CO: output bytes
 // per pixel (3 for a fused expand of a 1-channel stencil, else C).
 template <int C, int CO = C>
@@ -280,8 +285,10 @@ __device__ __forceinline__ void band_margins(const KArgs& a, const WaveTask& t, 
   const int px = a.out_px;
   if (px == 0) return;
   const int E = a.W * C;
-  const bool left = t.xt == 0;
-  const bool right = (t.xt + 1) * tile_bytes >= E;
+  const int tb0 = t.xt * tile_bytes, tb1 = min(tb0 + tile_bytes, E);  // stencil bytes this tile stored
+  const int reach = (px + 1) * C;  // stencil bytes a side's margins copy from
+  const bool left = tb0 < reach;
+  const bool right = tb1 > E - reach;
   if (!left && !right) return;
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this band's stores are done
   const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
@@ -293,9 +300,14 @@ __device__ __forceinline__ void band_margins(const KArgs& a, const WaveTask& t, 
     const int side = q >= nb;
     const int k = (side ? q - nb : q) / CO + 1;
     const int c = (side ? q - nb : q) % CO;
-    if ((side == 0 && !left) || (side == 1 && !right)) continue;
     const int m = side ? a.W - 1 + k : -k;
     const int src = border_index_dev(m, a.W, a.out_border);
+    if (src >= 0) {
+      const int sb = src * C + c * C / CO;  // the source's stencil byte
+      if (sb < tb0 || sb >= tb1) continue;
+    } else if ((side == 0 && t.xt != 0) || (side == 1 && tb1 != E)) {
+      continue;
+    }
     const uint32_t row = a.out_org + (uint32_t)((int64_t)y * a.out_pitch);
     uint8_t v = 0;
     if (src >= 0) v = __builtin_amdgcn_raw_buffer_load_b8(rout, row + src * CO + c, 0, 1);

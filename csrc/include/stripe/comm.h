@@ -58,6 +58,16 @@ class Comm {
   // each way, ordered on stream `s` (nullptr pointers: no neighbour on that
   // side).  Returns false when the backend has no collective form; the caller
   // then posts the grouped sends and receives.
+  // Hint for the next group: its send buffers are written again only after
+  // this rank's next group on the same stream (or after flush_sends()), as in
+  // the serial halo schedule, where every step exchanges and then overwrites
+  // the rows it sent one step earlier.  A backend may then complete those
+  // sends lazily: the wait for the peers' copies moves from this step's group
+  // end (on the critical path, one more cross-stream hop per step) to the next
+  // one, by when the copies are long done.
+  virtual void hint_lazy_sends() {}
+  // Enqueue (and host-wait for) every send completion a lazy group deferred.
+  virtual void flush_sends() {}
   virtual bool exchange_rows(int participants, const void* send_up, void* recv_up, const void* send_down,
                              void* recv_down, size_t bytes, hipStream_t s) {
     (void)participants, (void)send_up, (void)recv_up, (void)send_down, (void)recv_down, (void)bytes, (void)s;

@@ -318,7 +318,7 @@ class Engine {
   int tune_streams_ = 2;                     // set_tune_streams
   uint8_t* origin(const Buffer& b, int C) const;
   uint8_t* root_origin(const Buffer& b, int C) const;
-  void exchange_halo(uint8_t* org, int C, int R, hipStream_t s);
+  void exchange_halo(uint8_t* org, int C, int R, hipStream_t s, bool lazy_sends = false);
   void post_halo_ops(uint8_t* org, int C, int R, hipStream_t s);
   int posted_buf_ = -1;     // buffer whose halo post_halo() posted (-1: none)
   bool posted_ahead_ = false;    // that post is post_halo_ahead's, on another stream

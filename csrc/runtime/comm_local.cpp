@@ -339,6 +339,7 @@ class LocalComm final : public Comm {
   }
   ~LocalComm() override {
     for (hipEvent_t e : free_events_) (void)hipEventDestroy(e);
+    for (hipEvent_t e : lazy_events_) (void)hipEventDestroy(e);  // a lazy group never flushed (failed run)
   }
 
  private:
@@ -373,48 +374,107 @@ class LocalComm final : public Comm {
     try {
       int dev = 0;
       if (hub_->device() && !recvs_.empty()) HIP_CHECK(hipGetDevice(&dev));
-      hipStream_t waited_s = nullptr;
-      hipEvent_t waited_e = nullptr;
-      for (auto& r : recvs_) {
-        auto m = hub_->take(r.peer, rank_);
-        STRIPE_CHECK(m->bytes == r.bytes, "size mismatch: rank " << r.peer << " sent " << m->bytes
-                                                                 << " B, rank " << rank_ << " expects " << r.bytes);
-        if (hub_->device()) {
-          if (r.s != waited_s || m->ready != waited_e) HIP_CHECK(hipStreamWaitEvent(r.s, m->ready, 0));
-          waited_s = r.s;
-          waited_e = m->ready;
-          if (m->src_dev == dev)
-            HIP_CHECK(hipMemcpyAsync(r.buf, m->ptr, r.bytes, hipMemcpyDeviceToDevice, r.s));
-          else
-            HIP_CHECK(hipMemcpyPeerAsync(r.buf, dev, m->ptr, m->src_dev, r.bytes, r.s));
-          if (m->src_dev != dev) {  // an event is recorded on its own device's streams only
-            HIP_CHECK(hipEventCreateWithFlags(&m->done, hipEventDisableTiming));
-            m->own_done = true;
-          }
-          HIP_CHECK(hipEventRecord(m->done, r.s));  // the sender's pooled event, same device
-        } else {
-          std::memcpy(r.buf, m->ptr, r.bytes);
+      if (hub_->device()) {
+        // Same-device receives on one stream go out as ONE multi-copy launch
+        // after the waits on their senders' `ready` events (a halo exchange's
+        // two rows: one kernel instead of two hipMemcpyAsync calls, whose
+        // pointer lookups contend between the rank threads)
+        std::vector<std::shared_ptr<Msg>> got;
+        got.reserve(recvs_.size());
+        for (auto& r : recvs_) {
+          got.push_back(hub_->take(r.peer, rank_));
+          STRIPE_CHECK(got.back()->bytes == r.bytes, "size mismatch: rank " << r.peer << " sent " << got.back()->bytes
+                                                                            << " B, rank " << rank_ << " expects "
+                                                                            << r.bytes);
         }
-        hub_->mark_consumed(m);
+        size_t i = 0;
+        while (i < recvs_.size()) {
+          const hipStream_t s = recvs_[i].s;
+          size_t j = i;
+          while (j < recvs_.size() && recvs_[j].s == s) ++j;  // [i, j): one stream's run of receives
+          std::vector<hipEvent_t> waited;
+          std::vector<CopyDesc> cps;
+          for (size_t k = i; k < j; ++k) {
+            const auto& m = got[k];
+            if (std::find(waited.begin(), waited.end(), m->ready) == waited.end()) {
+              HIP_CHECK(hipStreamWaitEvent(s, m->ready, 0));
+              waited.push_back(m->ready);
+            }
+            if (m->src_dev == dev)
+              cps.push_back(CopyDesc{static_cast<const uint8_t*>(m->ptr), static_cast<uint8_t*>(recvs_[k].buf),
+                                     (int64_t)recvs_[k].bytes});
+            else
+              HIP_CHECK(hipMemcpyPeerAsync(recvs_[k].buf, dev, m->ptr, m->src_dev, recvs_[k].bytes, s));
+          }
+          if (!cps.empty()) launch_copy_multi(cps.data(), (int)cps.size(), s);
+          for (size_t k = i; k < j; ++k) {
+            const auto& m = got[k];
+            if (m->src_dev != dev) {  // an event is recorded on its own device's streams only
+              HIP_CHECK(hipEventCreateWithFlags(&m->done, hipEventDisableTiming));
+              m->own_done = true;
+            }
+            HIP_CHECK(hipEventRecord(m->done, s));  // the sender's pooled event, same device
+          }
+          i = j;
+        }
+        for (const auto& m : got) hub_->mark_consumed(m);
+      } else {
+        for (auto& r : recvs_) {
+          auto m = hub_->take(r.peer, rank_);
+          STRIPE_CHECK(m->bytes == r.bytes, "size mismatch: rank " << r.peer << " sent " << m->bytes
+                                                                   << " B, rank " << rank_ << " expects " << r.bytes);
+          std::memcpy(r.buf, m->ptr, r.bytes);
+          hub_->mark_consumed(m);
+        }
       }
       recvs_.clear();
-      for (auto& sd : sends_) {
-        hub_->wait_consumed(sd.m, sd.peer);
-        if (hub_->device()) {
-          HIP_CHECK(hipStreamWaitEvent(sd.s, sd.m->done, 0));
-          if (sd.m->own_done) HIP_CHECK(hipEventDestroy(sd.m->done));
-        }
+      settle_lazy();  // the previous lazy group's sends, before this group's buffers are written
+      if (lazy_next_) {
+        lazy_next_ = false;
+        lazy_sends_.swap(sends_);
+        lazy_events_.swap(group_events_);
+        return;
       }
-      sends_.clear();
-      // every wait on this group's events is enqueued: they may be re-recorded
-      free_events_.insert(free_events_.end(), group_events_.begin(), group_events_.end());
-      group_events_.clear();
+      complete_sends(sends_, group_events_);
     } catch (const std::exception& e) {
       hub_->abort(std::string("rank ") + std::to_string(rank_) + ": " + e.what());
       drop_group();
       throw;
     }
   }
+  // A group's sends are complete once each peer has taken its message (host)
+  // and the stream has a wait on the peer's copy (device); then every wait on
+  // the group's events is enqueued and they may be re-recorded.
+  void complete_sends(std::vector<PendingSend>& sends, std::vector<hipEvent_t>& events) {
+    for (auto& sd : sends) {
+      hub_->wait_consumed(sd.m, sd.peer);
+      if (hub_->device()) {
+        HIP_CHECK(hipStreamWaitEvent(sd.s, sd.m->done, 0));
+        if (sd.m->own_done) HIP_CHECK(hipEventDestroy(sd.m->done));
+      }
+    }
+    sends.clear();
+    free_events_.insert(free_events_.end(), events.begin(), events.end());
+    events.clear();
+  }
+  void settle_lazy() {
+    if (!lazy_sends_.empty() || !lazy_events_.empty()) complete_sends(lazy_sends_, lazy_events_);
+  }
+
+ public:
+  void hint_lazy_sends() override { lazy_next_ = hub_->device(); }
+  void flush_sends() override {
+    lazy_next_ = false;
+    try {
+      settle_lazy();
+    } catch (const std::exception& e) {
+      hub_->abort(std::string("rank ") + std::to_string(rank_) + ": " + e.what());
+      drop_group();
+      throw;
+    }
+  }
+
+ private:
   // A failed group: its events are destroyed rather than pooled (a peer's
   // stream may still hold a wait on them, and the aborted hub runs no later
   // group), a receiver-created `done` of a consumed message with it (the
@@ -422,18 +482,23 @@ class LocalComm final : public Comm {
   // lock), and the pending lists are cleared so no later call sees them.
   void drop_group() {
     if (hub_->device()) {
-      for (auto& sd : sends_)
-        if (hub_->is_consumed(sd.m) && sd.m->own_done && sd.m->done) {
-          (void)hipEventDestroy(sd.m->done);
-          sd.m->done = nullptr;
-        }
+      for (auto* list : {&sends_, &lazy_sends_})
+        for (auto& sd : *list)
+          if (hub_->is_consumed(sd.m) && sd.m->own_done && sd.m->done) {
+            (void)hipEventDestroy(sd.m->done);
+            sd.m->done = nullptr;
+          }
       for (hipEvent_t ev : group_events_) (void)hipEventDestroy(ev);
+      for (hipEvent_t ev : lazy_events_) (void)hipEventDestroy(ev);
       (void)hipGetLastError();
     }
     group_events_.clear();
+    lazy_events_.clear();
     sends_.clear();
+    lazy_sends_.clear();
     recvs_.clear();
     in_group_ = false;
+    lazy_next_ = false;
   }
 
   std::shared_ptr<LocalHub> hub_;
@@ -443,6 +508,9 @@ class LocalComm final : public Comm {
   std::vector<PendingRecv> recvs_;
   std::vector<hipEvent_t> free_events_;   // pooled, unreferenced
   std::vector<hipEvent_t> group_events_;  // taken by the open group's sends
+  bool lazy_next_ = false;                // hint_lazy_sends: the next group completes its sends lazily
+  std::vector<PendingSend> lazy_sends_;   // a lazy group's sends, completed by the next group / flush_sends
+  std::vector<hipEvent_t> lazy_events_;   // and their events
 };
 
 class CallbackComm final : public Comm {

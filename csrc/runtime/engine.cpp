@@ -311,6 +311,15 @@ double& phase_field(PhaseTimes& t, Stage s) {
   }
 }
 thread_local double host_stage_t0[(int)Stage::kCount];
+// STUDY: STRIPE_LOCAL_LAZY=0 completes every serial exchange's sends at its own
+// group end (the eager form, A/B)
+bool lazy_sends_ok() {
+  static const bool on = [] {
+    const char* e = std::getenv("STRIPE_LOCAL_LAZY");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
 }  // namespace
 
 // Device backend: events on the stage's stream, read after synchronize();
@@ -500,7 +509,7 @@ void Engine::scatter() {
   cur_c_ = C;
 }
 
-void Engine::exchange_halo(uint8_t* org, int C, int R, hipStream_t s) {
+void Engine::exchange_halo(uint8_t* org, int C, int R, hipStream_t s, bool lazy_sends) {
   const Stripe& st = stripe();
   if (st.rows == 0 || !neighbours()) return;
   const int64_t P = pitch(C);
@@ -534,6 +543,7 @@ void Engine::exchange_halo(uint8_t* org, int C, int R, hipStream_t s) {
     if (time_halo_) stage_end(Stage::Halo, s);
     return;
   }
+  if (lazy_sends) comm_->hint_lazy_sends();
   comm_->group_start();
   post_halo_ops(org, C, R, s);
   comm_->group_end();
@@ -678,6 +688,11 @@ void Engine::run_pass(const Pass& p, const uint8_t* in, uint8_t* out) {
   const RowGeom g = geom();
   const int R = p.R;
   const bool xchg = !halo_done_ && ((cfg_.halo && R > 0 && neighbours()) || (device() && schedule_emu() == 1 && R > 0));
+  // sends of a serial exchange complete lazily (Comm::hint_lazy_sends): any
+  // other form of this pass may write rows the previous pass sent before its
+  // own group, so those sends complete first
+  const bool serial_xchg = device() && xchg && !(cfg_.overlap && rows > 2 * R) && schedule_emu() != 3;
+  if (!serial_xchg && comm_) comm_->flush_sends();
   if (device() && schedule_emu() == 3 && R > 0 && rows > 2 * R) {  // two launches, one stream, no events
     const size_t pi3 = (size_t)(&p - plan_.passes.data());
     PassLaunch L3 = make_launch(p, in, out, (int)pi3);
@@ -735,7 +750,9 @@ void Engine::run_pass(const Pass& p, const uint8_t* in, uint8_t* out) {
     HIP_CHECK(hipStreamWaitEvent(s_compute_, ev_[5], 0));
     if (!edges_on_comm) launch_pass(p, pc, E, s_compute_);
   } else {
-    exchange_halo(const_cast<uint8_t*>(in), p.cin, R, s_compute_);
+    // the rows sent here are next written by the pass after this one, whose
+    // own exchange comes first on this stream (or run()'s flush_sends)
+    exchange_halo(const_cast<uint8_t*>(in), p.cin, R, s_compute_, lazy_sends_ok());
     L.nrange = 1;
     L.ry[0] = 0;
     L.ry[1] = rows;
@@ -817,6 +834,7 @@ void Engine::run(int iterations) {
   } else {
     iterate(iterations);
   }
+  if (comm_) comm_->flush_sends();  // every lazily completed send of this run
   stage_end(Stage::Compute, s_compute_);
   time_halo_ = true;
   out_buf_ = cur_;

@@ -2,12 +2,31 @@
 streams with hardware queues of their own (C.dedicated_stream); the schedule
 probe measures both with two streams and keeps the fastest
 (profiles/r5/streams/README.md)."""
-import time
-
 import pytest
 
 import mpi_cuda_imagemanipulation_amd as m
 from mpi_cuda_imagemanipulation_amd import parallel
+
+
+class _Clock:
+    """A fake clock the stand-in steps advance by their cost: the probe's
+    timings are then exact, whatever the load on the host."""
+
+    def __init__(self):
+        self.t = 0.0
+
+    def perf_counter(self):
+        return self.t
+
+    def sleep(self, dt):
+        self.t += dt
+
+
+@pytest.fixture(autouse=True)
+def _fake_clock(monkeypatch):
+    clock = _Clock()
+    monkeypatch.setattr(parallel, "time", clock)
+    return clock
 
 
 def _stand_in(cost):
@@ -29,7 +48,7 @@ def _stand_in(cost):
         applied.append((tuple(fs.streams), n))
 
     fs.set_streams = set_streams
-    fs.step = lambda i=None: time.sleep(cost(fs.schedule, fs.nstreams, fs.queues))
+    fs.step = lambda i=None: parallel.time.sleep(cost(fs.schedule, fs.nstreams, fs.queues))
     fs.synchronize = lambda: None
     return fs, frames
 
@@ -37,8 +56,7 @@ def _stand_in(cost):
 def test_probe_picks_stream_set():
     # two streams on the pool set are fastest here: the probe must land there
     def cost(sched, n, q):
-        # ms-scale gaps, so sleep jitter on a loaded host cannot reorder them
-        base = {"pipeline": 0.04, "overlap": 0.03, "serial": 0.02, "batched": 0.035, "ahead": 0.037}[sched]
+        base = {"pipeline": 0.004, "overlap": 0.003, "serial": 0.002, "batched": 0.0035, "ahead": 0.0037}[sched]
         return base / 2 if (n == 2 and q == "plain") else base
 
     fs, frames = _stand_in(cost)

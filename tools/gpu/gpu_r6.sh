@@ -143,6 +143,24 @@ local2)
     done
   done
   ;;
+local3)
+  # the `local` hub: first run, receives as one multi-copy launch per stream
+  # vs one hipMemcpyAsync each (STRIPE_LOCAL_MEMCPY=1, since removed); second
+  # run, serial exchanges completing their sends lazily (at the next exchange)
+  # vs at their own group end (STRIPE_LOCAL_LAZY=0), alternating: the
+  # local-rank tests, then depth 1 (serial, the shared-GPU default) and the
+  # automatic depth
+  timeout -k 10 900 python -u -m pytest tests/test_r6_margins.py tests/test_r6_local.py tests/test_gpu_engine.py tests/test_dist_pipelined.py tests/test_deep_halo.py tests/test_advice_r2.py tests/test_weighted_split.py tests/test_n8.py tests/test_multi_gpu.py tests/test_resilience.py -m gpu -q -x --timeout 200 --timeout-method thread > $O/tests.txt 2>&1 || exit 2
+  CFG3="bin/stripe bench --synthetic 8192x8192x1 --chain sobel --ranks 4 --iters 64 --warmup 8 --scope resident --backend local"
+  for r in 1 2 3; do
+    for lz in 1 0; do
+      echo "lazy $lz depth 1" >> $O/cfg3_depth1.txt
+      STRIPE_LOCAL_LAZY=$lz timeout -k 10 120 $CFG3 --halo-depth 1 2>&1 | grep -v amdgpu.ids >> $O/cfg3_depth1.txt || exit 3
+      echo "lazy $lz depth auto" >> $O/cfg3_auto.txt
+      STRIPE_LOCAL_LAZY=$lz timeout -k 10 120 $CFG3 2>&1 | grep -v amdgpu.ids >> $O/cfg3_auto.txt || exit 3
+    done
+  done
+  ;;
 blurdiag)
   # which memory stream sets blur:31's time: loads / stores masked out of range
   # (STRIPE_BLUR_VARIANT 7 / 8 / 9, wrong output, timing only), alternating
