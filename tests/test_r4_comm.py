@@ -363,15 +363,26 @@ def test_frame_stream_pick_schedule_single_candidate(C, monkeypatch):
     assert fs.schedule == "serial"
 
 
-def test_frame_stream_pick_schedule_takes_fastest_max_over_ranks():
+def test_frame_stream_pick_schedule_takes_fastest_max_over_ranks(monkeypatch):
     # device engines: all three schedules are timed `rounds` times (the same
     # list on every rank, whatever each rank's stripe runs), the per-rank
     # time goes through reduce_max (every rank must agree), the fastest wins
     # and stays set on every frame
-    import time as _t
     from types import SimpleNamespace
 
     from mpi_cuda_imagemanipulation_amd import parallel
+
+    class _Clock:  # the stand-in steps advance a fake clock: exact timings on a loaded host
+        t = 0.0
+
+        def perf_counter(self):
+            return self.t
+
+        def sleep(self, dt):
+            self.t += dt
+
+    _t = _Clock()
+    monkeypatch.setattr(parallel, "time", _t)
 
     cost = {"pipeline": 0.004, "overlap": 0.001, "serial": 0.002}
     frames = [SimpleNamespace(engine=SimpleNamespace(halo_schedule="pipeline")) for _ in range(2)]
