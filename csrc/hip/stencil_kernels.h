@@ -270,25 +270,33 @@ __device__ __forceinline__ void apply_skip(const KArgs& a, int gy, int R, const 
   }
 }
 
-// After a band: waves rewrite the x-margins of their output rows (margin
-// pixel m <- pixel border_index(m) of the same row).  A margin byte is written
-// by the wave whose tile stored its source byte: that wave's own stores are
-// complete after vmcnt(0), and the reads use sc0 (L2) so they see them.  (The
-// row's edge tile cannot copy them all: when the last tile holds fewer than
-// px + 1 pixels, a right-margin source byte belongs to the tile before it --
-// another wave, unordered with this one; e.g. 333-pixel RGB rows, whose last
-// tile holds 7 bytes.)  Constant-border zeros are written by the edge tiles.
+// First stencil byte of wave tile xt (tb bytes a tile) of a row.  The row's
+// last tile starts early enough to hold every byte its right margins copy:
+// with a plain grid, a last tile shorter than the margin reach ((px + 1) C
+// bytes) would copy pixels the tile before it stores -- another wave,
+// unordered with it (e.g. 333-pixel RGB rows: 999 bytes, a 7-byte last tile).
+// It then overlaps its neighbour, and both store the same values there.
+template <int C>
+__device__ __forceinline__ int tile_base(const KArgs& a, int xt, int tb) {
+  const int b = xt * tb;
+  if (xt == 0 || xt != a.ntx - 1 || a.out_px == 0) return b;
+  return min(b, (a.E - (a.out_px + 1) * C) & ~15);
+}
+
+// After a band: the row's edge waves rewrite the x-margins of their output
+// rows (margin pixel m <- pixel border_index(m) of the same row).  A margin
+// byte's writer must follow the store of its source byte and the store of the
+// row's last chunk, whose 16 bytes reach past the row into the right margin:
+// the edge tile makes both (tile_base), so vmcnt(0) orders them; the reads
+// use sc0 (L2) so they see them.
 // C: stencil channels (the wave tiling covers W * C bytes); CO: output bytes
 // per pixel (3 for a fused expand of a 1-channel stencil, else C).
 template <int C, int CO = C>
-__device__ __forceinline__ void band_margins(const KArgs& a, const WaveTask& t, int tile_bytes = kOutChunks * 16) {
+__device__ __forceinline__ void band_margins(const KArgs& a, const WaveTask& t) {
   const int px = a.out_px;
   if (px == 0) return;
-  const int E = a.W * C;
-  const int tb0 = t.xt * tile_bytes, tb1 = min(tb0 + tile_bytes, E);  // stencil bytes this tile stored
-  const int reach = (px + 1) * C;  // stencil bytes a side's margins copy from
-  const bool left = tb0 < reach;
-  const bool right = tb1 > E - reach;
+  const bool left = t.xt == 0;
+  const bool right = t.xt == a.ntx - 1;
   if (!left && !right) return;
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this band's stores are done
   const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
@@ -300,14 +308,9 @@ __device__ __forceinline__ void band_margins(const KArgs& a, const WaveTask& t, 
     const int side = q >= nb;
     const int k = (side ? q - nb : q) / CO + 1;
     const int c = (side ? q - nb : q) % CO;
+    if ((side == 0 && !left) || (side == 1 && !right)) continue;
     const int m = side ? a.W - 1 + k : -k;
     const int src = border_index_dev(m, a.W, a.out_border);
-    if (src >= 0) {
-      const int sb = src * C + c * C / CO;  // the source's stencil byte
-      if (sb < tb0 || sb >= tb1) continue;
-    } else if ((side == 0 && t.xt != 0) || (side == 1 && tb1 != E)) {
-      continue;
-    }
     const uint32_t row = a.out_org + (uint32_t)((int64_t)y * a.out_pitch);
     uint8_t v = 0;
     if (src >= 0) v = __builtin_amdgcn_raw_buffer_load_b8(rout, row + src * CO + c, 0, 1);
@@ -532,6 +535,51 @@ __device__ __forceinline__ void dpp_window(const uint32_t (&v)[8], uint32_t (&w)
   }
 }
 
+// Horizontal pass of an H16 separable filter (SepTraits::H16): the lane's 16
+// output bytes from its window of vertical sums (dpp_window).
+template <int C, class F, int WLO, int WDW>
+__device__ __forceinline__ void sep_h16_out(const uint32_t (&w)[WDW], uint32_t (&o)[4]) {
+  using T = SepTraits<F>;
+  constexpr int R = F::R, K = F::K;
+  uint32_t h[8];
+#pragma unroll
+  for (int pp = 0; pp < 8; ++pp) {
+    u16x2 sacc;
+    if constexpr (T::SYM && F::g(0) == 1) {
+      // mirrored taps share a weight: (x[-i] + x[+i]) * g, outermost pair
+      // (weight 1) first, centre last: 2R ops per output pair.  Plain u32
+      // arithmetic on the packed pair is exact (H16: every partial sum and
+      // product is < 2^16, so nothing crosses into the high field), which
+      // turns power-of-two weights into one v_lshl_add_u32.
+      auto madd = [](uint32_t s, uint32_t acc, int g) __attribute__((always_inline)) {
+        if ((g & (g - 1)) == 0) {
+          int k = 0;
+          while ((1 << k) < g) ++k;
+          return (s << k) + acc;
+        }
+        return as_u32(as_u16x2(s) * (unsigned short)g + as_u16x2(acc));
+      };
+      uint32_t acc = sym_pair(w, WLO + 2 * pp, R * C, PkAddU16{});
+#pragma unroll
+      for (int i = 1; i < R; ++i) acc = madd(sym_pair(w, WLO + 2 * pp, (R - i) * C, PkAddU16{}), acc, F::g(i));
+      acc = madd(pair_at(w, WLO + 2 * pp), acc, F::g(R));
+      sacc = as_u16x2(acc);
+      if constexpr (!T::FOLD) sacc += (u16x2)(unsigned short)(F::DIV / 2);
+    } else {
+      sacc = (u16x2)(unsigned short)(F::DIV / 2);
+#pragma unroll
+      for (int i = 0; i < K; ++i)
+        sacc += as_u16x2(pair_at(w, WLO + 2 * pp + (i - R) * C)) * (unsigned short)F::g(i);
+    }
+    if constexpr (T::log2div() != 8) sacc = sacc >> (unsigned short)T::log2div();
+    h[pp] = as_u32(sacc);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    o[q] = T::log2div() == 8 ? __builtin_amdgcn_perm(h[2 * q + 1], h[2 * q], 0x07050301u)
+                             : __builtin_amdgcn_perm(h[2 * q + 1], h[2 * q], 0x06040200u);
+}
+
 // One wave task (a band of rows of one tile column) of a separable filter.
 template <int C, class F, int PRO, bool SKIP, int SAUX, bool EXP>
 __device__ __forceinline__ void sep_task(const KArgs& a, const WaveTask& t, const uint8_t* luts, uint4* xb) {
@@ -551,7 +599,7 @@ __device__ __forceinline__ void sep_task(const KArgs& a, const WaveTask& t, cons
   const int pbase = kRev && t.dir < 0 ? ys + ye - 1 : 0;
   const int psign = kRev && t.dir < 0 ? -1 : 1;
   auto phys = [&](int y) __attribute__((always_inline)) { return pbase + psign * y; };
-  const int cb = t.xt * (kOutChunks * 16) - 16 + lane * 16;
+  const int cb = tile_base<C>(a, t.xt, kOutChunks * 16) - 16 + lane * 16;
   const uint32_t lane_in = cb < a.E + 16 ? (uint32_t)(cb * CIN) : kOOB;
   const OutLanes lout = out_lanes<EXP>(a, lane, cb - 16 * lane);
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);
@@ -661,43 +709,7 @@ __device__ __forceinline__ void sep_task(const KArgs& a, const WaveTask& t, cons
 #pragma unroll
       for (int q = 0; q < 4; ++q) o[q] = __builtin_amdgcn_perm(h[2 * q + 1], h[2 * q], 0x06040200u);
     } else if constexpr (T::H16) {
-      uint32_t h[8];
-#pragma unroll
-      for (int pp = 0; pp < 8; ++pp) {
-        u16x2 sacc;
-        if constexpr (T::SYM && F::g(0) == 1) {
-          // mirrored taps share a weight: (x[-i] + x[+i]) * g, outermost pair
-          // (weight 1) first, centre last: 2R ops per output pair.  Plain u32
-          // arithmetic on the packed pair is exact (H16: every partial sum and
-          // product is < 2^16, so nothing crosses into the high field), which
-          // turns power-of-two weights into one v_lshl_add_u32.
-          auto madd = [](uint32_t s, uint32_t acc, int g) __attribute__((always_inline)) {
-            if ((g & (g - 1)) == 0) {
-              int k = 0;
-              while ((1 << k) < g) ++k;
-              return (s << k) + acc;
-            }
-            return as_u32(as_u16x2(s) * (unsigned short)g + as_u16x2(acc));
-          };
-          uint32_t acc = sym_pair(w, WLO + 2 * pp, R * C, PkAddU16{});
-#pragma unroll
-          for (int i = 1; i < R; ++i) acc = madd(sym_pair(w, WLO + 2 * pp, (R - i) * C, PkAddU16{}), acc, F::g(i));
-          acc = madd(pair_at(w, WLO + 2 * pp), acc, F::g(R));
-          sacc = as_u16x2(acc);
-          if constexpr (!T::FOLD) sacc += (u16x2)(unsigned short)(F::DIV / 2);
-        } else {
-          sacc = (u16x2)(unsigned short)(F::DIV / 2);
-#pragma unroll
-          for (int i = 0; i < K; ++i)
-            sacc += as_u16x2(pair_at(w, WLO + 2 * pp + (i - R) * C)) * (unsigned short)F::g(i);
-        }
-        if constexpr (T::log2div() != 8) sacc = sacc >> (unsigned short)T::log2div();
-        h[pp] = as_u32(sacc);
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        o[q] = T::log2div() == 8 ? __builtin_amdgcn_perm(h[2 * q + 1], h[2 * q], 0x07050301u)
-                                 : __builtin_amdgcn_perm(h[2 * q + 1], h[2 * q], 0x06040200u);
+      sep_h16_out<C, F, WLO, WDW>(w, o);
     } else {
       uint32_t ob[16];
 #pragma unroll
@@ -844,7 +856,7 @@ __global__ __launch_bounds__(kNT, 4) void k_sobel_rp(KArgs a) {
   const int lane = t.lane;
   const int ys = t.ys, ye = t.ye;
   constexpr int kTile = WIDE ? kW * 16 : kOutChunks * 16;  // output bytes per wave row
-  const int cb0 = t.xt * kTile - (WIDE ? 0 : 16);
+  const int cb0 = tile_base<1>(a, t.xt, kTile) - (WIDE ? 0 : 16);
   const int cb = cb0 + lane * 16;
   const uint32_t lane_in = cb < a.E + 16 ? (uint32_t)cb : kOOB;
   OutLanes lout;
@@ -949,7 +961,7 @@ __global__ __launch_bounds__(kNT, 4) void k_sobel_rp(KArgs a) {
       step(y + 2, nx[1], ne[1]);
     }
   }
-  band_margins<1, 1>(a, t, kTile);
+  band_margins<1, 1>(a, t);
 }
 
 // ------------------------------------------------------------------------------
@@ -989,7 +1001,7 @@ __global__ __launch_bounds__(kNT, (F::K >= 5 ? 3 : 4)) void k_direct(KArgs a) {
   if (!t.valid) return;
   const int lane = t.lane;
   const int ys = t.ys, ye = t.ye;
-  const int cb = t.xt * (kOutChunks * 16) - 16 + lane * 16;
+  const int cb = tile_base<C>(a, t.xt, kOutChunks * 16) - 16 + lane * 16;
   const uint32_t lane_in = cb < a.E + 16 ? (uint32_t)(cb * CIN) : kOOB;
   const OutLanes lout = out_lanes<EXP>(a, lane, cb - 16 * lane);
   const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);

@@ -1,14 +1,16 @@
-"""Output x-margins written by the wave that stored their source bytes.
+"""Output x-margins when the row's last wave tile is short.
 
-The stencil kernels (k_sep, k_direct, k_sobel_rp) keep each output row's
-x-margins (the border extension the next pass reads) up to date after every
-band.  Until round 6 only the row's edge tiles rewrote them, copying from
-pixels that, when the last tile holds fewer than px + 1 pixels, the tile
-before it had stored: another wave, unordered with the copying one.  A
-333-pixel RGB row (999 bytes: tiles of 992 + 7) then read stale right-margin
-sources now and then -- 1-LSB errors in the last columns, first seen in
-`test_r6_local.py` under the pipelined schedule.  These shapes put the
-straddle in every row and iterate, so a stale margin shows as a mismatch
+The stencil kernels (k_sep, k_sep_st, k_direct, k_sobel_rp) keep each output
+row's x-margins (the border extension the next pass reads) up to date after
+every band: the row's edge tiles rewrite them.  Until round 6 a last tile
+holding fewer than px + 1 pixels copied pixels the tile before it had stored:
+another wave, unordered with the copying one.  A 333-pixel RGB row (999
+bytes: tiles of 992 + 7) then read stale right-margin sources now and then --
+1-LSB errors in the last columns, first seen in `test_r6_local.py` under the
+pipelined schedule.  The last tile now starts early enough to hold them
+(`tile_base`); it cannot hand the copy to the tile before it, because its own
+last 16-byte store reaches past the row into the margin.  These shapes put the
+short tile in every row and iterate, so a stale margin shows as a mismatch
 against the golden path.
 
 Reference: the interior-only bounds of embossKernel (kernel.cu:83)

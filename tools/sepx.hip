@@ -6,7 +6,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Icsrc/include -Icsrc/hip -Itools \
 //         -o bin/sepx tools/sepx.hip
 //   bin/sepx [rows] [frames] [stamp_csv_prefix] [sweep: tail | policy | sobel | wg | quad | sobelquad | runs | fetch |
-//             pattern | pitch (SEPX_PAD=bytes added to the row pitch)]
+//             pattern | pitch (SEPX_PAD=bytes added to the row pitch) | lds]
 //
 // Every measurement rotates over `frames` independent in/out buffer pairs
 // (default: enough that frames x (in + out) > 3 x 256 MiB), so each launch
@@ -124,6 +124,60 @@ __global__ __launch_bounds__(256) void k_band_copy2(KArgs a) {
   }
 }
 
+// Pattern probe (round 6): the NS waves of a workgroup stacked on one 1 KiB
+// tile column share ONE staged copy of their rows.  The workgroup loads the
+// NS RPW + 2R input rows of its NS RPW output rows once -- a wave's halo rows
+// come from LDS instead of a second read -- then each wave reads its RPW + 2R
+// rows from LDS and stores its RPW output rows (pattern only: no arithmetic).
+// Short per-wave row chains with the halo re-reads of a tall band.
+template <int R, int NS, int RPW>
+__global__ __launch_bounds__(64 * NS) void k_band_lds(KArgs a) {
+  constexpr int ROWS = NS * RPW, IN = ROWS + 2 * R, LPW = (IN + NS - 1) / NS;
+  __shared__ u32x4 tile[IN][kW];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int b = (int)blockIdx.x;
+  const int xt = b % a.ntx, y0 = (b / a.ntx) * ROWS;
+  if (y0 >= a.rows) return;
+  const int cb = xt * 1024 + lane * 16;
+  const uint32_t lane_in = cb < a.E ? (uint32_t)cb : kOOB;
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);
+  const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
+  u32x4 v[LPW];
+#pragma unroll
+  for (int i = 0; i < LPW; ++i) {
+    const int r = wave + NS * i;
+    const int y = min(y0 - R + r, a.rows - 1 + R);
+    v[i] = __builtin_amdgcn_raw_buffer_load_b128(rin, in_row_off(a, y) + (r < IN ? lane_in : kOOB), 0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < LPW; ++i)
+    if (wave + NS * i < IN) tile[wave + NS * i][lane] = v[i];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < RPW; ++j) {
+    const int ro = wave * RPW + j;  // output row within the group
+    u32x4 acc = tile[ro][lane];  // every row of the window read, as the stencil does
+#pragma unroll
+    for (int k = 1; k <= 2 * R; ++k) acc ^= tile[ro + k][lane];
+    const int y = y0 + ro;
+    if (y < a.rows && cb < a.E)
+      __builtin_amdgcn_raw_buffer_store_b128(acc, rout, a.out_org + (uint32_t)((int64_t)y * a.out_pitch) + (uint32_t)cb,
+                                             0, kNtAux);
+  }
+}
+
+struct LdsCfg {
+  int ns, rpw, cap;
+};
+static void (*lds_fn(const LdsCfg& c))(KArgs) {
+  if (c.ns == 4 && c.rpw == 2) return k_band_lds<2, 4, 2>;
+  if (c.ns == 4 && c.rpw == 4) return k_band_lds<2, 4, 4>;
+  if (c.ns == 4 && c.rpw == 8) return k_band_lds<2, 4, 8>;
+  if (c.ns == 8 && c.rpw == 2) return k_band_lds<2, 8, 2>;
+  if (c.ns == 8 && c.rpw == 4) return k_band_lds<2, 8, 4>;
+  return k_band_lds<2, 16, 2>;
+}
+
 struct PatCfg {
   int lb, pf, band, cap, r = 2;
 };
@@ -231,6 +285,28 @@ static void launch_sep(const SepCfg& c, const Frame& f, hipStream_t s, uint32_t*
   }
   if (grid_out) *grid_out = (int)grid.x;
   fn<<<grid, c.nw * kW, dyn, s>>>(a);
+}
+
+static void launch_lds(const LdsCfg& c, const Frame& f, hipStream_t s) {
+  KArgs a{};
+  a.in = f.in + g_org;
+  a.out = f.out + g_org;
+  a.in_pitch = a.out_pitch = g_pitch;
+  a.W = g_W;
+  a.E = g_W * g_C;
+  a.rows = g_rows;
+  a.Hg = g_rows;
+  a.in_base = f.in;
+  a.out_base = f.out;
+  a.in_bytes = a.out_bytes = (uint32_t)g_bytes;
+  a.in_org = a.out_org = (uint32_t)g_org;
+  a.in_zero = kMarginBytes;
+  a.ry0 = 0;
+  a.ry1 = g_rows;
+  a.ntx = (int)div_up(a.E, 1024);
+  void (*fn)(KArgs) = lds_fn(c);
+  const int64_t grid = (int64_t)a.ntx * div_up(g_rows, c.ns * c.rpw);
+  fn<<<dim3((unsigned)grid), 64 * c.ns, nt_lds_reserve((const void*)fn, c.cap), s>>>(a);
 }
 
 static void launch_pat(const PatCfg& c, const Frame& f, hipStream_t s) {
@@ -453,6 +529,30 @@ int main(int argc, char** argv) {
       }
     const PatCfg c8{16, 8, 64, 2, 0};
     report("pattern halo=0 band=64 (8 in flight)", [&](const Frame& f, hipStream_t s) { launch_pat(c8, f, s); });
+    return 0;
+  }
+  if (sweep == "lds") {  // stacked waves sharing staged rows through LDS vs the band walk (pattern only)
+    for (int aux : {2, 16}) report("copy aux=" + std::to_string(aux), [&](const Frame& f, hipStream_t s) {
+      launch_copy(aux, f, s);
+    });
+    for (int band : {8, 12, 16}) {
+      const PatCfg c{16, 4, band, 2, 2};
+      char name[96];
+      std::snprintf(name, sizeof name, "pattern halo=2 band=%2d (band walk, cap 2)", band);
+      report(name, [&](const Frame& f, hipStream_t s) { launch_pat(c, f, s); });
+    }
+    const PatCfg c0{16, 4, 8, 2, 0};
+    report("pattern halo=0 band= 8 (band walk, cap 2)", [&](const Frame& f, hipStream_t s) { launch_pat(c0, f, s); });
+    for (auto sr : std::vector<std::pair<int, int>>{{4, 2}, {4, 4}, {4, 8}, {8, 2}, {8, 4}, {16, 2}})
+      for (int cap : {0, 2, 4, 8}) {
+        const int waves = cap * sr.first;
+        if (cap > 0 && (waves < 8 || waves > 32)) continue;
+        const LdsCfg c{sr.first, sr.second, cap};
+        char name[96];
+        std::snprintf(name, sizeof name, "lds halo=2 %2d waves x %d rows (%2d-row groups) cap=%d", sr.first, sr.second,
+                      sr.first * sr.second, cap);
+        report(name, [&](const Frame& f, hipStream_t s) { launch_lds(c, f, s); });
+      }
     return 0;
   }
   if (sweep == "pattern2") {  // access pattern only: bytes per lane x rows in flight x band
