@@ -143,6 +143,22 @@ local2)
     done
   done
   ;;
+pairs)
+  # paired band walks (task order 2, k_sep_pairs, removed after this study
+  # with tests/test_r6_pairs.py): GPU tests, then the
+  # driver's headline command, the N=8 share on one stream and under the
+  # probe, with the order tuned (auto) or pinned to 0 (one-task) / 2
+  # (paired), alternating
+  timeout -k 10 900 python -u -m pytest tests/test_r6_pairs.py tests/test_r5_order.py tests/test_r6_margins.py tests/test_gpu_kernels.py -m gpu -q -x --timeout 200 --timeout-method thread > $O/tests.txt 2>&1 || exit 2
+  for r in 1 2; do
+    for o in auto 0 2; do
+      E=""; [ $o != auto ] && E="STRIPE_SEP_ORDER=$o"
+      env $E timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --dist-steps 0 --ref-steps 0 --e2e-steps 0 >> $O/head_$o.json 2>> $O/head_$o.err || exit 3
+      env $E timeout -k 10 300 python bench.py $SHARE --streams 1 >> $O/share1_$o.json 2>> $O/share1_$o.err || exit 3
+      env $E timeout -k 10 300 python bench.py $SHARE >> $O/share_$o.json 2>> $O/share_$o.err || exit 3
+    done
+  done
+  ;;
 stacked)
   # stacked separable groups (task order 2, k_sep_st, removed after this
   # study with tests/test_r6_stacked.py): GPU tests, then the driver's

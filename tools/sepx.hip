@@ -166,6 +166,71 @@ __global__ __launch_bounds__(64 * NS) void k_band_lds(KArgs a) {
   }
 }
 
+// Pattern probe (round 6): the 4 waves of a workgroup walk 4 stacked bands of
+// BAND rows on one 1 KiB tile column, even waves bottom-up, odd ones top-down,
+// so the two waves beside an inner boundary need its 2R halo rows at the same
+// moment (both first, or both last).  Each loads only its own side and they
+// swap through LDS (a barrier at the start and one at the end): per
+// workgroup only the outer 2R halo rows are read twice -- (4 BAND + 2R) / 4
+// BAND instead of (BAND + 2R) / BAND -- while every wave's walk stays BAND rows
+// long (pattern only: 4 rows in flight, no arithmetic).
+template <int R, int BAND>
+__global__ __launch_bounds__(256) void k_band_pairs(KArgs a) {
+  __shared__ u32x4 edge[4][2 * R][kW];  // wave w's first / last R own rows
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int b = (int)blockIdx.x;
+  const int xt = b % a.ntx, y0 = (b / a.ntx) * 4 * BAND + wave * BAND;
+  const int cb = xt * 1024 + lane * 16;
+  const uint32_t lane_in = cb < a.E ? (uint32_t)cb : kOOB;
+  const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in_base, a.in_bytes);
+  const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out_base, a.out_bytes);
+  const bool up = (wave & 1) == 0;  // bottom-up walk
+  auto row = [&](int i) { return up ? y0 + BAND - 1 - i : y0 + i; };  // i-th own row of the walk
+  auto ld = [&](int y) {
+    return __builtin_amdgcn_raw_buffer_load_b128(rin, in_row_off(a, min(y, a.rows - 1 + R)) + lane_in, 0, 0);
+  };
+  auto st = [&](int y, const u32x4& v) {
+    if (y < a.rows && cb < a.E)
+      __builtin_amdgcn_raw_buffer_store_b128(v, rout, a.out_org + (uint32_t)((int64_t)y * a.out_pitch) + (uint32_t)cb,
+                                             0, kNtAux);
+  };
+  // start: own first R rows (shared with the neighbour beside the start
+  // boundary, an inner one for every wave but... all: waves 0/1 and 2/3 meet at
+  // their start boundaries) -> LDS; the start halo comes from the neighbour
+  u32x4 acc = {0, 0, 0, 0};
+  u32x4 r[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r[i] = ld(row(i));
+#pragma unroll
+  for (int i = 0; i < R; ++i) edge[wave][i][lane] = r[i];
+  __syncthreads();
+  const int nb = wave ^ 1;  // the wave across the start boundary
+#pragma unroll
+  for (int i = 0; i < R; ++i) acc ^= edge[nb][i][lane];
+  for (int i = 0; i < BAND; i += 4) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const u32x4 v = r[j];
+      if (i + j + 4 < BAND) r[j] = ld(row(i + j + 4));
+      acc ^= v;
+      st(row(i + j), v);
+      if (i + j >= BAND - R) edge[wave][R + (i + j - (BAND - R))][lane] = v;  // last R own rows
+    }
+  }
+  // end: the boundary at the walk's end -- inner between waves 1 / 2, outer
+  // (read twice) for waves 0 and 3
+  __syncthreads();
+  if (wave == 1 || wave == 2) {
+    const int ne = wave == 1 ? 2 : 1;
+#pragma unroll
+    for (int i = 0; i < R; ++i) acc ^= edge[ne][R + i][lane];
+  } else {
+#pragma unroll
+    for (int i = 0; i < R; ++i) acc ^= ld(up ? y0 - 1 - i : y0 + BAND + i);
+  }
+  if (acc.x == 0x12345678u && acc.y == 0x9abcdef0u) st(y0, acc);  // keeps the reads live
+}
+
 struct LdsCfg {
   int ns, rpw, cap;
 };
@@ -285,6 +350,28 @@ static void launch_sep(const SepCfg& c, const Frame& f, hipStream_t s, uint32_t*
   }
   if (grid_out) *grid_out = (int)grid.x;
   fn<<<grid, c.nw * kW, dyn, s>>>(a);
+}
+
+static void launch_pairs(int band, const Frame& f, hipStream_t s) {
+  KArgs a{};
+  a.in = f.in + g_org;
+  a.out = f.out + g_org;
+  a.in_pitch = a.out_pitch = g_pitch;
+  a.W = g_W;
+  a.E = g_W * g_C;
+  a.rows = g_rows;
+  a.Hg = g_rows;
+  a.in_base = f.in;
+  a.out_base = f.out;
+  a.in_bytes = a.out_bytes = (uint32_t)g_bytes;
+  a.in_org = a.out_org = (uint32_t)g_org;
+  a.in_zero = kMarginBytes;
+  a.ry0 = 0;
+  a.ry1 = g_rows;
+  a.ntx = (int)div_up(a.E, 1024);
+  void (*fn)(KArgs) = band == 8 ? k_band_pairs<2, 8> : band == 12 ? k_band_pairs<2, 12> : k_band_pairs<2, 16>;
+  const int64_t grid = (int64_t)a.ntx * div_up(g_rows, 4 * band);
+  fn<<<dim3((unsigned)grid), 256, nt_lds_reserve((const void*)fn, 2), s>>>(a);
 }
 
 static void launch_lds(const LdsCfg& c, const Frame& f, hipStream_t s) {
@@ -543,6 +630,12 @@ int main(int argc, char** argv) {
     }
     const PatCfg c0{16, 4, 8, 2, 0};
     report("pattern halo=0 band= 8 (band walk, cap 2)", [&](const Frame& f, hipStream_t s) { launch_pat(c0, f, s); });
+    for (int band : {8, 12, 16}) {
+      char name[96];
+      std::snprintf(name, sizeof name, "pairs halo=2 band=%2d (4 stacked walks, LDS-swapped boundaries, cap 2)", band);
+      report(name, [&](const Frame& f, hipStream_t s) { launch_pairs(band, f, s); });
+    }
+    if (std::getenv("SEPX_PAIRS_ONLY")) return 0;
     for (auto sr : std::vector<std::pair<int, int>>{{4, 2}, {4, 4}, {4, 8}, {8, 2}, {8, 4}, {16, 2}})
       for (int cap : {0, 2, 4, 8}) {
         const int waves = cap * sr.first;
