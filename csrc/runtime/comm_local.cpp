@@ -44,6 +44,8 @@ struct Msg {
   hipEvent_t done = nullptr;   // recorded on the receiver's stream after the copy
   bool own_done = false;       // `done` created by a receiver on another device
   bool consumed = false;
+  hipStream_t ready_stream = nullptr;  // the sender's stream `ready` was recorded on
+  hipStream_t copy_stream = nullptr;   // the receiver's stream the copy (and `done`) went on
 };
 
 class LocalHub {
@@ -287,6 +289,7 @@ class LocalComm final : public Comm {
       }
       m->done = take_event();
       group_events_.push_back(m->done);
+      m->ready_stream = s;
     }
     hub_->post(rank_, peer, m);
     sends_.push_back({m, peer, s});
@@ -381,6 +384,7 @@ class LocalComm final : public Comm {
         // pointer lookups contend between the rank threads)
         std::vector<std::shared_ptr<Msg>> got;
         got.reserve(recvs_.size());
+        heard_.clear();
         for (auto& r : recvs_) {
           got.push_back(hub_->take(r.peer, rank_));
           STRIPE_CHECK(got.back()->bytes == r.bytes, "size mismatch: rank " << r.peer << " sent " << got.back()->bytes
@@ -414,6 +418,8 @@ class LocalComm final : public Comm {
               m->own_done = true;
             }
             HIP_CHECK(hipEventRecord(m->done, s));  // the sender's pooled event, same device
+            m->copy_stream = s;
+            heard_.push_back({recvs_[k].peer, m->ready_stream, s});
           }
           i = j;
         }
@@ -428,7 +434,8 @@ class LocalComm final : public Comm {
         }
       }
       recvs_.clear();
-      settle_lazy();  // the previous lazy group's sends, before this group's buffers are written
+      settle_lazy(true);  // the previous lazy group's sends, before this group's buffers are written
+      heard_.clear();
       if (lazy_next_) {
         lazy_next_ = false;
         lazy_sends_.swap(sends_);
@@ -445,11 +452,13 @@ class LocalComm final : public Comm {
   // A group's sends are complete once each peer has taken its message (host)
   // and the stream has a wait on the peer's copy (device); then every wait on
   // the group's events is enqueued and they may be re-recorded.
-  void complete_sends(std::vector<PendingSend>& sends, std::vector<hipEvent_t>& events) {
+  // implied: skip the stream wait on a copy the stream is already ordered
+  // after (a lazy group's sends, settled by the next group; heard_).
+  void complete_sends(std::vector<PendingSend>& sends, std::vector<hipEvent_t>& events, bool implied = false) {
     for (auto& sd : sends) {
       hub_->wait_consumed(sd.m, sd.peer);
       if (hub_->device()) {
-        HIP_CHECK(hipStreamWaitEvent(sd.s, sd.m->done, 0));
+        if (!(implied && ordered_after_copy(sd))) HIP_CHECK(hipStreamWaitEvent(sd.s, sd.m->done, 0));
         if (sd.m->own_done) HIP_CHECK(hipEventDestroy(sd.m->done));
       }
     }
@@ -457,8 +466,23 @@ class LocalComm final : public Comm {
     free_events_.insert(free_events_.end(), events.begin(), events.end());
     events.clear();
   }
-  void settle_lazy() {
-    if (!lazy_sends_.empty() || !lazy_events_.empty()) complete_sends(lazy_sends_, lazy_events_);
+  // The peer copied a lazy send on the stream that then recorded the `ready`
+  // of its next message to this rank, and this group waited on that `ready`
+  // on the send's stream: the copy is done before anything later on it (a
+  // serial halo exchange, where every step both sends to and receives from
+  // each neighbour: 2 stream waits a rank and step fewer).
+  bool ordered_after_copy(const PendingSend& sd) const {
+    static const bool on = [] {  // STUDY: STRIPE_LOCAL_IMPLIED=0 keeps every wait (A/B)
+      const char* e = std::getenv("STRIPE_LOCAL_IMPLIED");
+      return !(e && std::atoi(e) == 0);
+    }();
+    if (!on) return false;
+    for (const Heard& h : heard_)
+      if (h.peer == sd.peer && h.ready_stream == sd.m->copy_stream && h.our_stream == sd.s) return true;
+    return false;
+  }
+  void settle_lazy(bool implied = false) {
+    if (!lazy_sends_.empty() || !lazy_events_.empty()) complete_sends(lazy_sends_, lazy_events_, implied);
   }
 
  public:
@@ -497,6 +521,7 @@ class LocalComm final : public Comm {
     sends_.clear();
     lazy_sends_.clear();
     recvs_.clear();
+    heard_.clear();
     in_group_ = false;
     lazy_next_ = false;
   }
@@ -511,6 +536,11 @@ class LocalComm final : public Comm {
   bool lazy_next_ = false;                // hint_lazy_sends: the next group completes its sends lazily
   std::vector<PendingSend> lazy_sends_;   // a lazy group's sends, completed by the next group / flush_sends
   std::vector<hipEvent_t> lazy_events_;   // and their events
+  struct Heard {  // a receive of the open group: its peer, the peer's `ready` stream, ours
+    int peer;
+    hipStream_t ready_stream, our_stream;
+  };
+  std::vector<Heard> heard_;
 };
 
 class CallbackComm final : public Comm {

@@ -143,6 +143,23 @@ local2)
     done
   done
   ;;
+local4)
+  # the `local` hub's lazy sends with the send-completion waits a serial
+  # exchange implies skipped (default) vs kept (STRIPE_LOCAL_IMPLIED=0) vs the
+  # eager form (STRIPE_LOCAL_LAZY=0), alternating: the local-rank tests, then
+  # 4 ranks on 8192^2 gray sobel at depth 1 and at the automatic depth
+  timeout -k 10 900 python -u -m pytest tests/test_r6_margins.py tests/test_r6_local.py tests/test_gpu_engine.py tests/test_dist_pipelined.py tests/test_deep_halo.py tests/test_advice_r2.py tests/test_weighted_split.py tests/test_n8.py tests/test_multi_gpu.py tests/test_resilience.py -m gpu -q -x --timeout 200 --timeout-method thread > $O/tests.txt 2>&1 || exit 2
+  CFG3="bin/stripe bench --synthetic 8192x8192x1 --chain sobel --ranks 4 --iters 64 --warmup 8 --scope resident --backend local"
+  for r in 1 2 3; do
+    for v in implied kept eager; do
+      case $v in implied) E="" ;; kept) E="STRIPE_LOCAL_IMPLIED=0" ;; eager) E="STRIPE_LOCAL_LAZY=0" ;; esac
+      echo "$v depth 1" >> $O/cfg3_depth1.txt
+      env $E timeout -k 10 120 $CFG3 --halo-depth 1 2>&1 | grep -v amdgpu.ids >> $O/cfg3_depth1.txt || exit 3
+    done
+    echo "implied depth auto" >> $O/cfg3_auto.txt
+    timeout -k 10 120 $CFG3 2>&1 | grep -v amdgpu.ids >> $O/cfg3_auto.txt || exit 3
+  done
+  ;;
 pairs)
   # paired band walks (task order 2, k_sep_pairs, removed after this study
   # with tests/test_r6_pairs.py): GPU tests, then the
