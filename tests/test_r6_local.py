@@ -75,3 +75,26 @@ def test_host_local_group_unchanged():
     img = C.synth_rows(9, 120, 3, 0, 77)
     out = np.asarray(m.models.Pipeline("gaussian5", halo_depth=1).run_distributed(img, 3, "host", 2))
     assert np.array_equal(out.reshape(img.shape), _golden(img, "gaussian5", 2))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chain,cc", [("gaussian5,invert,gaussian3", 3), ("sobel,brightness:10,gaussian3", 1),
+                                      ("blur:9,invert", 3)])
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_local_lazy_sends_mixed_passes_gpu(monkeypatch, chain, cc, ranks):
+    # per-pass serial exchanges (STRIPE_DEEP=0; blur has no chain-level halo
+    # anyway) complete their sends lazily, at the next pass's exchange; a
+    # pointwise pass between two stencils has no exchange and writes the rows
+    # the previous pass sent, so it must complete them first (flush_sends).
+    # Stitched output == golden, iterated
+    monkeypatch.setenv("STRIPE_DEEP", "0")
+    monkeypatch.setenv("STRIPE_HALO_SCHEDULE", "serial")
+    W, H, it = 333, 203, 3
+    img = C.synth_rows(17, W, cc, 0, H)
+    if cc == 1:
+        img = img.reshape(H, W)
+    out = np.asarray(m.models.Pipeline(chain, halo_depth=1).run_distributed(img, ranks, "local", it))
+    ref = _golden(img, chain, it)
+    tol = 1 if chain.startswith("blur") else 0
+    d = np.abs(out.reshape(ref.shape).astype(np.int16) - ref.astype(np.int16))
+    assert d.max() <= tol, (chain, ranks, int(d.max()), np.argwhere(d > tol)[:4])
