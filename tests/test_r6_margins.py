@@ -1,6 +1,6 @@
 """Output x-margins when the row's last wave tile is short.
 
-The stencil kernels (k_sep, k_sep_st, k_direct, k_sobel_rp) keep each output
+The stencil kernels (k_sep, k_direct, k_sobel_rp) keep each output
 row's x-margins (the border extension the next pass reads) up to date after
 every band: the row's edge tiles rewrite them.  Until round 6 a last tile
 holding fewer than px + 1 pixels copied pixels the tile before it had stored:

@@ -99,6 +99,7 @@ def common_flags() -> list[str]:
         f"-I{CSRC / 'include'}",
         f"-I{CSRC / 'hip'}",
         "-I/opt/rocm/include",
+        *os.environ.get("STRIPE_EXTRA_CFLAGS", "").split(),  # study builds (e.g. -DSTRIPE_DIRECT_GRAY_PF=1)
     ]
 
 

@@ -143,6 +143,21 @@ local2)
     done
   done
   ;;
+graypf)
+  # gray-prologue direct stencils (the reference pipeline): rows in flight 2K
+  # (default build) vs K (build_alt1, -DSTRIPE_DIRECT_GRAY_PF=1), alternating;
+  # GPU tests of the kernels first
+  timeout -k 10 900 python -u -m pytest tests/test_gpu_kernels.py tests/test_r6_margins.py tests/test_r5_order.py -m gpu -q -x --timeout 200 --timeout-method thread > $O/tests.txt 2>&1 || exit 2
+  PK="import sys; sys.path.insert(0, sys.argv[1]); import mpi_cuda_imagemanipulation_amd as m, runpy; print('package', m._C.__file__, file=sys.stderr); sys.argv = sys.argv[2:]; runpy.run_path(sys.argv[0], run_name='__main__')"
+  CH="gray:ref,contrast:3.5,emboss3@skip,expand|gray:ref,contrast:3.5,emboss3@skip|gray,sharpen"
+  for r in 1 2 3; do
+    for v in 2 1; do
+      P=.; [ $v = 1 ] && P=build_alt1
+      timeout -k 10 300 python -c "$PK" $P tools/kbench.py --chains "$CH" --shape 16384x16384x3 --iters 30 >> $O/k16_pf$v.json 2>> $O/k16_pf$v.err || exit 3
+      timeout -k 10 300 python -c "$PK" $P tools/kbench.py --chains "$CH" --shape 16384x2048x3 --iters 100 >> $O/kshare_pf$v.json 2>> $O/kshare_pf$v.err || exit 3
+    done
+  done
+  ;;
 local4)
   # the `local` hub's lazy sends with the send-completion waits a serial
   # exchange implies skipped (default) vs kept (STRIPE_LOCAL_IMPLIED=0) vs the
