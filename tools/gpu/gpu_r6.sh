@@ -143,6 +143,14 @@ local2)
     done
   done
   ;;
+rehearse)
+  # the driver's multi-GPU bench command on the final sources, as processes
+  # sharing the one GPU (gloo-gpu transport; RCCL needs a GPU per rank): N = 2
+  # and 4, the full record (tune, schedule probe, every scope)
+  for n in 2 4; do
+    timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29600 + n)) bench.py --gpus $n --backend gloo-gpu --steps 20 --warmup 5 > $O/bench_16k_n$n.json 2> $O/bench_16k_n$n.err || exit 2
+  done
+  ;;
 graypf)
   # gray-prologue direct stencils (the reference pipeline): rows in flight 2K
   # (default build) vs K (build_alt1, -DSTRIPE_DIRECT_GRAY_PF=1), alternating;
